@@ -1,0 +1,627 @@
+"""ORACLE -- TEST INFRASTRUCTURE, NOT PRODUCT CODE.
+
+CPU restatement (Python + numpy) of the reference `waafle_orgscorer` contig-scoring
+path (menickname/waafle v0.1.0).  It exists only to check the HIP path:
+
+* only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may
+  import it, and only as the checker / the timed CPU baseline -- never as a
+  fallback for the product path (`waafle_amd/`), which fails loudly without its
+  HIP library;
+* parity of THIS file is pinned against (a) golden TSVs produced by running the
+  reference itself in the build container (`tests/golden/make_golden.py`, demo
+  inputs x a flag matrix, seeded synthetic sets, quirk cases) and (b) the
+  reference's own shipped demo goldens (`demo/output*/`), which were written by an
+  older version and match with `--sister-penalty off --ambiguous-threshold strict`
+  at 3 decimals.  See `tests/test_oracle_golden.py`.
+
+Every function cites the reference file:line it restates (paths relative to the
+reference checkout).  numpy is used for the same array operations the reference
+uses (`np.maximum` slices, `np.mean`, `np.min`), so float64 results are bit-exact
+with it by construction.
+
+One deliberate, documented difference: the reference iterates the clades of a
+contig from a Python `set` (`orgscorer.py:587,603`), so on EXACT rank ties its
+output depends on PYTHONHASHSEED.  This oracle iterates clades in sorted
+(code-point) name order -- one of the orders a set may legally produce -- which is
+the deterministic tie policy the HIP path implements too.  The golden generator
+runs the reference under that same order (a sorted-iteration set) and under raw
+hash seeds, and flags contigs whose outputs differ between seeds.
+"""
+
+from __future__ import annotations
+
+import csv
+import os
+import re
+from collections import OrderedDict
+
+import numpy as np
+
+C_EPS = 1e-6                        # orgscorer.py:58
+UNKNOWN = "Unknown"                 # utils.py:367
+ROOT = "r__Root"                    # utils.py:368
+ANNOT_PREFIX = "ANNOTATIONS:"       # orgscorer.py:60
+MISSING_ANNOT = "None"              # orgscorer.py:61
+
+# output column layouts, orgscorer.py:76-114
+FORMATS = {
+    "lgt": ["contig_name", "call", "contig_length", "min_max_score", "avg_max_score",
+            "synteny", "direction", "clade_A", "clade_B", "lca", "melded_A",
+            "melded_B", "taxonomy_A", "taxonomy_B", "loci"],
+    "no_lgt": ["contig_name", "call", "contig_length", "min_score", "avg_score",
+               "synteny", "clade", "melded", "taxonomy", "loci"],
+    "unclassified": ["contig_name", "call", "contig_length", "loci"],
+}
+
+BLAST_FIELDS = [  # utils.py:167-183
+    ("qseqid", str), ("sseqid", str), ("qlen", int), ("slen", int), ("length", int),
+    ("qstart", int), ("qend", int), ("sstart", int), ("send", int), ("pident", float),
+    ("positive", int), ("gaps", int), ("evalue", float), ("bitscore", float),
+    ("sstrand", str),
+]
+GFF_FIELDS = [  # utils.py:282-292
+    ("seqname", str), ("source", str), ("feature", str), ("start", int), ("end", int),
+    ("score", float), ("strand", str), ("frame", str), ("attribute", str),
+]
+
+
+class OracleError(RuntimeError):
+    """Stands in for the reference's `die()` (utils.py:49-52)."""
+
+
+# ---------------------------------------------------------------------------
+# parameters: orgscorer.py:135-303 + genecaller.py:81-101 (shared args)
+# ---------------------------------------------------------------------------
+
+DEFAULTS = dict(
+    one_clade_threshold=0.5, two_clade_threshold=0.8, disambiguate_one="meld",
+    disambiguate_two="meld", range=0.05, jump_taxonomy=None, allow_lca=False,
+    ambiguous_fraction=0.1, ambiguous_threshold="lenient", sister_penalty="strict",
+    clade_genes=None, clade_leaves=None, weak_loci="ignore",
+    annotation_threshold="lenient", min_overlap=0.1, min_gene_length=200.0,
+    min_scov=0.75, stranded=False,
+)
+
+
+class Params:
+    def __init__(self, **kw):
+        vals = dict(DEFAULTS)
+        for k, v in kw.items():
+            if k not in vals:
+                raise KeyError(k)
+            vals[k] = v
+        self.__dict__.update(vals)
+        self.k1 = float(self.one_clade_threshold)
+        self.k2 = float(self.two_clade_threshold)
+        self.kmin = min(self.k1, self.k2)            # orgscorer.py:338
+        self.kmax = max(self.k1, self.k2)            # orgscorer.py:339
+        self.annot_ref = {"off": C_EPS, "lenient": self.kmin,  # orgscorer.py:341-346
+                          "strict": self.kmax}[self.annotation_threshold]
+
+
+# ---------------------------------------------------------------------------
+# inputs (utils.py)
+# ---------------------------------------------------------------------------
+
+def fasta_lengths(path):
+    """utils.py:109-120: header = first token after '>', length = sum of stripped lines."""
+    out = OrderedDict()
+    name = None
+    with open(path) as fh:
+        for raw in fh:
+            line = raw.strip()
+            if line[0] == ">":          # a blank line raises IndexError, as upstream
+                name = line[1:].split()[0]
+                out[name] = 0
+            else:
+                out[name] += len(line)
+    return out
+
+
+class BlastHit:
+    """utils.py:207-241 -- one tabular BLAST row and its derived values."""
+    __slots__ = [f for f, _ in BLAST_FIELDS] + [
+        "strand", "scov_mod", "score", "taxon", "annotations", "order"]
+
+    def __init__(self, row, order=0):
+        if len(row) != len(BLAST_FIELDS):
+            raise OracleError("inconsistent blast row: {}".format(row))
+        for (name, cast), raw in zip(BLAST_FIELDS, row):
+            setattr(self, name, cast(raw))
+        self.strand = "-" if self.sstrand == "minus" else "+"          # :214
+        # :216-217 (scov/qcov are computed upstream; division errors included)
+        (abs(self.send - self.sstart) + 1) / float(self.slen)
+        (abs(self.qend - self.qstart) + 1) / float(self.qlen)
+        if self.strand == "-":                                          # :219-224
+            s0, s1 = self.slen - self.sstart + 1, self.slen - self.send + 1
+        else:
+            s0, s1 = self.sstart, self.send
+        left = max(0, s0 - self.qstart)                                 # :225
+        right = max(0, self.slen - s0 - self.qlen + self.qstart)        # :226
+        self.scov_mod = (s1 - s0 + 1) / float(self.slen - left - right)  # :227
+        self.score = self.scov_mod * self.pident / 100.0                # :229
+        parts = self.sseqid.split("|")                                  # :231-241
+        if len(parts) < 2:
+            raise OracleError("bad subject id header: " + self.sseqid)
+        self.taxon = parts[1]
+        self.annotations = {}
+        for item in parts[2:]:
+            system, value = item.split("=")
+            self.annotations[system] = value
+        self.order = order
+
+
+def _tsv_rows(path):
+    with open(path) as fh:
+        for row in csv.reader(fh, dialect="excel-tab"):
+            yield row
+
+
+def blast_groups(path):
+    """utils.py:255-270: consecutive rows sharing qseqid form one group."""
+    name, group = None, []
+    for i, row in enumerate(_tsv_rows(path)):
+        hit = BlastHit(row, i)
+        if name is not None and hit.qseqid != name:
+            yield name, group
+            group = []
+        name = hit.qseqid
+        group.append(hit)
+    yield name, group
+
+
+class GeneLocus:
+    """utils.py:298-322 (annotations from the GFF are never attached by orgscorer,
+    orgscorer.py:920)."""
+
+    def __init__(self, row):
+        if len(row) != len(GFF_FIELDS):
+            raise OracleError("Bad GFF row: {}".format(row))
+        for (name, cast), raw in zip(GFF_FIELDS, row):
+            setattr(self, name, cast(raw) if raw != "." else raw)
+        self.code = "{}:{}:{}".format(self.start, self.end, self.strand)
+        self.annotations = {}
+        self.annotation_scores = {}
+        self.ignore = False
+        self.name = None
+
+    def __len__(self):
+        return abs(self.end - self.start) + 1
+
+
+def gff_groups(path):
+    """utils.py:341-355: '#'-rows skipped; consecutive seqname groups."""
+    name, group = None, []
+    for row in _tsv_rows(path):
+        if row[0][0] == "#":
+            continue
+        loc = GeneLocus(row)
+        if name is not None and loc.seqname != name:
+            yield name, group
+            group = []
+        name = loc.seqname
+        group.append(loc)
+    yield name, group
+
+
+class Taxonomy:
+    """utils.py:374-447 (parent map, lineage, LCA, tails, sisters, leaf counts)."""
+
+    def __init__(self, edges):
+        self.parents = {}
+        self.children = {}
+        for child, parent in edges:
+            self.parents[child] = parent
+            self.children.setdefault(parent, set()).add(child)
+        self._leaves = {}
+
+    @classmethod
+    def from_file(cls, path):
+        return cls([(c, p) for c, p in _tsv_rows(path)])
+
+    def parent(self, clade):                      # :386-387
+        return self.parents.get(clade, ROOT)
+
+    def lineage(self, clade):                     # :392-399 (root first)
+        path = [clade]
+        while path[-1] != ROOT:
+            path.append(self.parent(path[-1]))
+        return path[::-1]
+
+    def lca(self, clades):                        # :401-411
+        paths = [self.lineage(c) for c in clades]
+        best = ROOT
+        for level in zip(*paths):
+            if len(set(level)) != 1:
+                break
+            best = level[0]
+        return best
+
+    def tails(self, clades, lca):                 # :413-426
+        out = []
+        for c in clades:
+            path = self.lineage(c)
+            if lca in path:
+                path = path[len(path) - path[::-1].index(lca):]
+            out.append(path)
+        return out
+
+    def sisters(self, clade):                     # :428-434
+        return self.children.get(self.parent(clade), set()) - {clade}
+
+    def leaf_count(self, clade):                  # :436-447
+        if clade not in self._leaves:
+            kids = self.children.get(clade)
+            self._leaves[clade] = 1 if kids is None else sum(self.leaf_count(k) for k in kids)
+        return self._leaves[clade]
+
+
+def overlap_fraction(a1, a2, b1, b2):
+    """utils.py:487-500 (normalised by the shorter interval; int 0 when disjoint)."""
+    a1, a2 = min(a1, a2), max(a1, a2)
+    b1, b2 = min(b1, b2), max(b1, b2)
+    if b1 > a2 or a1 > b2:
+        return 0
+    return (min(a2, b2) - max(a1, b1) + 1) / float(min(a2 - a1 + 1, b2 - b1 + 1))
+
+
+# ---------------------------------------------------------------------------
+# per-contig model (orgscorer.py:309-461)
+# ---------------------------------------------------------------------------
+
+class Explanation:
+    """orgscorer.py:467-493 (an option)."""
+
+    def __init__(self, crit, rank, c1, c2=None):
+        self.ok = True
+        self.crit, self.rank = crit, rank
+        self.clade1, self.clade2 = c1, c2
+        self.synteny = None
+        self.direction = "A?B"
+        self.donor = self.recip = None
+        self.tails1, self.tails2 = [], []
+
+
+def _ordered(clades):
+    """Deterministic stand-in for set iteration (see module docstring)."""
+    return sorted(clades)
+
+
+class ContigModel:
+
+    def __init__(self, name, length, params):
+        self.name = name
+        self.length = length
+        self.p = params
+        self.loci = []          # kept loci in GFF order (orgscorer.py:350-352)
+        self.sites = {}         # clade -> {locus index -> float64 site array}
+        self.genes = {}         # clade -> float64 per-locus scores
+        self.mask = None
+        self.clades = set()
+        self.best_one = None
+        self.best_two = None
+        self.iterations = 0
+        self.pair_evals = 0
+
+    def add_loci(self, loci):
+        """orgscorer.py:348-357 (names by start rank over ALL loci of the group)."""
+        for L in loci:
+            if len(L) >= self.p.min_gene_length:
+                self.loci.append(L)
+        for rank, L in enumerate(sorted(loci, key=lambda x: x.start)):
+            L.name = str(rank + 1)
+
+    def add_hits(self, hits):
+        """orgscorer.py:359-392 (+ hit_locus_overlap :559-564)."""
+        p = self.p
+        for h in hits:
+            if not h.scov_mod >= p.min_scov:
+                continue
+            for gi, L in enumerate(self.loci):
+                if p.stranded and h.strand != L.strand:
+                    continue
+                if overlap_fraction(h.qstart, h.qend, L.start, L.end) >= p.min_overlap:
+                    self._paint(h, gi, L)
+        self.clades = set(self.sites)
+
+    def _paint(self, h, gi, L):
+        lo = min(L.start, L.end)
+        first = max(0, min(h.qstart, h.qend) - lo)
+        last = min(len(L) - 1, max(h.qstart, h.qend) - lo)
+        per = self.sites.setdefault(h.taxon, {})
+        if gi not in per:
+            per[gi] = np.zeros(len(L))
+        seg = per[gi][first:last + 1]             # python slice semantics (wraps if last < -1)
+        per[gi][first:last + 1] = np.maximum(seg, h.score)
+        for system, value in h.annotations.items():   # :384-392
+            ref = L.annotation_scores.get(system, self.p.annot_ref)
+            if ref is None:
+                continue
+            if h.score >= ref:
+                L.annotations[system] = value
+                L.annotation_scores[system] = h.score
+
+    def refresh(self):
+        """orgscorer.py:394-429 (gene scores = np.mean of site arrays; weak loci)."""
+        G = len(self.loci)
+        self.genes = {}
+        for clade, per in self.sites.items():
+            self.genes[clade] = np.array(
+                [np.mean(per[g]) if g in per else 0 for g in range(G)])
+        top = np.zeros(G)
+        for clade, row in self.genes.items():
+            if clade != UNKNOWN:
+                top = np.maximum(top, row)
+        mode = self.p.weak_loci
+        if mode == "assign-unknown":
+            self.genes[UNKNOWN] = 1 - top
+            self.clades.add(UNKNOWN)
+        elif mode == "ignore":
+            keep = []
+            for g, v in enumerate(top):
+                self.loci[g].ignore = not (v >= self.p.kmin)
+                if not self.loci[g].ignore:
+                    keep.append(g)
+            self.mask = None if len(keep) == G else np.array(keep)
+        self.clades = set(self.genes)
+
+    def raise_level(self, tax):
+        """orgscorer.py:431-445 (site arrays re-keyed to parents, merged by max)."""
+        merged = {}
+        for clade, per in self.sites.items():
+            dest = merged.setdefault(tax.parent(clade), {})
+            for g, arr in per.items():
+                dest[g] = arr.copy() if g not in dest else np.maximum(dest[g], arr)
+        self.sites = merged
+        self.refresh()
+
+    def evaluate(self, c1, c2=None):
+        """orgscorer.py:447-461: (min, mean) of the (pairwise max) masked scores."""
+        row = self.genes[c1]
+        if c2 is not None:
+            row = np.maximum(row, self.genes[c2])
+        if self.mask is not None:
+            row = row[self.mask]
+        return np.min(row), np.mean(row)
+
+
+# ---------------------------------------------------------------------------
+# explanations, melds and LGT filters (orgscorer.py:495-744)
+# ---------------------------------------------------------------------------
+
+def synteny_one(C, opt):
+    """orgscorer.py:495-509."""
+    chars = []
+    for s, L in zip(C.genes[opt.clade1], C.loci):
+        chars.append("~" if L.ignore else ("A" if s >= C.p.k1 else "!"))
+    opt.synteny = "".join(chars)
+
+
+def synteny_two(C, opt):
+    """orgscorer.py:511-545 (incl. the literal donor/recip assignment at :542-545)."""
+    p = C.p
+    k_amb = {"off": C_EPS, "lenient": p.kmin, "strict": p.kmax}[p.ambiguous_threshold]
+    unknown = UNKNOWN in (opt.clade1, opt.clade2)
+    chars = []
+    for s1, s2, L in zip(C.genes[opt.clade1], C.genes[opt.clade2], C.loci):
+        if L.ignore:
+            chars.append("~")
+        elif min(s1, s2) >= k_amb and not unknown:
+            chars.append("*")
+        elif s1 >= p.k2:
+            chars.append("A")
+        elif s2 >= p.k2:
+            chars.append("B")
+        else:
+            chars.append("!")
+    syn = "".join(chars)
+    if re.search("^[^A]*B", syn):
+        opt.clade1, opt.clade2 = opt.clade2, opt.clade1
+        syn = syn.translate(str.maketrans("AB", "BA"))
+    opt.synteny = syn
+    if re.search("^A+B+A+$", syn.replace("~", "")):
+        opt.direction = "B>A"
+        opt.donor, opt.recip = opt.clade1, opt.clade2
+
+
+def one_clade(C, tax):
+    """orgscorer.py:585-597 + meld_one :621-631."""
+    p = C.p
+    opts = []
+    for clade in _ordered(C.clades):
+        crit, rank = C.evaluate(clade)
+        if crit >= p.k1:
+            o = Explanation(crit, rank, clade)
+            synteny_one(C, o)
+            opts.append(o)
+    if not opts:
+        return None
+    opts.sort(key=lambda o: o.rank)
+    best = opts[-1]
+    near = [o for o in opts if best.rank - o.rank <= p.range]
+    if p.disambiguate_one == "meld":
+        group = [o.clade1 for o in near]
+        best.clade1 = tax.lca(group)
+        best.tails1 = tax.tails(group, best.clade1)
+    return best
+
+
+def two_clade(C, tax):
+    """orgscorer.py:599-619 + meld_two :633-669."""
+    p = C.p
+    pool = [c for c in _ordered(C.clades) if max(C.genes[c]) >= p.k2]
+    C.pair_evals += len(pool) * (len(pool) - 1) // 2
+    opts = []
+    for a in pool:
+        for b in pool:
+            if a < b:
+                crit, rank = C.evaluate(a, b)
+                if crit >= p.k2:
+                    o = Explanation(crit, rank, a, b)
+                    synteny_two(C, o)
+                    opts.append(o)
+    if not opts:
+        return None
+    opts.sort(key=lambda o: o.rank)
+    best = opts[-1]
+    near = [o for o in opts if best.rank - o.rank <= p.range]
+    for o in near:
+        lgt_filters(C, o, tax)
+    if len(near) == 1 or p.disambiguate_two == "report-best":
+        return best
+    if p.disambiguate_two == "jump":
+        return None
+    if any(not o.ok or o.synteny != near[0].synteny for o in near):   # :671-676
+        return None
+    g1 = [o.clade1 for o in near]
+    g2 = [o.clade2 for o in near]
+    best.clade1 = tax.lca(g1)
+    best.clade2 = tax.lca(g2)
+    best.tails1 = tax.tails(g1, best.clade1)
+    best.tails2 = tax.tails(g2, best.clade2)
+    if not p.allow_lca and tax.lca([best.clade1, best.clade2]) in (best.clade1, best.clade2):
+        return None
+    return best
+
+
+def lgt_filters(C, o, tax):
+    """orgscorer.py:678-744 (ambiguous fraction, clade genes/leaves, sister penalty)."""
+    p = C.p
+    if p.ambiguous_fraction is not None:                                  # :693-702
+        total = amb = 0
+        for ch, L in zip(o.synteny, C.loci):
+            if ch in "AB*":
+                total += len(L)
+                if ch == "*":
+                    amb += len(L)
+        if amb / float(total) > p.ambiguous_fraction:
+            o.ok = False
+    if p.clade_genes is not None:                                         # :704-708
+        if min(o.synteny.count("A"), o.synteny.count("B")) < p.clade_genes:
+            o.ok = False
+    if p.clade_leaves is not None:                                        # :710-715
+        group = [o.recip] if o.recip is not None else [o.clade1, o.clade2]
+        if min(tax.leaf_count(c) for c in group) < p.clade_leaves:
+            o.ok = False
+    if p.sister_penalty != "off":                                         # :717-744
+        thr = {"lenient": p.kmax, "strict": p.kmin}[p.sister_penalty]
+        sis = {"B": tax.sisters(o.clade1) - {o.clade2},
+               "A": tax.sisters(o.clade2) - {o.clade1}}
+        flagged = {}
+        for i, ch in enumerate(o.synteny):
+            if ch not in sis:
+                continue
+            n = sum(1 for s in sis[ch] if s in C.genes and C.genes[s][i] >= thr)
+            frac = n / float(len(sis[ch])) if sis[ch] else n
+            flagged.setdefault(ch, []).append(frac)
+        worst = {ch: np.mean(v) for ch, v in flagged.items()}
+        if max(worst.get(ch, 0) for ch in ("B" if o.recip is not None else "AB")) > 0:
+            o.ok = False
+
+
+def _ok(o):
+    return o is not None and o.ok
+
+
+def evaluate_contig(C, tax):
+    """orgscorer.py:566-583 (roll-up loop; runaway guard at 100 iterations)."""
+    it = 1
+    one = one_clade(C, tax)
+    two = two_clade(C, tax) if not _ok(one) else None
+    while C.clades and ROOT not in C.clades and not _ok(one) and not _ok(two):
+        C.raise_level(tax)
+        one = one_clade(C, tax)
+        two = two_clade(C, tax) if not _ok(one) else None
+        it += 1
+        if it > 100:
+            raise OracleError("  Warning: Runaway taxonomic recursion for " + C.name)
+    C.best_one, C.best_two = one, two
+    C.iterations = it
+
+
+# ---------------------------------------------------------------------------
+# driver + writer (orgscorer.py:750-964, utils.py:122-143)
+# ---------------------------------------------------------------------------
+
+def score_contigs(lengths, loci_groups, hit_groups, tax, params, warn=None):
+    """orgscorer.py:900-960 without the file writing: returns {name: ContigModel}."""
+    contigs = OrderedDict()
+    for name, n in lengths.items():
+        contigs[name] = ContigModel(name, n, params)
+    for name, loci in loci_groups:
+        if name not in contigs:
+            if warn:
+                warn("  Unknown contig in <gff> file " + str(name))
+            continue
+        contigs[name].add_loci(loci)
+    for name, hits in hit_groups:
+        if name not in contigs:
+            if warn:
+                warn("  Unknown contig in <blastout> file " + str(name))
+            continue
+        C = contigs[name]
+        C.add_hits(hits)
+        C.refresh()
+        if params.jump_taxonomy is not None:
+            for _ in range(params.jump_taxonomy):
+                C.raise_level(tax)
+        if not all(L.ignore for L in C.loci):
+            evaluate_contig(C, tax)
+    return contigs
+
+
+def _tails_field(tails):                          # orgscorer.py:750-759
+    return "; ".join(sorted({"|".join(t) for t in tails if t}))
+
+
+def _fmt(v):                                      # utils.py:122-143
+    if isinstance(v, (float, np.floating)):
+        return "{:.4f}".format(v)
+    v = str(v)
+    return v if v != "" else "--"
+
+
+def render_rows(contigs, tax):
+    """orgscorer.py:814-894 -> {kind: [header, row, ...]} with rows as tab-joined str."""
+    systems = sorted({s for C in contigs.values() for L in C.loci for s in L.annotations})
+    out = {}
+    for kind, cols in FORMATS.items():
+        cols = cols + [ANNOT_PREFIX + s for s in systems]
+        out[kind] = ["\t".join(c.upper() for c in cols)]
+    for name in sorted(contigs):
+        C = contigs[name]
+        one, two = C.best_one, C.best_two
+        loci = "|".join(L.code for L in C.loci)
+        if not _ok(one) and not _ok(two):
+            kind, vals = "unclassified", [name, "unclassified", C.length, loci]
+        elif _ok(one):
+            kind = "no_lgt"
+            vals = [name, "no_lgt", C.length, one.crit, one.rank, one.synteny, one.clade1,
+                    _tails_field(one.tails1), "|".join(tax.lineage(one.clade1)), loci]
+        else:
+            kind = "lgt"
+            a, b = two.clade1, two.clade2
+            vals = [name, "lgt", C.length, two.crit, two.rank, two.synteny, two.direction,
+                    a, b, tax.lca([a, b]), _tails_field(two.tails1), _tails_field(two.tails2),
+                    "|".join(tax.lineage(a)), "|".join(tax.lineage(b)), loci]
+        for s in systems:
+            vals.append("|".join(L.annotations.get(s, MISSING_ANNOT) for L in C.loci))
+        out[kind].append("\t".join(_fmt(v) for v in vals))
+    return out
+
+
+def run(contigs_path, blastout_path, gff_path, taxonomy_path, params, warn=None):
+    """File-level entry point: returns ({name: ContigModel}, Taxonomy)."""
+    tax = Taxonomy.from_file(taxonomy_path)
+    lengths = fasta_lengths(contigs_path)
+    contigs = score_contigs(lengths, gff_groups(gff_path), blast_groups(blastout_path),
+                            tax, params, warn=warn)
+    return contigs, tax
+
+
+def write_outputs(contigs, tax, outdir, basename):
+    rows = render_rows(contigs, tax)
+    for kind, lines in rows.items():
+        with open(os.path.join(outdir, "{}.{}.tsv".format(basename, kind)), "w") as fh:
+            fh.write("\n".join(lines) + "\n")
+    return rows

@@ -1,0 +1,88 @@
+"""Loading committed golden fixtures and materialising their inputs (no reference access)."""
+import glob
+import gzip
+import json
+import os
+import shutil
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+DEMO_FILES = {
+    "homology": ["demo_contigs.fna", "demo_contigs.blastout", "demo_contigs.gff", "demo_taxonomy.tsv"],
+    "prodigal": ["demo_contigs.fna", "demo_contigs.blastout", "demo_contigs.prodigal.gff",
+                 "demo_taxonomy.tsv"],
+}
+
+
+def case_names():
+    return sorted(os.path.basename(p)[:-len(".json.gz")]
+                  for p in glob.glob(os.path.join(GOLDEN, "*.json.gz")))
+
+
+def load(name):
+    with gzip.open(os.path.join(GOLDEN, name + ".json.gz"), "rt") as fh:
+        return json.load(fh)
+
+
+def demo_file(fname, tmpdir):
+    dest = os.path.join(str(tmpdir), fname)
+    if not os.path.exists(dest):
+        with gzip.open(os.path.join(GOLDEN, "demo_inputs", fname + ".gz"), "rb") as src, \
+                open(dest, "wb") as out:
+            shutil.copyfileobj(src, out)
+    return dest
+
+
+def materialize(fixture, tmpdir):
+    """Return the 4 input paths (contigs, blastout, gff, taxonomy) for a fixture."""
+    recipe = fixture["recipe"]
+    if recipe["kind"] == "demo":
+        return [demo_file(f, tmpdir) for f in DEMO_FILES[recipe["gff"]]]
+    if recipe["kind"] == "files":
+        d = os.path.join(GOLDEN, recipe["dir"])
+        return [os.path.join(d, f) for f in
+                ("tie.fna", "tie.blastout", "tie.gff", "tie.taxonomy.tsv")]
+    from waafle_amd import synth
+    sub = os.path.join(str(tmpdir), "synth_" + "_".join(
+        "{}{}".format(k, v) for k, v in sorted(recipe["params"].items())))
+    paths = [os.path.join(sub, "synth" + e) for e in (".fna", ".blastout", ".gff", ".taxonomy.tsv")]
+    if not os.path.exists(paths[-1]):
+        synth.write_text(synth.generate(**recipe["params"]), sub, "synth")
+    return paths
+
+
+def rows_by_contig(texts):
+    out = {}
+    for kind, text in texts.items():
+        for line in text.splitlines()[1:]:
+            out[line.split("\t", 1)[0]] = (kind, line)
+    return out
+
+
+def headers(texts):
+    return {kind: text.splitlines()[0] for kind, text in texts.items()}
+
+
+def compare_tsv(fixture, texts):
+    """Compare produced TSV texts {kind: text} with a fixture; tie contigs may match any
+    of the reference's outcomes.  Returns a list of mismatch descriptions."""
+    bad = []
+    want_h, got_h = headers(fixture["tsv"]), headers(texts)
+    if want_h != got_h:
+        bad.append(("headers", want_h, got_h))
+    want, got = rows_by_contig(fixture["tsv"]), rows_by_contig(texts)
+    if set(want) != set(got):
+        bad.append(("contig set", sorted(set(want) ^ set(got))[:10]))
+    for contig, row in want.items():
+        g = got.get(contig)
+        if g == row:
+            continue
+        if contig in fixture["ties"] and g is not None and list(g) in fixture["alt_rows"].get(contig, []):
+            continue
+        bad.append((contig, row, g))
+    for kind, text in fixture["tsv"].items():   # row order (sorted contig names)
+        order_w = [l.split("\t", 1)[0] for l in text.splitlines()[1:]]
+        order_g = [l.split("\t", 1)[0] for l in texts[kind].splitlines()[1:]]
+        if order_w != order_g:
+            bad.append(("row order", kind))
+    return bad

@@ -1,0 +1,245 @@
+"""Seeded synthetic contig / hit / gene-call / taxonomy tables.
+
+Shapes follow SURVEY.md §8(d) (BASELINE.json configs 2-5).  Everything is generated
+as integer fields (pident in thousandths) so that the text rendering (BLAST
+`-outfmt 6` with the 15 WAAFLE columns, utils.py:167-184; GFF, utils.py:282-292;
+FASTA; 2-column taxonomy, utils.py:380) and the binary packing produce the SAME
+float64 scores: `pident_milli / 1000.0` is the correctly rounded value of the
+3-decimal string, exactly what `float("87.207")` returns.
+
+Taxonomy: r__Root -> 1 k -> 2 p -> 4 c -> C/48 o -> C/16 f -> C/4 g -> C s, plus
+1..3 t__ leaves per species (so leaf counts and sister sets are non-trivial).
+
+Per contig: G genes (length U[250,1500), gap U[5,150), strand +/-).  Each gene gets
+one full-length "owner" hit (pident U[85,100]) and D decoy hits from uniformly
+drawn clades (pident U[70,90], 5 % U[80,100]; coverage U[0.8,1.0) at a random
+offset).  A fraction `lgt_frac` of contigs carry a 2-gene run owned by a donor B.
+The stress shape (`stress=True`, config 5) instead gives every other clade one
+full-length hit on gene (clade mod G) with pident U(80.5,94.5), so ~C clades pass
+the k2 pre-filter and the all-pairs search runs over ~C^2/2 pairs per contig.
+"""
+
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+CONFIGS = {
+    # name: (N contigs, G genes, C clades, extra)
+    "demo": None,
+    "cfg2": dict(n=10_000, genes=8, clades=200),
+    "cfg3": dict(n=100_000, genes=12, clades=1000),
+    "cfg4": dict(n=1_000_000, genes=10, clades=2000),
+    "cfg5": dict(n=50_000, genes=20, clades=5000, stress=True),
+}
+
+
+@dataclass
+class SynthTaxonomy:
+    edges: list            # [(child, parent)] in file order
+    species: list          # species names, index = clade number
+
+
+@dataclass
+class SynthData:
+    tax: SynthTaxonomy
+    contig_names: list
+    contig_lengths: np.ndarray      # int64[N]
+    # loci (grouped by contig, GFF order)
+    loc_contig: np.ndarray          # int64[L]
+    loc_start: np.ndarray           # int64[L]
+    loc_end: np.ndarray             # int64[L]
+    loc_strand: np.ndarray          # uint8[L]  (ord('+') / ord('-'))
+    # hits (grouped by contig, sorted by qstart)
+    hit_contig: np.ndarray          # int64[H]
+    hit_clade: np.ndarray           # int64[H]  species index
+    hit_gene: np.ndarray            # int64[H]  gene index (for the subject id)
+    qlen: np.ndarray
+    slen: np.ndarray
+    length: np.ndarray
+    qstart: np.ndarray
+    qend: np.ndarray
+    sstart: np.ndarray
+    send: np.ndarray
+    pident_milli: np.ndarray        # int64, pident * 1000
+    minus: np.ndarray               # bool: sstrand == "minus"
+
+    @property
+    def n_contigs(self):
+        return len(self.contig_names)
+
+    @property
+    def n_hits(self):
+        return len(self.hit_contig)
+
+
+def make_taxonomy(n_clades, rng):
+    levels = [("k", 1), ("p", 2), ("c", 4), ("o", max(1, n_clades // 48)),
+              ("f", max(1, n_clades // 16)), ("g", max(1, n_clades // 4)), ("s", n_clades)]
+    edges = []
+    prev = ["r__Root"]
+    names_by_level = []
+    for tag, count in levels:
+        cur = ["{}__{}{}".format(tag, tag.upper(), i) for i in range(count)]
+        for i, name in enumerate(cur):
+            edges.append((name, prev[i * len(prev) // count]))
+        names_by_level.append(cur)
+        prev = cur
+    species = names_by_level[-1]
+    n_leaves = rng.integers(1, 4, size=n_clades)
+    for i, sp in enumerate(species):
+        for j in range(int(n_leaves[i])):
+            edges.append(("t__S{}_{}".format(i, j), sp))
+    return SynthTaxonomy(edges=edges, species=species)
+
+
+def _subject_coords(aligned, extra, minus):
+    """Subject coordinates for a fully aligned subject of length aligned+extra."""
+    slen = aligned + extra
+    sstart = np.where(minus, aligned, 1)
+    send = np.where(minus, 1, aligned)
+    return slen, sstart, send
+
+
+def generate(n, genes, clades, decoys=20, lgt_frac=0.10, seed=0, stress=False,
+             short_frac=0.0, name_prefix="contig"):
+    rng = np.random.default_rng(seed)
+    tax = make_taxonomy(clades, rng)
+    N, G = int(n), int(genes)
+
+    glen = rng.integers(250, 1500, size=(N, G))
+    if short_frac > 0:
+        short = rng.random((N, G)) < short_frac
+        glen = np.where(short, rng.integers(60, 200, size=(N, G)), glen)
+    gap = rng.integers(5, 150, size=(N, G))
+    gstart = np.cumsum(gap + np.concatenate([np.zeros((N, 1), np.int64), glen[:, :-1]], 1), 1) + 1
+    gend = gstart + glen - 1
+    gminus = rng.random((N, G)) < 0.5
+    clen = gend[:, -1] + rng.integers(0, 150, size=N)
+
+    owner = rng.integers(0, clades, size=N)
+    donor = (owner + rng.integers(1, clades, size=N)) % clades if clades > 1 else owner
+    has_lgt = np.ones(N, bool) if stress else rng.random(N) < lgt_frac
+    run0 = rng.integers(0, max(1, G - 1), size=N)
+    gidx = np.arange(G)[None, :]
+    in_run = has_lgt[:, None] & (gidx >= run0[:, None]) & (gidx < run0[:, None] + 2)
+
+    # owner hits: one per gene, full length
+    o_clade = np.where(in_run, donor[:, None], owner[:, None])
+    if stress:
+        o_pid = np.where(in_run, rng.integers(90_000, 100_001, size=(N, G)),
+                         rng.integers(85_000, 100_001, size=(N, G)))
+    else:
+        o_pid = rng.integers(85_000, 100_001, size=(N, G))
+    o_minus = rng.random((N, G)) < 0.5
+    o_slen, o_ss, o_se = _subject_coords(glen, rng.integers(0, 40, size=(N, G)), o_minus)
+    parts = [dict(contig=np.repeat(np.arange(N), G), clade=o_clade.ravel(),
+                  gene=np.tile(np.arange(G), N), qstart=gstart.ravel(), qend=gend.ravel(),
+                  length=glen.ravel(), slen=o_slen.ravel(), sstart=o_ss.ravel(),
+                  send=o_se.ravel(), pid=o_pid.ravel(), minus=o_minus.ravel())]
+
+    if stress:
+        # every other clade d: one full-length hit on gene d mod G
+        d = np.arange(clades)
+        per = []
+        for i in range(N):
+            keep = (d != owner[i]) & (d != donor[i] if has_lgt[i] else True)
+            dd = d[keep]
+            g = dd % G
+            per.append((np.full(len(dd), i), dd, g))
+        c_idx = np.concatenate([p[0] for p in per])
+        c_cl = np.concatenate([p[1] for p in per])
+        c_g = np.concatenate([p[2] for p in per])
+        L = glen[c_idx, c_g]
+        mi = rng.random(len(c_idx)) < 0.5
+        sl, ss, se = _subject_coords(L, rng.integers(0, 40, size=len(c_idx)), mi)
+        parts.append(dict(contig=c_idx, clade=c_cl, gene=c_g, qstart=gstart[c_idx, c_g],
+                          qend=gend[c_idx, c_g], length=L, slen=sl, sstart=ss, send=se,
+                          pid=rng.integers(80_501, 94_500, size=len(c_idx)), minus=mi))
+    elif decoys > 0:
+        M = N * G * decoys
+        c_idx = np.repeat(np.arange(N), G * decoys)
+        c_g = np.tile(np.repeat(np.arange(G), decoys), N)
+        L = glen[c_idx, c_g]
+        cov = rng.uniform(0.8, 1.0, size=M)
+        a = np.maximum(1, (cov * L).astype(np.int64))
+        off = (rng.random(M) * (L - a + 1)).astype(np.int64)
+        qs = gstart[c_idx, c_g] + off
+        hi = rng.random(M) < 0.05
+        pid = np.where(hi, rng.integers(80_000, 100_001, size=M), rng.integers(70_000, 90_001, size=M))
+        mi = rng.random(M) < 0.5
+        sl, ss, se = _subject_coords(a, rng.integers(0, 40, size=M), mi)
+        parts.append(dict(contig=c_idx, clade=rng.integers(0, clades, size=M), gene=c_g,
+                          qstart=qs, qend=qs + a - 1, length=a, slen=sl, sstart=ss, send=se,
+                          pid=pid, minus=mi))
+
+    cat = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    order = np.lexsort((cat["qstart"], cat["contig"]))
+    cat = {k: v[order] for k, v in cat.items()}
+
+    names = ["{}{}".format(name_prefix, i) for i in range(N)]
+    return SynthData(
+        tax=tax, contig_names=names, contig_lengths=clen.astype(np.int64),
+        loc_contig=np.repeat(np.arange(N), G), loc_start=gstart.ravel().astype(np.int64),
+        loc_end=gend.ravel().astype(np.int64),
+        loc_strand=np.where(gminus.ravel(), ord("-"), ord("+")).astype(np.uint8),
+        hit_contig=cat["contig"].astype(np.int64), hit_clade=cat["clade"].astype(np.int64),
+        hit_gene=cat["gene"].astype(np.int64), qlen=clen[cat["contig"]].astype(np.int64),
+        slen=cat["slen"].astype(np.int64), length=cat["length"].astype(np.int64),
+        qstart=cat["qstart"].astype(np.int64), qend=cat["qend"].astype(np.int64),
+        sstart=cat["sstart"].astype(np.int64), send=cat["send"].astype(np.int64),
+        pident_milli=cat["pid"].astype(np.int64), minus=cat["minus"].astype(bool))
+
+
+def generate_config(name, seed=None, n=None, **kw):
+    spec = dict(CONFIGS[name])
+    if n is not None:
+        spec["n"] = n
+    spec.update(kw)
+    return generate(seed=(int(name[-1]) if seed is None else seed), **spec)
+
+
+# ---------------------------------------------------------------------------
+# text rendering (the reference's on-disk formats)
+# ---------------------------------------------------------------------------
+
+def sseqids(data):
+    sp = data.tax.species
+    return ["GENE{}_{}|{}|UniProt=U{}x{}".format(c, g, sp[c], c, g % 50)
+            for c, g in zip(data.hit_clade.tolist(), data.hit_gene.tolist())]
+
+
+def write_text(data, outdir, basename="synth"):
+    """Write <basename>.fna / .blastout / .gff / .taxonomy.tsv; returns the 4 paths."""
+    os.makedirs(outdir, exist_ok=True)
+    paths = [os.path.join(outdir, basename + ext)
+             for ext in (".fna", ".blastout", ".gff", ".taxonomy.tsv")]
+    with open(paths[0], "w") as fh:
+        for name, n in zip(data.contig_names, data.contig_lengths.tolist()):
+            fh.write(">{}\n".format(name))
+            for i in range(0, n, 80):
+                fh.write("N" * min(80, n - i) + "\n")
+    names = data.contig_names
+    sids = sseqids(data)
+    pm = data.pident_milli
+    pid = ["{}.{:03d}".format(v // 1000, v % 1000) for v in pm.tolist()]
+    cols = [data.hit_contig.tolist(), sids, data.qlen.tolist(), data.slen.tolist(),
+            data.length.tolist(), data.qstart.tolist(), data.qend.tolist(),
+            data.sstart.tolist(), data.send.tolist(), pid,
+            ((data.length * pm) // 100_000).tolist(), data.minus.tolist()]
+    with open(paths[1], "w") as fh:
+        for (ci, sid, ql, sl, ln, qs, qe, ss, se, pi, pos, mi) in zip(*cols):
+            fh.write("{}\t{}\t{}\t{}\t{}\t{}\t{}\t{}\t{}\t{}\t{}\t0\t0.0\t{}\t{}\n".format(
+                names[ci], sid, ql, sl, ln, qs, qe, ss, se, pi, pos, ln * 2,
+                "minus" if mi else "plus"))
+    with open(paths[2], "w") as fh:
+        fh.write("##gff-version 3\n")
+        for ci, s, e, st in zip(data.loc_contig.tolist(), data.loc_start.tolist(),
+                                data.loc_end.tolist(), data.loc_strand.tolist()):
+            fh.write("{}\tsynth\tgene\t{}\t{}\t.\t{}\t0\t.\n".format(names[ci], s, e, chr(st)))
+    with open(paths[3], "w") as fh:
+        for child, parent in data.tax.edges:
+            fh.write("{}\t{}\n".format(child, parent))
+    return paths
