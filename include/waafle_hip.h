@@ -1,0 +1,152 @@
+/*
+ * waafle_hip.h -- C-ABI of libwaafle_hip.so, the MI355X (gfx950) implementation of the
+ * waafle_orgscorer contig-scoring hot path.
+ *
+ * The reference (menickname/waafle v0.1.0, pure Python + numpy) has no FFI; its
+ * in-process seam is the per-contig loop of `waafle/waafle_orgscorer.py:943-960`
+ * (attach_hits -> update_gene_scores -> [jump_taxonomy] -> evaluate_contig).  One
+ * wf_score() call replaces that loop for a whole batch of contigs.  The host side
+ * (Python, ctypes) parses the four input files, interns taxa, packs the flat arrays
+ * below and renders the three TSVs from the result records.
+ *
+ * Conventions: plain pointers + sizes, no ownership transfer (every buffer is owned by
+ * the caller and only borrowed for the duration of the call), 0 = success and a
+ * negative WF_E_* code otherwise with the message in wf_last_error(ctx), no exceptions
+ * and no exit() inside the library.  One wf_ctx per device; distinct contexts may be
+ * used from different host threads concurrently; a context is not re-entrant.
+ */
+#ifndef WAAFLE_HIP_H
+#define WAAFLE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WF_ABI_VERSION 1
+
+enum wf_status {
+  WF_OK = 0,
+  WF_E_BADINPUT = -1,  /* malformed arguments (sizes, null pointers, limits) */
+  WF_E_HIP = -2,       /* a HIP runtime call failed */
+  WF_E_RUNAWAY = -3,   /* > 100 roll-up iterations: orgscorer.py:580-581 */
+  WF_E_NOMEM = -4,     /* per-contig workspace too small (see wf_result.need_bytes) */
+  WF_E_STATE = -5,     /* call order (e.g. wf_score before wf_set_taxonomy) */
+  WF_E_EMPTYMASK = -6  /* every locus masked at a roll-up level (np.min of empty) */
+};
+
+enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
+
+typedef struct wf_ctx wf_ctx;
+
+/* Interned taxonomy.  Ids are the ranks of all names (taxonomy file names, hit taxa,
+ * "r__Root", "Unknown") in Python code-point order, so `clade1 < clade2`
+ * (orgscorer.py:608) is an integer compare.  Replaces utils.py:374-447. */
+typedef struct wf_taxonomy {
+  int32_t n;                  /* number of names */
+  const int32_t* parent;      /* [n] Taxonomy.get_parent (utils.py:386-387) */
+  const int32_t* depth;       /* [n] len(Taxonomy.get_lineage) - 1 (utils.py:392-399) */
+  const int32_t* sib_parent;  /* [n] parent the name is listed under as a child in the
+                                 taxonomy file (children map, utils.py:382), or -1 */
+  const int64_t* leaf_count;  /* [n] Taxonomy.get_leaf_count (utils.py:436-447) */
+  int32_t root;               /* id of "r__Root" (utils.py:368) */
+  int32_t unknown;            /* id of "Unknown" (utils.py:367) */
+} wf_taxonomy;
+
+/* orgscorer.py:135-303 + genecaller.py:81-101 (enums in the choice order shown). */
+typedef struct wf_params {
+  double k1;                  /* -k1 / --one-clade-threshold */
+  double k2;                  /* -k2 / --two-clade-threshold */
+  double range;               /* --range */
+  double min_overlap;         /* --min-overlap */
+  double min_scov;            /* --min-scov */
+  double ambiguous_fraction;  /* --ambiguous-fraction */
+  int32_t disambiguate_one;   /* 0 report-best, 1 meld */
+  int32_t disambiguate_two;   /* 0 report-best, 1 jump, 2 meld */
+  int32_t jump_taxonomy;      /* 0 = off (None) */
+  int32_t allow_lca;          /* --allow-lca */
+  int32_t ambiguous_threshold;/* 0 off, 1 lenient, 2 strict */
+  int32_t sister_penalty;     /* 0 off, 1 lenient, 2 strict */
+  int32_t clade_genes;        /* -1 = off (None) */
+  int32_t clade_leaves;       /* -1 = off (None) */
+  int32_t weak_loci;          /* 0 ignore, 1 penalize, 2 assign-unknown */
+  int32_t annotation_threshold; /* 0 off, 1 lenient, 2 strict */
+  int32_t stranded;           /* --stranded */
+} wf_params;
+
+/* A batch of contigs in CSR form.  Contig c owns hits [hit_off[c], hit_off[c+1]) in
+ * blastout file order (utils.py:255-270) and loci [loc_off[c], loc_off[c+1]) -- the
+ * loci that passed --min-gene-length, in GFF order (orgscorer.py:348-352). */
+typedef struct wf_batch {
+  int32_t n_contigs;
+  int32_t n_systems;          /* annotation systems (<= 32); bit s of hit_sysmask */
+  int64_t n_hits;
+  int64_t n_loci;
+  int32_t max_hits;           /* max hits of one contig (workspace sizing) */
+  int32_t max_loci;           /* max loci of one contig */
+  int32_t device_resident;    /* 1: all pointers (batch and result) are device memory
+                                 and wf_score only enqueues on the context stream;
+                                 0: host memory, wf_score copies and synchronises */
+  int32_t _pad;
+  const int64_t* hit_off;     /* [n_contigs+1] */
+  const int32_t* hit_qlo;     /* [n_hits] min(qstart, qend)  (utils.py:173-174) */
+  const int32_t* hit_qhi;     /* [n_hits] max(qstart, qend) */
+  const int32_t* hit_taxon;   /* [n_hits] taxon id = sseqid.split("|")[1] (utils.py:234-235) */
+  const int8_t*  hit_strand;  /* [n_hits] 0 '+', 1 '-' (sstrand, utils.py:214) */
+  const double*  hit_score;   /* [n_hits] waafle_score (utils.py:229) */
+  const double*  hit_scov;    /* [n_hits] scov_modified (utils.py:227) */
+  const uint32_t* hit_sysmask;/* [n_hits] annotation systems present (utils.py:237-241) */
+  const int64_t* loc_off;     /* [n_contigs+1] */
+  const int32_t* loc_start;   /* [n_loci] GFF start */
+  const int32_t* loc_end;     /* [n_loci] GFF end */
+  const int8_t*  loc_strand;  /* [n_loci] 0 '+', 1 '-', 2 anything else */
+} wf_batch;
+
+/* Per-contig results (caller-allocated, same residency as the batch). */
+typedef struct wf_result {
+  int8_t*  call;              /* [n] wf_call: routing of orgscorer.py:838-890 */
+  double*  crit;              /* [n] min (max) score of the reported option */
+  double*  rank;              /* [n] avg (max) score of the reported option */
+  int32_t* clade1;            /* [n] reported clade / clade_A (after melding) */
+  int32_t* clade2;            /* [n] clade_B (lgt only) */
+  int8_t*  direction;         /* [n] 0 "A?B", 1 "B>A" */
+  int16_t* iterations;        /* [n] roll-up iterations performed (1 = none) */
+  uint8_t* synteny;           /* [n_loci] synteny characters, CSR by loc_off */
+  int32_t* n_meld1;           /* [n] melded clades for clade1 (tails), 0 = none */
+  int32_t* n_meld2;           /* [n] melded clades for clade2 */
+  int32_t* meld;              /* [2*n_hits + 2*n]; contig c writes its meld1 ids then its
+                                 meld2 ids from 2*hit_off[c] + 2*c */
+  int32_t* annot_hit;         /* [n_loci * n_systems] batch hit index whose annotation
+                                 the locus keeps (orgscorer.py:384-392), or -1 */
+  int64_t* pair_evals;        /* [n] sum of P_pot*(P_pot-1)/2 over explain_two calls */
+  int32_t* status;            /* [n] 0 or a WF_E_* code for this contig */
+  int64_t* need_bytes;        /* [n] workspace bytes asked for when status == WF_E_NOMEM */
+} wf_result;
+
+/* Kernel timing accumulated while enabled (HIP events on the context stream around
+ * the per-contig kernel launches). */
+typedef struct wf_timing {
+  double lds_kernel_ms;       /* sum over launches of the LDS-resident contig kernel */
+  double big_kernel_ms;       /* sum over launches of the overflow (HBM-workspace) kernel */
+  int64_t launches;           /* number of wf_score calls timed */
+  int64_t overflow_contigs;   /* contigs that went to the overflow kernel (host mode) */
+} wf_timing;
+
+int wf_abi_version(void);
+int wf_device_count(int* count);
+int wf_init(int device, wf_ctx** out);
+void wf_free(wf_ctx* ctx);
+const char* wf_last_error(const wf_ctx* ctx);
+int wf_set_stream(wf_ctx* ctx, void* hip_stream);     /* NULL = the context's own stream */
+int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes);     /* dynamic LDS per workgroup */
+int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* tax);
+int wf_score(wf_ctx* ctx, const wf_batch* batch, const wf_params* params, wf_result* out);
+int wf_synchronize(wf_ctx* ctx);
+int wf_timing_enable(wf_ctx* ctx, int on);             /* also resets the counters */
+int wf_timing_read(wf_ctx* ctx, wf_timing* out);       /* synchronises first */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WAAFLE_HIP_H */

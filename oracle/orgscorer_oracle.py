@@ -182,6 +182,7 @@ class GeneLocus:
         self.code = "{}:{}:{}".format(self.start, self.end, self.strand)
         self.annotations = {}
         self.annotation_scores = {}
+        self.annotation_rows = {}       # oracle-only: file row of the winning hit
         self.ignore = False
         self.name = None
 
@@ -340,6 +341,7 @@ class ContigModel:
             if h.score >= ref:
                 L.annotations[system] = value
                 L.annotation_scores[system] = h.score
+                L.annotation_rows[system] = h.order
 
     def refresh(self):
         """orgscorer.py:394-429 (gene scores = np.mean of site arrays; weak loci)."""

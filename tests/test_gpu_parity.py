@@ -1,0 +1,220 @@
+"""GPU parity: the HIP path (through the C-ABI) against the oracle and the goldens.
+
+Bar: bit-exact for every integer/index/string field and for the float64 crit/rank
+(the kernels follow numpy's summation order), TSV bytes identical to the reference
+goldens except tie-flagged contigs (output must be one of the reference's outcomes).
+"""
+import numpy as np
+import pytest
+
+import golden_cases as gc
+from oracle_bridge import oracle_results, run_oracle
+from oracle import orgscorer_oracle as orc
+from waafle_amd import cli, engine, inputs, output, synth
+
+pytestmark = pytest.mark.gpu
+
+CASES = gc.case_names()
+FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n_meld1",
+          "n_meld2", "annot_hit", "pair_evals", "iterations", "status")
+
+
+@pytest.fixture(scope="module")
+def scorer():
+    s = engine.GpuScorer(0)
+    yield s
+    s.close()
+
+
+def gpu_score(scorer, batch, tax, flags):
+    scorer.set_taxonomy(tax)
+    return scorer.score(batch, cli.param_dict(cli.parse_flags(flags)))
+
+
+def meld_sets(res, batch, c):
+    base = 2 * int(batch.hit_off[c]) + 2 * c
+    n1, n2 = int(res.n_meld1[c]), int(res.n_meld2[c])
+    return (sorted(res.meld[base:base + n1].tolist()),
+            sorted(res.meld[base + n1:base + n1 + n2].tolist()))
+
+
+def assert_same_results(got, want, batch, skip=()):
+    bad = []
+    for f in FIELDS:
+        a, b = getattr(got, f), getattr(want, f)
+        if f in ("crit", "rank"):
+            a, b = a.view(np.int64), b.view(np.int64)
+        if f == "clade2":   # only meaningful for lgt rows
+            a = np.where(got.call == 2, a, -1)
+            b = np.where(want.call == 2, b, -1)
+        if f in ("synteny",):
+            keep = np.repeat(want.call != 0, np.diff(batch.loc_off))
+            a, b = a[keep], b[keep]
+        if f == "iterations":
+            keep = want.call != 0
+            a, b = a[keep], b[keep]
+        diff = np.nonzero(a != b)[0]
+        if len(diff):
+            bad.append((f, diff[:5].tolist()))
+    for c in range(batch.n_contigs):
+        if c in skip:
+            continue
+        if meld_sets(got, batch, c) != meld_sets(want, batch, c):
+            bad.append(("meld", c))
+            break
+    assert bad == []
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_gpu_matches_goldens_and_oracle(name, scorer, tmp_path):
+    fx = gc.load(name)
+    paths = gc.materialize(fx, tmp_path)
+    args = cli.parse_flags(fx["flags"])
+    batch, tax = inputs.load_inputs(*paths, args.min_gene_length, warn=None)
+    res = gpu_score(scorer, batch, tax, fx["flags"])
+    rows = output.render(batch, tax, res)
+    texts = {k: "\n".join(v) + "\n" for k, v in rows.items()}
+    assert gc.compare_tsv(fx, texts) == []
+    contigs, _ = run_oracle(paths, fx["flags"])
+    want = oracle_results(contigs, batch, tax)
+    assert_same_results(res, want, batch)
+
+
+def synth_case(tmp_path, flags=(), **kw):
+    data = synth.generate(**kw)
+    paths = synth.write_text(data, str(tmp_path), "s")
+    args = cli.parse_flags(list(flags))
+    batch, tax = inputs.load_inputs(*paths, args.min_gene_length, warn=None)
+    contigs, _ = run_oracle(paths, list(flags))
+    return batch, tax, oracle_results(contigs, batch, tax)
+
+
+@pytest.mark.parametrize("kw,flags", [
+    (dict(n=1500, genes=8, clades=200, seed=21), []),
+    (dict(n=600, genes=12, clades=1000, seed=31), ["-k1", "0.9"]),
+    (dict(n=800, genes=5, clades=12, seed=41, decoys=4, lgt_frac=0.4), []),
+    (dict(n=800, genes=5, clades=12, seed=42, decoys=4, lgt_frac=0.4),
+     ["--weak-loci", "assign-unknown", "--disambiguate-two", "report-best"]),
+    (dict(n=500, genes=7, clades=40, seed=43, decoys=6, short_frac=0.3),
+     ["--min-overlap", "0", "--jump-taxonomy", "2"]),
+    (dict(n=2, genes=20, clades=2500, seed=5, stress=True), []),
+])
+def test_gpu_matches_oracle_synthetic(kw, flags, scorer, tmp_path):
+    batch, tax, want = synth_case(tmp_path, flags, **kw)
+    got = gpu_score(scorer, batch, tax, flags)
+    assert_same_results(got, want, batch)
+
+
+def test_long_locus_uses_numpy_buffered_sum(scorer, tmp_path):
+    """A 20 kb gene: the site mean crosses numpy's 8192-element reduction buffer."""
+    fna = tmp_path / "x.fna"
+    fna.write_text(">big\n" + "N" * 30000 + "\n")
+    (tmp_path / "x.gff").write_text("big\tx\tgene\t101\t20100\t.\t+\t0\t.\n"
+                                    "big\tx\tgene\t20201\t29900\t.\t-\t0\t.\n")
+    rows = []
+    for i, (qs, qe, pid, tx) in enumerate([(101, 15000, "91.237", "s__A"),
+                                          (9000, 20100, "88.001", "s__A"),
+                                          (300, 20000, "79.999", "s__B"),
+                                          (20201, 29900, "95.5", "s__A"),
+                                          (20201, 28000, "99.1", "s__B")]):
+        L = qe - qs + 1
+        rows.append("big\tG{}|{}|KO=K{}\t30000\t{}\t{}\t{}\t{}\t1\t{}\t{}\t{}\t0\t0.0\t9\tplus"
+                    .format(i, tx, i, L, L, qs, qe, L, pid, L))
+    (tmp_path / "x.blastout").write_text("\n".join(rows) + "\n")
+    (tmp_path / "x.tsv").write_text("s__A\tg__G\ns__B\tg__G\ng__G\tr__Root\n")
+    paths = [str(tmp_path / f) for f in ("x.fna", "x.blastout", "x.gff", "x.tsv")]
+    for flags in ([], ["-k1", "0.95", "-k2", "0.9"]):
+        batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
+        got = gpu_score(scorer, batch, tax, flags)
+        contigs, _ = run_oracle(paths, flags)
+        assert_same_results(got, oracle_results(contigs, batch, tax), batch)
+
+
+def test_empty_and_degenerate_contigs(scorer, tmp_path):
+    fna = tmp_path / "e.fna"
+    fna.write_text(">nohits\nNNNN\n>noloci\nNNNNNNNN\n>ok\n" + "N" * 2000 + "\n")
+    (tmp_path / "e.gff").write_text("nohits\tx\tgene\t1\t300\t.\t+\t0\t.\n"
+                                    "ok\tx\tgene\t1\t400\t.\t+\t0\t.\n"
+                                    "ok\tx\tgene\t20\t80\t.\t+\t0\t.\n")
+    (tmp_path / "e.blastout").write_text(
+        "noloci\tG|s__A\t8\t8\t8\t1\t8\t1\t8\t99.0\t8\t0\t0.0\t9\tplus\n"
+        "ok\tG|s__A\t2000\t400\t400\t1\t400\t1\t400\t99.0\t8\t0\t0.0\t9\tplus\n"
+        "ok\tG|s__B\t2000\t400\t10\t1\t10\t1\t10\t99.0\t8\t0\t0.0\t9\tplus\n")
+    (tmp_path / "e.tsv").write_text("s__A\tr__Root\n")
+    paths = [str(tmp_path / f) for f in ("e.fna", "e.blastout", "e.gff", "e.tsv")]
+    for flags in ([], ["--weak-loci", "assign-unknown"], ["--weak-loci", "penalize"]):
+        batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
+        got = gpu_score(scorer, batch, tax, flags)
+        contigs, _ = run_oracle(paths, flags)
+        assert_same_results(got, oracle_results(contigs, batch, tax), batch)
+
+
+def test_full_size_cfg2_properties(scorer):
+    """BASELINE config 2 at full size: deterministic, shard-invariant, LDS-budget
+    invariant (forcing the HBM-workspace kernel), and equal to the oracle on a sample."""
+    data = synth.generate_config("cfg2")
+    batch, tax = synth.to_batch(data)
+    params = cli.param_dict(cli.parse_flags([]))
+    scorer.set_taxonomy(tax)
+    a = scorer.score(batch, params)
+    b = scorer.score(batch, params)
+    assert_same_results(a, b, batch)
+    small = engine.GpuScorer(0, lds_bytes=8192)      # most contigs overflow LDS
+    small.set_taxonomy(tax)
+    c = small.score(batch, params)
+    small.close()
+    assert_same_results(a, c, batch)
+    bounds = engine.shard_bounds(engine.contig_cost(batch), 4)
+    parts = [scorer.score(batch.slice(x, y), params) for x, y in bounds]
+    d = engine.Results.concat(parts, [int(batch.hit_off[x]) for x, _ in bounds])
+    assert_same_results(a, d, batch)
+    assert (a.call == 2).sum() > 0 and (a.call == 1).sum() > 0
+    # oracle on a 300-contig sample (contigs are independent)
+    sub = batch.slice(5000, 5300)
+    opar = orc.Params(**params)
+    otax = orc.Taxonomy(data.tax.edges)
+    hits = oracle_hits_from_batch(sub, tax)
+    loci = oracle_loci_from_batch(sub)
+    lengths = dict(zip(sub.contig_names, sub.contig_lengths.tolist()))
+    contigs = orc.score_contigs(lengths, loci, hits, otax, opar)
+    want = oracle_results(contigs, sub, tax)
+    got = scorer.score(sub, params)
+    assert_same_results(got, want, sub)
+
+
+class _Hit:
+    pass
+
+
+def oracle_hits_from_batch(b, tax):
+    """In-memory oracle hits for a packed batch (scores are already exact floats)."""
+    groups = []
+    for c, name in enumerate(b.contig_names):
+        hs = []
+        for i in range(int(b.hit_off[c]), int(b.hit_off[c + 1])):
+            h = _Hit()
+            h.qstart, h.qend = int(b.hit_qlo[i]), int(b.hit_qhi[i])
+            h.strand = "-" if b.hit_strand[i] else "+"
+            h.scov_mod = float(b.hit_scov[i])
+            h.score = float(b.hit_score[i])
+            h.taxon = tax.names[int(b.hit_taxon[i])]
+            vid = int(b.annot_value_ids[i, 0])
+            h.annotations = {"UniProt": b.annot_values[0][vid]} if vid >= 0 else {}
+            h.order = int(b.hit_row[i])
+            hs.append(h)
+        if hs:
+            groups.append((name, hs))
+    return groups
+
+
+def oracle_loci_from_batch(b):
+    groups = []
+    for c, name in enumerate(b.contig_names):
+        ls = []
+        for l in range(int(b.loc_off[c]), int(b.loc_off[c + 1])):
+            st = {0: "+", 1: "-"}.get(int(b.loc_strand[l]), ".")
+            ls.append(orc.GeneLocus([name, "x", "gene", str(int(b.loc_start[l])),
+                                     str(int(b.loc_end[l])), ".", st, "0", "."]))
+        if ls:
+            groups.append((name, ls))
+    return groups

@@ -1,0 +1,97 @@
+"""Host-side product logic on CPU: parsing/packing, taxonomy interning, sharding and
+TSV rendering, driven by oracle decisions (the GPU supplies them in production)."""
+import numpy as np
+import pytest
+
+import golden_cases as gc
+from oracle_bridge import oracle_results, run_oracle
+from waafle_amd import cli, engine, inputs, output, synth
+from waafle_amd.taxonomy import TaxonomyTables, TaxonomyError
+
+CASES = gc.case_names()
+
+
+def load(fx, tmp_path):
+    paths = gc.materialize(fx, tmp_path)
+    args = cli.parse_flags(fx["flags"])
+    batch, tax = inputs.load_inputs(*paths, args.min_gene_length, warn=None)
+    return paths, batch, tax
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_render_from_oracle_decisions_matches_goldens(name, tmp_path):
+    fx = gc.load(name)
+    paths, batch, tax = load(fx, tmp_path)
+    contigs, _ = run_oracle(paths, fx["flags"])
+    res = oracle_results(contigs, batch, tax)
+    rows = output.render(batch, tax, res)
+    texts = {k: "\n".join(v) + "\n" for k, v in rows.items()}
+    assert gc.compare_tsv(fx, texts) == []
+
+
+def test_packed_scores_match_oracle_hits(tmp_path):
+    fx = gc.load("demo_prodigal_default")
+    paths, batch, tax = load(fx, tmp_path)
+    from oracle import orgscorer_oracle as orc
+    rows = list(orc._tsv_rows(paths[1]))
+    for i in range(batch.n_hits):
+        h = orc.BlastHit(rows[int(batch.hit_row[i])])
+        assert batch.hit_score[i] == h.score and batch.hit_scov[i] == h.scov_mod
+        assert tax.names[batch.hit_taxon[i]] == h.taxon
+        assert batch.hit_qlo[i] == min(h.qstart, h.qend)
+        assert batch.hit_strand[i] == (1 if h.strand == "-" else 0)
+
+
+def test_synth_text_and_binary_agree(tmp_path):
+    data = synth.generate(n=40, genes=6, clades=30, seed=3, short_frac=0.1)
+    paths = synth.write_text(data, str(tmp_path), "s")
+    batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
+    direct, dtax = synth.to_batch(data, 200.0)
+    assert tax.names == dtax.names
+    for f in ("hit_off", "hit_qlo", "hit_qhi", "hit_taxon", "hit_strand", "hit_score",
+              "hit_scov", "hit_sysmask", "loc_off", "loc_start", "loc_end", "loc_strand"):
+        np.testing.assert_array_equal(getattr(batch, f), getattr(direct, f), err_msg=f)
+
+
+def test_shard_concat_roundtrip(tmp_path):
+    fx = gc.load("syn_cfg2_default")
+    paths, batch, tax = load(fx, tmp_path)
+    contigs, _ = run_oracle(paths, fx["flags"])
+    full = oracle_results(contigs, batch, tax)
+    bounds = engine.shard_bounds(engine.contig_cost(batch), 3)
+    assert bounds[0][0] == 0 and bounds[-1][1] == batch.n_contigs and len(bounds) == 3
+    parts = []
+    for a, b in bounds:
+        sub = batch.slice(a, b)
+        r = oracle_results(contigs, sub, tax)
+        parts.append(r)
+    merged = engine.Results.concat(parts, [int(batch.hit_off[a]) for a, _ in bounds])
+    for f in full.__dataclass_fields__:
+        np.testing.assert_array_equal(getattr(full, f), getattr(merged, f), err_msg=f)
+
+
+def test_taxonomy_tables():
+    edges = [("k__A", "r__Root"), ("g__B", "k__A"), ("s__C", "g__B"), ("s__D", "g__B")]
+    t = TaxonomyTables(edges, extra_names={"s__X"})
+    assert t.names == sorted(t.names)
+    i = t.index
+    assert t.parent[i["s__C"]] == i["g__B"] and t.parent[i["s__X"]] == i["r__Root"]
+    assert t.depth[i["s__C"]] == 3 and t.depth[i["r__Root"]] == 0 and t.depth[i["s__X"]] == 1
+    assert t.sib_parent[i["s__C"]] == i["g__B"] and t.sib_parent[i["s__X"]] == -1
+    assert t.leaf_count[i["g__B"]] == 2 and t.leaf_count[i["r__Root"]] == 2
+    assert t.lca([i["s__C"], i["s__D"]]) == "g__B"
+    assert t.tail(i["s__C"], "k__A") == ["g__B", "s__C"]
+    with pytest.raises(TaxonomyError):
+        TaxonomyTables([("a", "b"), ("b", "a")])
+    with pytest.raises(TaxonomyError):
+        TaxonomyTables([("s__C", "g__B"), ("s__C", "g__Z")])
+
+
+def test_ungrouped_blastout_is_rejected(tmp_path):
+    fx = gc.load("tie_default")
+    paths = gc.materialize(fx, tmp_path)
+    lines = open(paths[1]).read().splitlines()
+    bad = tmp_path / "bad.blastout"
+    bad.write_text("\n".join([lines[0], lines[4], lines[1]]) + "\n")
+    with pytest.raises(inputs.InputError):
+        inputs.load_inputs(paths[0], str(bad), paths[2], paths[3], 200.0, warn=None)

@@ -1,0 +1,504 @@
+// C-ABI of libwaafle_hip.so (see include/waafle_hip.h): context/device management,
+// taxonomy upload, batch staging and the two-kernel launch sequence.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "waafle_hip.h"
+#include "wf_internal.h"
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct wf_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // taxonomy
+  int32_t tax_n = 0, root = -1, unknown = -1;
+  DevBuf parent, depth, sibp, leaves;
+  // overflow work list + counter
+  DevBuf ovf_list, ovf_count;
+  DevBuf retry_list, retry_count;
+  DevBuf big_ws;
+  int64_t lds_bytes = 48 * 1024;
+  int big_slots = 512;
+  // staging for host-resident batches
+  DevBuf b_hit_off, b_qlo, b_qhi, b_taxon, b_hstrand, b_score, b_scov, b_sysmask;
+  DevBuf b_loc_off, b_lstart, b_lend, b_lstrand;
+  DevBuf r_call, r_crit, r_rank, r_c1, r_c2, r_dir, r_iters, r_syn, r_nm1, r_nm2, r_meld,
+      r_annot, r_pairs, r_status, r_need;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_lds, ev_big;  // indices into ev_pool
+  int64_t launches = 0, overflow_contigs = 0;
+};
+
+namespace {
+
+int fail(wf_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                             \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(ctx, WF_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));       \
+  } while (0)
+
+int ensure(wf_ctx* ctx, DevBuf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.bytes >= bytes) return WF_OK;
+  if (b.p) {
+    hipStreamSynchronize(ctx->stream);
+    hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = std::max(bytes, b.bytes * 3 / 2);
+  hipError_t e = hipMalloc(&b.p, want);
+  if (e != hipSuccess) {
+    e = hipMalloc(&b.p, bytes);
+    want = bytes;
+  }
+  if (e != hipSuccess)
+    return fail(ctx, WF_E_HIP, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+  b.bytes = want;
+  return WF_OK;
+}
+
+void release(DevBuf& b) {
+  if (b.p) hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+template <class T>
+int upload(wf_ctx* ctx, DevBuf& b, const T* src, int64_t count, const T** dst) {
+  int rc = ensure(ctx, b, sizeof(T) * (size_t)std::max<int64_t>(count, 1));
+  if (rc) return rc;
+  if (count > 0) {
+    hipError_t e = hipMemcpyAsync(b.p, src, sizeof(T) * count, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) return fail(ctx, WF_E_HIP, "H2D copy failed: %s", hipGetErrorString(e));
+  }
+  *dst = static_cast<const T*>(b.p);
+  return WF_OK;
+}
+
+template <class T>
+int alloc_out(wf_ctx* ctx, DevBuf& b, int64_t count, T** dst) {
+  int rc = ensure(ctx, b, sizeof(T) * (size_t)std::max<int64_t>(count, 1));
+  if (rc) return rc;
+  *dst = static_cast<T*>(b.p);
+  return WF_OK;
+}
+
+template <class T>
+int download(wf_ctx* ctx, T* host, const T* dev, int64_t count) {
+  if (count <= 0) return WF_OK;
+  hipError_t e = hipMemcpyAsync(host, dev, sizeof(T) * count, hipMemcpyDeviceToHost, ctx->stream);
+  if (e != hipSuccess) return fail(ctx, WF_E_HIP, "D2H copy failed: %s", hipGetErrorString(e));
+  return WF_OK;
+}
+
+int take_event_pair(wf_ctx* ctx, std::vector<std::pair<int, int>>& list) {
+  for (int k = 0; k < 2; ++k) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return -1;
+    ctx->ev_pool.push_back(ev);
+  }
+  int a = (int)ctx->ev_pool.size() - 2;
+  list.push_back({a, a + 1});
+  return a;
+}
+
+wf::DevParams derive_params(const wf_params& p) {
+  wf::DevParams d{};
+  d.k1 = p.k1;
+  d.k2 = p.k2;
+  d.kmin = std::min(p.k1, p.k2);   // orgscorer.py:338-339
+  const double kmax = std::max(p.k1, p.k2);
+  const double eps = 1e-6;          // c_eps, orgscorer.py:58
+  d.k_amb = p.ambiguous_threshold == 0 ? eps : (p.ambiguous_threshold == 1 ? d.kmin : kmax);
+  d.sister_thr = p.sister_penalty == 1 ? kmax : d.kmin;   // lenient: max, strict: min
+  d.sister_on = p.sister_penalty != 0;
+  d.annot_ref = p.annotation_threshold == 0 ? eps : (p.annotation_threshold == 1 ? d.kmin : kmax);
+  d.range = p.range;
+  d.min_overlap = p.min_overlap;
+  d.min_scov = p.min_scov;
+  d.amb_frac = p.ambiguous_fraction;
+  d.dis1 = p.disambiguate_one;
+  d.dis2 = p.disambiguate_two;
+  d.jump = p.jump_taxonomy > 0 ? p.jump_taxonomy : 0;
+  d.allow_lca = p.allow_lca;
+  d.clade_genes = p.clade_genes;
+  d.clade_leaves = p.clade_leaves;
+  d.weak = p.weak_loci;
+  d.stranded = p.stranded;
+  return d;
+}
+
+int64_t slot_estimate(const wf_batch* b) {
+  // persistent (loci + leaves + attachments) + one level (keys, segments, clades, S)
+  const int64_t H = std::max(b->max_hits, 1), G = std::max(b->max_loci, 1);
+  const int64_t A = 2 * H + 64;
+  int64_t npow = 1;
+  while (npow < A + 1) npow <<= 1;
+  const int64_t P = H + 1;
+  return 64 * G + 16 * (G * 24 + 8) + 36 * A + 8 * npow + 12 * (A + 2) +
+         P * (8 * G + 56) + G * 32 + 8 * G * std::max(b->n_systems, 1) + 4096;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wf_abi_version(void) { return WF_ABI_VERSION; }
+
+int wf_device_count(int* count) {
+  if (!count) return WF_E_BADINPUT;
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) {
+    *count = 0;
+    return WF_E_HIP;
+  }
+  return WF_OK;
+}
+
+int wf_init(int device, wf_ctx** out) {
+  if (!out) return WF_E_BADINPUT;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return WF_E_HIP;
+  if (device < 0 || device >= n) return WF_E_BADINPUT;
+  wf_ctx* ctx = new (std::nothrow) wf_ctx();
+  if (!ctx) return WF_E_NOMEM;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return WF_E_HIP;
+  }
+  ctx->stream = ctx->own_stream;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess)
+    ctx->big_slots = std::max(64, prop.multiProcessorCount * 2);
+  *out = ctx;
+  return WF_OK;
+}
+
+void wf_free(wf_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->ovf_list,
+                    &ctx->ovf_count, &ctx->retry_list, &ctx->retry_count, &ctx->big_ws,
+                    &ctx->b_hit_off, &ctx->b_qlo, &ctx->b_qhi, &ctx->b_taxon, &ctx->b_hstrand,
+                    &ctx->b_score, &ctx->b_scov, &ctx->b_sysmask, &ctx->b_loc_off,
+                    &ctx->b_lstart, &ctx->b_lend, &ctx->b_lstrand, &ctx->r_call, &ctx->r_crit,
+                    &ctx->r_rank, &ctx->r_c1, &ctx->r_c2, &ctx->r_dir, &ctx->r_iters,
+                    &ctx->r_syn, &ctx->r_nm1, &ctx->r_nm2, &ctx->r_meld, &ctx->r_annot,
+                    &ctx->r_pairs, &ctx->r_status, &ctx->r_need};
+  for (DevBuf* b : bufs) release(*b);
+  for (hipEvent_t ev : ctx->ev_pool) hipEventDestroy(ev);
+  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+const char* wf_last_error(const wf_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int wf_set_stream(wf_ctx* ctx, void* hip_stream) {
+  if (!ctx) return WF_E_BADINPUT;
+  ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  return WF_OK;
+}
+
+int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes) {
+  if (!ctx) return WF_E_BADINPUT;
+  if (bytes < 4096 || bytes > 150 * 1024)
+    return fail(ctx, WF_E_BADINPUT, "LDS budget %lld out of [4096, 153600]", (long long)bytes);
+  ctx->lds_bytes = bytes;
+  return WF_OK;
+}
+
+int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* t) {
+  if (!ctx || !t) return WF_E_BADINPUT;
+  if (t->n <= 0 || !t->parent || !t->depth || !t->sib_parent || !t->leaf_count)
+    return fail(ctx, WF_E_BADINPUT, "taxonomy arrays missing");
+  if (t->n >= (1 << 24)) return fail(ctx, WF_E_BADINPUT, "more than 2^24-1 taxonomy names");
+  if (t->root < 0 || t->root >= t->n || t->unknown < 0 || t->unknown >= t->n)
+    return fail(ctx, WF_E_BADINPUT, "root/unknown ids out of range");
+  for (int32_t i = 0; i < t->n; ++i) {   // parent ids valid; depth consistent with parents
+    const int32_t p = t->parent[i];
+    if (p < 0 || p >= t->n) return fail(ctx, WF_E_BADINPUT, "parent id out of range at %d", i);
+    if (i == t->root ? t->depth[i] != 0 : t->depth[i] != t->depth[p] + 1)
+      return fail(ctx, WF_E_BADINPUT, "depth inconsistent with parent at %d", i);
+  }
+  hipSetDevice(ctx->device);
+  const int32_t *dp, *dd, *ds;
+  const int64_t* dl;
+  int rc;
+  if ((rc = upload(ctx, ctx->parent, t->parent, t->n, &dp)) ||
+      (rc = upload(ctx, ctx->depth, t->depth, t->n, &dd)) ||
+      (rc = upload(ctx, ctx->sibp, t->sib_parent, t->n, &ds)) ||
+      (rc = upload(ctx, ctx->leaves, t->leaf_count, t->n, &dl)))
+    return rc;
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  ctx->tax_n = t->n;
+  ctx->root = t->root;
+  ctx->unknown = t->unknown;
+  return WF_OK;
+}
+
+static int check_batch(wf_ctx* ctx, const wf_batch* b, const wf_params* p, const wf_result* r) {
+  if (!b || !p || !r) return fail(ctx, WF_E_BADINPUT, "null batch/params/result");
+  if (ctx->tax_n <= 0) return fail(ctx, WF_E_STATE, "wf_set_taxonomy must precede wf_score");
+  if (b->n_contigs < 0 || b->n_hits < 0 || b->n_loci < 0)
+    return fail(ctx, WF_E_BADINPUT, "negative sizes");
+  if (b->n_systems < 0 || b->n_systems > 32)
+    return fail(ctx, WF_E_BADINPUT, "n_systems %d not in [0, 32]", b->n_systems);
+  if (b->n_hits >= (int64_t)1 << 31) return fail(ctx, WF_E_BADINPUT, "n_hits must be < 2^31");
+  if (b->max_loci >= 0xFFFF) return fail(ctx, WF_E_BADINPUT, "more than 65534 loci in a contig");
+  if (p->disambiguate_one < 0 || p->disambiguate_one > 1 || p->disambiguate_two < 0 ||
+      p->disambiguate_two > 2 || p->ambiguous_threshold < 0 || p->ambiguous_threshold > 2 ||
+      p->sister_penalty < 0 || p->sister_penalty > 2 || p->weak_loci < 0 || p->weak_loci > 2 ||
+      p->annotation_threshold < 0 || p->annotation_threshold > 2)
+    return fail(ctx, WF_E_BADINPUT, "parameter enum out of range");
+  if (b->n_contigs > 0 && (!b->hit_off || !b->loc_off))
+    return fail(ctx, WF_E_BADINPUT, "null offsets");
+  if (b->n_hits > 0 && (!b->hit_qlo || !b->hit_qhi || !b->hit_taxon || !b->hit_strand ||
+                        !b->hit_score || !b->hit_scov || !b->hit_sysmask))
+    return fail(ctx, WF_E_BADINPUT, "null hit arrays");
+  if (b->n_loci > 0 && (!b->loc_start || !b->loc_end || !b->loc_strand))
+    return fail(ctx, WF_E_BADINPUT, "null locus arrays");
+  if (!r->call || !r->crit || !r->rank || !r->clade1 || !r->clade2 || !r->direction ||
+      !r->iterations || !r->synteny || !r->n_meld1 || !r->n_meld2 || !r->meld ||
+      !r->annot_hit || !r->pair_evals || !r->status || !r->need_bytes)
+    return fail(ctx, WF_E_BADINPUT, "null result arrays");
+  if (!b->device_resident) {   // host batches: validate CSR and ids before any launch
+    const int64_t* ho = b->hit_off;
+    const int64_t* lo = b->loc_off;
+    if (ho[0] != 0 || lo[0] != 0 || ho[b->n_contigs] != b->n_hits || lo[b->n_contigs] != b->n_loci)
+      return fail(ctx, WF_E_BADINPUT, "CSR offsets inconsistent with sizes");
+    for (int32_t c = 0; c < b->n_contigs; ++c) {
+      if (ho[c + 1] < ho[c] || lo[c + 1] < lo[c]) return fail(ctx, WF_E_BADINPUT, "offsets decrease");
+      if (ho[c + 1] - ho[c] > b->max_hits || lo[c + 1] - lo[c] > b->max_loci)
+        return fail(ctx, WF_E_BADINPUT, "max_hits/max_loci understate contig %d", c);
+    }
+    for (int64_t i = 0; i < b->n_hits; ++i)
+      if (b->hit_taxon[i] < 0 || b->hit_taxon[i] >= ctx->tax_n)
+        return fail(ctx, WF_E_BADINPUT, "hit %lld taxon id out of range", (long long)i);
+  }
+  return WF_OK;
+}
+
+static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
+  int rc;
+  // overflow list
+  if ((rc = ensure(ctx, ctx->ovf_list, sizeof(int32_t) * (size_t)std::max(b->n_contigs, 1))) ||
+      (rc = ensure(ctx, ctx->ovf_count, 64)))
+    return rc;
+  K.ovf_list = static_cast<int32_t*>(ctx->ovf_list.p);
+  K.ovf_count = static_cast<int32_t*>(ctx->ovf_count.p);
+  K.work_list = K.ovf_list;
+  K.work_count = K.ovf_count;
+  HIP_TRY(ctx, hipMemsetAsync(K.ovf_count, 0, sizeof(int32_t), ctx->stream));
+  // HBM workspace for overflow contigs
+  const int64_t slot = slot_estimate(b);
+  const int slots = std::min(ctx->big_slots, std::max(b->n_contigs, 1));
+  if ((rc = ensure(ctx, ctx->big_ws, (size_t)slot * slots))) return rc;
+  K.big_ws = static_cast<char*>(ctx->big_ws.p);
+  K.slot_bytes = slot;
+  K.lds_bytes = ctx->lds_bytes;
+  K.root = ctx->root;
+  K.unknown = ctx->unknown;
+
+  std::pair<int, int> el{-1, -1}, eb{-1, -1};
+  if (ctx->timing) {
+    take_event_pair(ctx, ctx->ev_lds);
+    el = ctx->ev_lds.back();
+    take_event_pair(ctx, ctx->ev_big);
+    eb = ctx->ev_big.back();
+  }
+  if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
+  HIP_TRY(ctx, wf::launch_lds_kernel(K, ctx->stream));
+  if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
+  if (eb.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[eb.first], ctx->stream));
+  HIP_TRY(ctx, wf::launch_big_kernel(K, slots, ctx->stream));
+  if (eb.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[eb.second], ctx->stream));
+  ++ctx->launches;
+  return WF_OK;
+}
+
+int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
+  if (!ctx) return WF_E_BADINPUT;
+  int rc = check_batch(ctx, b, p, r);
+  if (rc) return rc;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  wf::KArgs K{};
+  K.n_contigs = b->n_contigs;
+  K.n_sys = b->n_systems;
+  K.parent = static_cast<const int32_t*>(ctx->parent.p);
+  K.depth = static_cast<const int32_t*>(ctx->depth.p);
+  K.sibp = static_cast<const int32_t*>(ctx->sibp.p);
+  K.leaves = static_cast<const int64_t*>(ctx->leaves.p);
+  K.p = derive_params(*p);
+  const int64_t N = b->n_contigs, NH = b->n_hits, NL = b->n_loci;
+  const int64_t n_meld = 2 * NH + 2 * N, n_annot = NL * b->n_systems;
+
+  if (b->device_resident) {
+    K.hit_off = b->hit_off; K.qlo = b->hit_qlo; K.qhi = b->hit_qhi; K.taxon = b->hit_taxon;
+    K.hstrand = b->hit_strand; K.score = b->hit_score; K.scov = b->hit_scov;
+    K.sysmask = b->hit_sysmask; K.loc_off = b->loc_off; K.lstart = b->loc_start;
+    K.lend = b->loc_end; K.lstrand = b->loc_strand;
+    K.call = r->call; K.crit = r->crit; K.rank = r->rank; K.c1 = r->clade1; K.c2 = r->clade2;
+    K.dir = r->direction; K.iters = r->iterations; K.syn = r->synteny; K.nm1 = r->n_meld1;
+    K.nm2 = r->n_meld2; K.meld = r->meld; K.annot = r->annot_hit; K.pair_evals = r->pair_evals;
+    K.status = r->status; K.need = r->need_bytes;
+    return run_kernels(ctx, K, b);
+  }
+
+  // host-resident: stage, run, copy back, retry workspace overflows with exact sizes
+  if ((rc = upload(ctx, ctx->b_hit_off, b->hit_off, N + 1, &K.hit_off)) ||
+      (rc = upload(ctx, ctx->b_qlo, b->hit_qlo, NH, &K.qlo)) ||
+      (rc = upload(ctx, ctx->b_qhi, b->hit_qhi, NH, &K.qhi)) ||
+      (rc = upload(ctx, ctx->b_taxon, b->hit_taxon, NH, &K.taxon)) ||
+      (rc = upload(ctx, ctx->b_hstrand, b->hit_strand, NH, &K.hstrand)) ||
+      (rc = upload(ctx, ctx->b_score, b->hit_score, NH, &K.score)) ||
+      (rc = upload(ctx, ctx->b_scov, b->hit_scov, NH, &K.scov)) ||
+      (rc = upload(ctx, ctx->b_sysmask, b->hit_sysmask, NH, &K.sysmask)) ||
+      (rc = upload(ctx, ctx->b_loc_off, b->loc_off, N + 1, &K.loc_off)) ||
+      (rc = upload(ctx, ctx->b_lstart, b->loc_start, NL, &K.lstart)) ||
+      (rc = upload(ctx, ctx->b_lend, b->loc_end, NL, &K.lend)) ||
+      (rc = upload(ctx, ctx->b_lstrand, b->loc_strand, NL, &K.lstrand)))
+    return rc;
+  if ((rc = alloc_out(ctx, ctx->r_call, N, &K.call)) ||
+      (rc = alloc_out(ctx, ctx->r_crit, N, &K.crit)) ||
+      (rc = alloc_out(ctx, ctx->r_rank, N, &K.rank)) ||
+      (rc = alloc_out(ctx, ctx->r_c1, N, &K.c1)) || (rc = alloc_out(ctx, ctx->r_c2, N, &K.c2)) ||
+      (rc = alloc_out(ctx, ctx->r_dir, N, &K.dir)) ||
+      (rc = alloc_out(ctx, ctx->r_iters, N, &K.iters)) ||
+      (rc = alloc_out(ctx, ctx->r_syn, NL, &K.syn)) ||
+      (rc = alloc_out(ctx, ctx->r_nm1, N, &K.nm1)) ||
+      (rc = alloc_out(ctx, ctx->r_nm2, N, &K.nm2)) ||
+      (rc = alloc_out(ctx, ctx->r_meld, n_meld, &K.meld)) ||
+      (rc = alloc_out(ctx, ctx->r_annot, n_annot, &K.annot)) ||
+      (rc = alloc_out(ctx, ctx->r_pairs, N, &K.pair_evals)) ||
+      (rc = alloc_out(ctx, ctx->r_status, N, &K.status)) ||
+      (rc = alloc_out(ctx, ctx->r_need, N, &K.need)))
+    return rc;
+  if ((rc = run_kernels(ctx, K, b))) return rc;
+  if ((rc = download(ctx, r->status, K.status, N)) || (rc = download(ctx, r->need_bytes, K.need, N)))
+    return rc;
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+
+  // contigs whose state outgrew the estimated HBM slot: rerun with an exact slot size
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    std::vector<int32_t> retry;
+    int64_t need = 0;
+    for (int32_t c = 0; c < b->n_contigs; ++c)
+      if (r->status[c] == WF_E_NOMEM || r->status[c] == wf::kPending) {
+        retry.push_back(c);
+        need = std::max(need, r->need_bytes[c]);
+      }
+    if (retry.empty()) break;
+    ctx->overflow_contigs += (int64_t)retry.size();
+    need = std::max<int64_t>(need * 2, 1 << 20);
+    const int slots = std::min<int>(ctx->big_slots, (int)retry.size());
+    const int32_t count = (int32_t)retry.size();
+    if ((rc = ensure(ctx, ctx->big_ws, (size_t)need * slots)) ||
+        (rc = ensure(ctx, ctx->retry_list, sizeof(int32_t) * retry.size())) ||
+        (rc = ensure(ctx, ctx->retry_count, 64)))
+      return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->retry_list.p, retry.data(), sizeof(int32_t) * retry.size(),
+                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->retry_count.p, &count, sizeof(int32_t), hipMemcpyHostToDevice,
+                                ctx->stream));
+    K.work_list = static_cast<const int32_t*>(ctx->retry_list.p);
+    K.work_count = static_cast<const int32_t*>(ctx->retry_count.p);
+    K.big_ws = static_cast<char*>(ctx->big_ws.p);
+    K.slot_bytes = need;
+    HIP_TRY(ctx, wf::launch_big_kernel(K, slots, ctx->stream));
+    if ((rc = download(ctx, r->status, K.status, N)) ||
+        (rc = download(ctx, r->need_bytes, K.need, N)))
+      return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  if ((rc = download(ctx, r->call, K.call, N)) || (rc = download(ctx, r->crit, K.crit, N)) ||
+      (rc = download(ctx, r->rank, K.rank, N)) || (rc = download(ctx, r->clade1, K.c1, N)) ||
+      (rc = download(ctx, r->clade2, K.c2, N)) || (rc = download(ctx, r->direction, K.dir, N)) ||
+      (rc = download(ctx, r->iterations, K.iters, N)) ||
+      (rc = download(ctx, r->synteny, K.syn, NL)) || (rc = download(ctx, r->n_meld1, K.nm1, N)) ||
+      (rc = download(ctx, r->n_meld2, K.nm2, N)) || (rc = download(ctx, r->meld, K.meld, n_meld)) ||
+      (rc = download(ctx, r->annot_hit, K.annot, n_annot)) ||
+      (rc = download(ctx, r->pair_evals, K.pair_evals, N)))
+    return rc;
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (int32_t c = 0; c < b->n_contigs; ++c)
+    if (r->status[c] != 0)
+      return fail(ctx, r->status[c] == wf::kPending ? WF_E_NOMEM : r->status[c],
+                  "contig %d failed with status %d", c, r->status[c]);
+  return WF_OK;
+}
+
+int wf_synchronize(wf_ctx* ctx) {
+  if (!ctx) return WF_E_BADINPUT;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  return WF_OK;
+}
+
+int wf_timing_enable(wf_ctx* ctx, int on) {
+  if (!ctx) return WF_E_BADINPUT;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  for (hipEvent_t ev : ctx->ev_pool) hipEventDestroy(ev);
+  ctx->ev_pool.clear();
+  ctx->ev_lds.clear();
+  ctx->ev_big.clear();
+  ctx->launches = 0;
+  ctx->overflow_contigs = 0;
+  ctx->timing = on != 0;
+  return WF_OK;
+}
+
+int wf_timing_read(wf_ctx* ctx, wf_timing* out) {
+  if (!ctx || !out) return WF_E_BADINPUT;
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  double lds = 0.0, big = 0.0;
+  for (auto& pr : ctx->ev_lds) {
+    float ms = 0.f;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev_pool[pr.first], ctx->ev_pool[pr.second]));
+    lds += ms;
+  }
+  for (auto& pr : ctx->ev_big) {
+    float ms = 0.f;
+    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev_pool[pr.first], ctx->ev_pool[pr.second]));
+    big += ms;
+  }
+  out->lds_kernel_ms = lds;
+  out->big_kernel_ms = big;
+  out->launches = (int64_t)ctx->ev_lds.size();
+  out->overflow_contigs = ctx->overflow_contigs;
+  return WF_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,50 @@
+// Internal definitions shared by the HIP kernels (wf_kernels.hip) and the C-ABI
+// implementation (wf_api.cpp).  Not part of the public interface.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wf {
+
+constexpr int kBlock = 256;             // 4 waves of 64 lanes per contig workgroup
+constexpr int kWaves = kBlock / 64;
+constexpr int kLeafMax = 128;           // numpy pairwise-sum leaf size (PW_BLOCKSIZE)
+constexpr int kNpyBuf = 8192;           // numpy reduction buffer (NPY_BUFSIZE)
+constexpr int kLeafSlots = 160;         // >= leaves of one 8192-element buffer
+constexpr int kMaxIter = 100;           // orgscorer.py:580
+constexpr int kPending = 1;             // status: handed to the overflow kernel
+
+// Parameters with the derived thresholds precomputed on the host
+// (orgscorer.py:338-346, :515-516, :720-721).
+struct DevParams {
+  double k1, k2, kmin, k_amb, range, min_overlap, min_scov, amb_frac, sister_thr, annot_ref;
+  int dis1;        // 0 report-best, 1 meld
+  int dis2;        // 0 report-best, 1 jump, 2 meld
+  int jump;        // number of initial raises
+  int allow_lca, clade_genes, clade_leaves, weak, stranded, sister_on;
+};
+
+struct KArgs {
+  // batch
+  int n_contigs, n_sys;
+  const int64_t* hit_off; const int32_t* qlo; const int32_t* qhi; const int32_t* taxon;
+  const int8_t* hstrand; const double* score; const double* scov; const uint32_t* sysmask;
+  const int64_t* loc_off; const int32_t* lstart; const int32_t* lend; const int8_t* lstrand;
+  // taxonomy
+  const int32_t* parent; const int32_t* depth; const int32_t* sibp; const int64_t* leaves;
+  int32_t root, unknown;
+  DevParams p;
+  // results
+  int8_t* call; double* crit; double* rank; int32_t* c1; int32_t* c2; int8_t* dir;
+  int16_t* iters; uint8_t* syn; int32_t* nm1; int32_t* nm2; int32_t* meld; int32_t* annot;
+  int64_t* pair_evals; int32_t* status; int64_t* need;
+  // overflow work list (filled by the LDS kernel, drained by the HBM-workspace kernel)
+  int32_t* ovf_list; int32_t* ovf_count;
+  const int32_t* work_list; const int32_t* work_count;   // list the big kernel drains
+  char* big_ws; int64_t slot_bytes; int64_t lds_bytes;
+};
+
+hipError_t launch_lds_kernel(const KArgs& k, hipStream_t s);
+hipError_t launch_big_kernel(const KArgs& k, int grid, hipStream_t s);
+
+}  // namespace wf

@@ -1,0 +1,1072 @@
+// HIP kernels for the waafle_orgscorer contig-scoring hot path (gfx950 / MI355X).
+//
+// One 256-thread workgroup scores one contig end to end: hit->locus attachment
+// (orgscorer.py:359-392), per-(clade, locus) site-score means in numpy's exact
+// pairwise float64 order (:394-429), the taxonomy roll-up loop (:431-445, :566-583),
+// the one-clade search + meld (:585-597, :621-631) and the all-pairs two-clade search
+// + meld + LGT filters (:599-619, :633-744).  The per-contig state lives in LDS
+// (k_contig_lds); contigs whose state does not fit the LDS budget are re-run by
+// k_contig_big with the same code on a per-workgroup HBM workspace slot.
+//
+// Exactness rules: device code is compiled with -ffp-contract=off (no fma fusion), fp64
+// division is IEEE-correct, and every float64 sum follows numpy's add.reduce order
+// (8192-element buffers added sequentially from 0.0; each buffer summed pairwise with
+// 128-element leaves of eight strided accumulators).
+#include "wf_internal.h"
+
+#include "waafle_hip.h"
+
+namespace wf {
+
+namespace {
+
+constexpr uint64_t kKeyPad = ~0ull;
+constexpr int kLocVirtual = 0xFFFF;     // locus field of the virtual "Unknown" key
+
+struct Ctl {
+  int A, A1, npow, S_n, P, Gu, Pp;
+  int overflow, status, cnt, cnt2, p_unk, root_present, all_ignored;
+  int n_in, all_ok, all_same, best_ok, best_dir, best_c1p, best_c2p;
+  int lca1, lca2, res_kind, lca_out;
+  double best_r, best_crit;
+  long long best_k;
+  int64_t need;
+  double red_r[kWaves];
+  long long red_k[kWaves];
+  int red_i[kWaves];
+  int red_j[kWaves];
+};
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+struct Arena {
+  char* base;
+  int64_t cap;
+  int64_t used;
+  template <class T>
+  __device__ __forceinline__ T* take(int64_t count) {
+    int64_t off = (used + 15) & ~int64_t(15);
+    used = off + count * (int64_t)sizeof(T);
+    return reinterpret_cast<T*>(base + off);
+  }
+  __device__ __forceinline__ bool fits() const { return used <= cap; }
+};
+
+__device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
+
+// --------------------------------------------------------------------------
+// block-wide primitives
+// --------------------------------------------------------------------------
+
+// Exclusive prefix sum of one int per thread; *total receives the block sum.
+__device__ int block_scan(int v, int* total, Ctl& ctl) {
+  const int lane = lane_id(), w = wave_id();
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) ctl.red_i[w] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) {
+    int t = ctl.red_i[i];
+    base += (i < w) ? t : 0;
+    tot += t;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// Two exclusive prefix sums at once.
+__device__ void block_scan2(int v1, int v2, int* p1, int* p2, int* t1, int* t2, Ctl& ctl) {
+  const int lane = lane_id(), w = wave_id();
+  int x = v1, y = v2;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int a = __shfl_up(x, d, 64), b = __shfl_up(y, d, 64);
+    if (lane >= d) { x += a; y += b; }
+  }
+  if (lane == 63) { ctl.red_i[w] = x; ctl.red_j[w] = y; }
+  __syncthreads();
+  int b1 = 0, b2 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+  for (int i = 0; i < kWaves; ++i) {
+    int a = ctl.red_i[i], b = ctl.red_j[i];
+    if (i < w) { b1 += a; b2 += b; }
+    s1 += a;
+    s2 += b;
+  }
+  __syncthreads();
+  *p1 = b1 + x - v1;
+  *p2 = b2 + y - v2;
+  *t1 = s1;
+  *t2 = s2;
+}
+
+// (rank, key) maximum; ties on rank go to the larger key (= later in enumeration order,
+// which is what `sorted(options, key=rank)[-1]` picks, orgscorer.py:623-624, 634-635).
+__device__ __forceinline__ bool better(double r2, long long k2, double r, long long k) {
+  return k2 >= 0 && (k < 0 || r2 > r || (r2 == r && k2 > k));
+}
+
+__device__ void block_argmax(double& r, long long& k, Ctl& ctl) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    double r2 = __shfl_xor(r, off, 64);
+    long long k2 = __shfl_xor(k, off, 64);
+    if (better(r2, k2, r, k)) { r = r2; k = k2; }
+  }
+  if (lane_id() == 0) { ctl.red_r[wave_id()] = r; ctl.red_k[wave_id()] = k; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double br = ctl.red_r[0];
+    long long bk = ctl.red_k[0];
+    for (int i = 1; i < kWaves; ++i)
+      if (better(ctl.red_r[i], ctl.red_k[i], br, bk)) { br = ctl.red_r[i]; bk = ctl.red_k[i]; }
+    ctl.best_r = br;
+    ctl.best_k = bk;
+  }
+  __syncthreads();
+  r = ctl.best_r;
+  k = ctl.best_k;
+}
+
+template <class T>
+__device__ void bitonic_sort(T* keys, int n) {
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += kBlock) {
+        int ixj = i ^ j;
+        if (ixj > i) {
+          T a = keys[i], b = keys[ixj];
+          bool up = (i & k) == 0;
+          if ((a > b) == up) { keys[i] = b; keys[ixj] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// --------------------------------------------------------------------------
+// taxonomy helpers (utils.py:401-411)
+// --------------------------------------------------------------------------
+
+__device__ int lca2(const KArgs& K, int a, int b) {
+  if (a < 0) return b;
+  if (b < 0) return a;
+  int da = K.depth[a], db = K.depth[b];
+  while (da > db) { a = K.parent[a]; --da; }
+  while (db > da) { b = K.parent[b]; --db; }
+  while (a != b) { a = K.parent[a]; b = K.parent[b]; }
+  return a;
+}
+
+// LCA of list[0..m) (clade ids); wave 0 folds, result broadcast through ctl.
+__device__ int block_lca(const KArgs& K, const int* list, int m, Ctl& ctl) {
+  if (m <= 0) return -1;
+  if (m == 1) return list[0];
+  if (wave_id() == 0) {
+    int acc = -1;
+    for (int i = lane_id(); i < m; i += 64) acc = lca2(K, acc, list[i]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      int o = __shfl_xor(acc, off, 64);
+      acc = lca2(K, acc, o);
+    }
+    if (lane_id() == 0) ctl.lca_out = acc;
+  }
+  __syncthreads();
+  int r = ctl.lca_out;
+  __syncthreads();
+  return r;
+}
+
+// --------------------------------------------------------------------------
+// numpy pairwise summation order
+// --------------------------------------------------------------------------
+
+// Leaves of numpy's pairwise sum over one buffer [off0, off0+cl): emitted left to right
+// as (start, length, number of parent additions completed right after this leaf).
+__device__ int gen_leaves(int off0, int cl, int4* out) {
+  int foff[16], flen[16], fst[16];
+  int sp = 1, cnt = 0;
+  foff[0] = off0; flen[0] = cl; fst[0] = 0;
+  while (sp > 0) {
+    int t = sp - 1;
+    if (flen[t] > kLeafMax && fst[t] == 0) {
+      int h = flen[t] / 2;
+      h -= h % 8;
+      fst[t] = 1;
+      foff[sp] = foff[t]; flen[sp] = h; fst[sp] = 0;
+      ++sp;
+      continue;
+    }
+    int lo = foff[t], ll = flen[t], adds = 0;
+    --sp;
+    while (sp > 0) {
+      int u = sp - 1;
+      if (fst[u] == 1) {
+        int h = flen[u] / 2;
+        h -= h % 8;
+        fst[u] = 2;
+        foff[sp] = foff[u] + h; flen[sp] = flen[u] - h; fst[sp] = 0;
+        ++sp;
+        break;
+      }
+      ++adds;
+      --sp;
+    }
+    if (out) out[cnt] = make_int4(lo, ll, adds, 0);
+    ++cnt;
+  }
+  return cnt;
+}
+
+__device__ int leaves_of_length(int n) {
+  int cnt = 0;
+  for (int o = 0; o < n; o += kNpyBuf) cnt += gen_leaves(o, min(kNpyBuf, n - o), nullptr);
+  return cnt;
+}
+
+__device__ double combine_leaves(const int4* lv, int nl, const double* ls) {
+  double stk[16];
+  int sp = 0;
+  for (int i = 0; i < nl; ++i) {
+    stk[sp++] = ls[i];
+    for (int a = 0; a < lv[i].z; ++a) {
+      double r = stk[--sp];
+      double l = stk[--sp];
+      stk[sp++] = l + r;
+    }
+  }
+  return stk[0];
+}
+
+// One leaf (<= 128 elements) exactly as numpy's pairwise_sum inner block.
+template <class F>
+__device__ double serial_block(int o, int l, F f) {
+  if (l < 8) {
+    double r = 0.0;
+    for (int i = 0; i < l; ++i) r += f(o + i);
+    return r;
+  }
+  double r0 = f(o), r1 = f(o + 1), r2 = f(o + 2), r3 = f(o + 3);
+  double r4 = f(o + 4), r5 = f(o + 5), r6 = f(o + 6), r7 = f(o + 7);
+  int i = 8;
+  const int m = l - (l & 7);
+  for (; i < m; i += 8) {
+    r0 += f(o + i); r1 += f(o + i + 1); r2 += f(o + i + 2); r3 += f(o + i + 3);
+    r4 += f(o + i + 4); r5 += f(o + i + 5); r6 += f(o + i + 6); r7 += f(o + i + 7);
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < l; ++i) res += f(o + i);
+  return res;
+}
+
+template <class F>
+__device__ double serial_pairwise(int off0, int cl, F f) {
+  if (cl <= kLeafMax) return serial_block(off0, cl, f);
+  int foff[16], flen[16], fst[16];
+  double facc[16];
+  int sp = 1;
+  foff[0] = off0; flen[0] = cl; fst[0] = 0;
+  for (;;) {
+    int t = sp - 1;
+    if (flen[t] > kLeafMax && fst[t] == 0) {
+      int h = flen[t] / 2;
+      h -= h % 8;
+      fst[t] = 1;
+      foff[sp] = foff[t]; flen[sp] = h; fst[sp] = 0;
+      ++sp;
+      continue;
+    }
+    double val = serial_block(foff[t], flen[t], f);
+    --sp;
+    for (;;) {
+      if (sp == 0) return val;
+      int u = sp - 1;
+      if (fst[u] == 1) {
+        int h = flen[u] / 2;
+        h -= h % 8;
+        facc[u] = val;
+        fst[u] = 2;
+        foff[sp] = foff[u] + h; flen[sp] = flen[u] - h; fst[sp] = 0;
+        ++sp;
+        break;
+      }
+      val = facc[u] + val;
+      --sp;
+    }
+  }
+}
+
+// np.add.reduce over f(0..n) (one thread).
+template <class F>
+__device__ double np_sum(int n, F f) {
+  double total = 0.0;
+  for (int o = 0; o < n; o += kNpyBuf) total += serial_pairwise(o, min(kNpyBuf, n - o), f);
+  return total;
+}
+
+// --------------------------------------------------------------------------
+// per-contig state
+// --------------------------------------------------------------------------
+
+struct Contig {
+  int64_t h0, l0, mbase;
+  int H, G;
+  // persistent
+  int *loc_lo, *loc_len, *loc_st, *leaf_off;
+  int4* leaves;
+  int *alo, *ahi, *ahit, *aloc, *acl;
+  double* asc;
+  uint64_t* maxes;
+  int *ign, *um;
+  // per level
+  uint64_t* keys;
+  int *seg_start, *seg_cl, *cl_id, *cl_sibp, *cl_flag, *pot, *mem1, *mem2;
+  double *S, *cl_rank, *cl_crit;
+  uint64_t* mask;
+  unsigned *bm1, *bm2;
+  uint8_t* best_syn;
+};
+
+// Exact site-score mean of one (clade, locus) segment, computed by one wave:
+// 8 leaves x 8 strided accumulators per pass, leaf sums combined in numpy's tree order.
+__device__ double wave_site_sum(const Contig& C, int g, int kb, int ke, double* lsum) {
+  const int lane = lane_id(), grp = lane >> 3, ch = lane & 7;
+  const int n = C.loc_len[g];
+  const int4* lv = C.leaves + C.leaf_off[g];
+  const int nl_total = C.leaf_off[g + 1] - C.leaf_off[g];
+  const int k = ke - kb;
+  int lo0 = 0, hi0 = 0;
+  double sc0 = 0.0;
+  if (k == 1) {
+    int a = (int)(C.keys[kb] & 0xFFFFFFull);
+    lo0 = C.alo[a]; hi0 = C.ahi[a]; sc0 = C.asc[a];
+  }
+  auto V = [&](int x) -> double {
+    if (k == 1) return (x >= lo0 && x < hi0) ? sc0 : 0.0;
+    double v = 0.0;
+    for (int t = kb; t < ke; ++t) {
+      int a = (int)(C.keys[t] & 0xFFFFFFull);
+      if (x >= C.alo[a] && x < C.ahi[a]) {
+        double s = C.asc[a];
+        v = s > v ? s : v;
+      }
+    }
+    return v;
+  };
+  double total = 0.0;
+  int leaf0 = 0;
+  for (int o = 0; o < n; o += kNpyBuf) {
+    const int cl = min(kNpyBuf, n - o);
+    const int nl = (cl == kNpyBuf) ? 64 : nl_total - leaf0;
+    for (int base = 0; base < nl; base += 8) {
+      const int leaf = base + grp;
+      double r = 0.0;
+      int st = 0, ln = 0;
+      if (leaf < nl) {
+        int4 e = lv[leaf0 + leaf];
+        st = e.x; ln = e.y;
+        const int m = ln >> 3;
+        if (m > 0) {
+          const int x = st + ch;
+          r = V(x);
+          for (int t = 1; t < m; ++t) r += V(x + 8 * t);
+        }
+      }
+      r += __shfl_xor(r, 1, 64);
+      r += __shfl_xor(r, 2, 64);
+      r += __shfl_xor(r, 4, 64);
+      if (ch == 0 && leaf < nl) {
+        for (int x = st + (ln & ~7); x < st + ln; ++x) r += V(x);
+        lsum[leaf] = r;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) total += combine_leaves(lv + leaf0, nl, lsum);
+    __builtin_amdgcn_wave_barrier();
+    leaf0 += nl;
+  }
+  return total;
+}
+
+// --- two-clade option evaluation (orgscorer.py:511-545, 678-744), one thread ---------
+struct OptEval {
+  int ok, swapped, dir, same, c1p, c2p;
+};
+
+__device__ __forceinline__ uint8_t two_char(const KArgs& K, const Contig& C, int pa, int pb,
+                                            bool unk, int g) {
+  const DevParams& P = K.p;
+  if (C.ign[g]) return '~';
+  double s1 = C.S[(int64_t)pa * C.G + g], s2 = C.S[(int64_t)pb * C.G + g];
+  double mn = s2 < s1 ? s2 : s1;
+  if (mn >= P.k_amb && !unk) return '*';
+  if (s1 >= P.k2) return 'A';
+  if (s2 >= P.k2) return 'B';
+  return '!';
+}
+
+__device__ OptEval eval_two(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
+                            const uint8_t* best, uint8_t* out) {
+  const DevParams& P = K.p;
+  const int G = C.G;
+  const bool unk = C.cl_id[pa] == K.unknown || C.cl_id[pb] == K.unknown;
+  OptEval e;
+  e.swapped = 0;
+  for (int g = 0; g < G; ++g) {  // "^[^A]*B" -> swap (orgscorer.py:537-540)
+    uint8_t c = two_char(K, C, pa, pb, unk, g);
+    if (c == 'A') break;
+    if (c == 'B') { e.swapped = 1; break; }
+  }
+  auto fin = [&](int g) -> uint8_t {
+    uint8_t c = two_char(K, C, pa, pb, unk, g);
+    if (e.swapped) c = (c == 'A') ? 'B' : (c == 'B' ? 'A' : c);
+    return c;
+  };
+  int state = 0, nA = 0, nB = 0;
+  bool dir_ok = true;
+  int64_t tot = 0, amb = 0;
+  e.same = 1;
+  for (int g = 0; g < G; ++g) {
+    uint8_t c = fin(g);
+    if (out) out[g] = c;
+    if (best && best[g] != c) e.same = 0;
+    const int len = C.loc_len[g];
+    if (c == 'A') { ++nA; tot += len; }
+    else if (c == 'B') { ++nB; tot += len; }
+    else if (c == '*') { tot += len; amb += len; }
+    if (c != '~') {  // "^A+B+A+$" on synteny without '~' (orgscorer.py:542)
+      if (state == 0) { if (c == 'A') state = 1; else dir_ok = false; }
+      else if (state == 1) { if (c == 'B') state = 2; else if (c != 'A') dir_ok = false; }
+      else if (state == 2) { if (c == 'A') state = 3; else if (c != 'B') dir_ok = false; }
+      else { if (c != 'A') dir_ok = false; }
+    }
+  }
+  e.dir = (dir_ok && state == 3) ? 1 : 0;
+  e.c1p = e.swapped ? pb : pa;
+  e.c2p = e.swapped ? pa : pb;
+  e.ok = 1;
+  // check_ambiguous_fraction (:693-702): total > 0 whenever crit >= k2 on >= 1 locus
+  if ((double)amb / (double)tot > P.amb_frac) e.ok = 0;
+  // check_clade_genes (:704-708)
+  if (P.clade_genes >= 0 && min(nA, nB) < P.clade_genes) e.ok = 0;
+  const int X = C.cl_id[e.c1p], Y = C.cl_id[e.c2p];
+  // check_clade_leaves (:710-715); recip = clade2 when the direction is known
+  if (P.clade_leaves >= 0) {
+    int64_t lc = e.dir ? K.leaves[Y] : min(K.leaves[X], K.leaves[Y]);
+    if (lc < P.clade_leaves) e.ok = 0;
+  }
+  // check_sister_penalty (:717-744): fail iff a checked locus has a present sister clade
+  // (other than the pair) scoring >= threshold there
+  if (P.sister_on && e.ok) {
+    const int px = K.parent[X], py = K.parent[Y];
+    for (int g = 0; g < G && e.ok; ++g) {
+      uint8_t c = fin(g);
+      int need;
+      if (c == 'B') need = px;
+      else if (c == 'A' && !e.dir) need = py;
+      else continue;
+      for (int q = 0; q < Pcount; ++q) {
+        if (C.cl_sibp[q] != need) continue;
+        int s = C.cl_id[q];
+        if (s == X || s == Y) continue;
+        if (C.S[(int64_t)q * G + g] >= P.sister_thr) { e.ok = 0; break; }
+      }
+    }
+  }
+  return e;
+}
+
+__device__ double pair_rank(const Contig& C, int pa, int pb, int Gu) {
+  const double* ra = C.S + (int64_t)pa * C.G;
+  const double* rb = C.S + (int64_t)pb * C.G;
+  return np_sum(Gu, [&](int u) {
+           double a = ra[C.um[u]], b = rb[C.um[u]];
+           return a < b ? b : a;
+         }) / (double)Gu;
+}
+
+__device__ double pair_crit(const Contig& C, int pa, int pb, int Gu) {
+  const double* ra = C.S + (int64_t)pa * C.G;
+  const double* rb = C.S + (int64_t)pb * C.G;
+  double m = 0.0;
+  for (int u = 0; u < Gu; ++u) {
+    double a = ra[C.um[u]], b = rb[C.um[u]];
+    double x = a < b ? b : a;
+    m = (u == 0 || x < m) ? x : m;
+  }
+  return m;
+}
+
+// --------------------------------------------------------------------------
+// the contig workgroup
+// --------------------------------------------------------------------------
+
+template <bool BIG>
+__device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap, Ctl& ctl,
+                               double (*lsum)[kLeafSlots]) {
+  const int tid = threadIdx.x, w = wave_id();
+  const DevParams& P = K.p;
+  const int nsys = K.n_sys;
+  Contig C;
+  C.h0 = K.hit_off[c];
+  C.H = (int)(K.hit_off[c + 1] - C.h0);
+  C.l0 = K.loc_off[c];
+  C.G = (int)(K.loc_off[c + 1] - C.l0);
+  C.mbase = 2 * C.h0 + 2 * (int64_t)c;
+  const int H = C.H, G = C.G;
+
+  if (tid == 0) {
+    ctl.overflow = 0; ctl.status = 0; ctl.need = 0;
+    K.call[c] = WF_CALL_UNCLASSIFIED;
+    K.crit[c] = 0.0; K.rank[c] = 0.0; K.c1[c] = -1; K.c2[c] = -1; K.dir[c] = 0;
+    K.iters[c] = 0; K.nm1[c] = 0; K.nm2[c] = 0; K.pair_evals[c] = 0; K.status[c] = 0;
+    K.need[c] = 0;
+  }
+  for (int i = tid; i < G * nsys; i += kBlock) K.annot[C.l0 * nsys + i] = -1;
+  if (H == 0 || G == 0) return;  // never evaluated -> unclassified (orgscorer.py:959)
+
+  Arena ar{abase, acap, 0};
+  // ---- loci and their pairwise-sum leaf tables ------------------------------------
+  C.loc_lo = ar.take<int>(G);
+  C.loc_len = ar.take<int>(G);
+  C.loc_st = ar.take<int>(G);
+  C.leaf_off = ar.take<int>(G + 1);
+  C.maxes = ar.take<uint64_t>(G);
+  C.ign = ar.take<int>(G);
+  C.um = ar.take<int>(G);
+  if (!ar.fits()) {
+    if (tid == 0) { ctl.overflow = 1; ctl.need = ar.used + 4096; }
+    __syncthreads();
+    return;
+  }
+  for (int g = tid; g < G; g += kBlock) {
+    int s = K.lstart[C.l0 + g], e = K.lend[C.l0 + g];
+    int lo = min(s, e), hi = max(s, e);
+    C.loc_lo[g] = lo;
+    C.loc_len[g] = hi - lo + 1;                 // len(Locus) (utils.py:321-322)
+    C.loc_st[g] = K.lstrand[C.l0 + g];
+    C.leaf_off[g + 1] = leaves_of_length(hi - lo + 1);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    C.leaf_off[0] = 0;
+    for (int g = 0; g < G; ++g) C.leaf_off[g + 1] += C.leaf_off[g];
+    ctl.cnt = C.leaf_off[G];
+  }
+  __syncthreads();
+  const int NL = ctl.cnt;
+  C.leaves = ar.take<int4>(NL);
+
+  // ---- attach hits to loci: count (orgscorer.py:359-369, :559-564; utils.py:487-500) ---
+  auto attaches = [&](int qlo, int qhi, int hs, int g) -> bool {
+    if (P.stranded && hs != C.loc_st[g]) return false;
+    const int l1 = C.loc_lo[g], l2 = l1 + C.loc_len[g] - 1;
+    if (l1 > qhi || qlo > l2) return 0.0 >= P.min_overlap;   // calc_overlap -> int 0
+    const int ov = min(qhi, l2) - max(qlo, l1) + 1;
+    const int den = min(qhi - qlo + 1, l2 - l1 + 1);
+    return (double)ov / (double)den >= P.min_overlap;
+  };
+  int local = 0;
+  for (int i = tid; i < H; i += kBlock) {
+    const int64_t hi_ = C.h0 + i;
+    if (!(K.scov[hi_] >= P.min_scov)) continue;
+    const int qlo = K.qlo[hi_], qhi = K.qhi[hi_], hs = K.hstrand[hi_];
+    for (int g = 0; g < G; ++g) local += attaches(qlo, qhi, hs, g) ? 1 : 0;
+  }
+  int A;
+  int off = block_scan(local, &A, ctl);
+  const int virt = (P.weak == 2) ? 1 : 0;       // assign-unknown adds "Unknown" (:416-418)
+  const int A1 = A + virt;
+  C.alo = ar.take<int>(A);
+  C.ahi = ar.take<int>(A);
+  C.ahit = ar.take<int>(A);
+  C.aloc = ar.take<int>(A);
+  C.acl = ar.take<int>(A);
+  C.asc = ar.take<double>(A);
+  if (!ar.fits() || A >= (1 << 24) || G >= kLocVirtual) {
+    if (tid == 0) {
+      ctl.overflow = 1;
+      ctl.status = (A >= (1 << 24) || G >= kLocVirtual) ? WF_E_BADINPUT : 0;
+      ctl.need = ar.used + (int64_t)A1 * (48 + 8 * G) + 8192;
+    }
+    __syncthreads();
+    return;
+  }
+  // leaf tables
+  for (int g = tid; g < G; g += kBlock) {
+    int k = C.leaf_off[g];
+    const int n = C.loc_len[g];
+    for (int o = 0; o < n; o += kNpyBuf) k += gen_leaves(o, min(kNpyBuf, n - o), C.leaves + k);
+  }
+  // ---- attach: fill, with the python-slice site range (orgscorer.py:371-382) ---------
+  for (int i = tid; i < H; i += kBlock) {
+    const int64_t hi_ = C.h0 + i;
+    if (!(K.scov[hi_] >= P.min_scov)) continue;
+    const int qlo = K.qlo[hi_], qhi = K.qhi[hi_], hs = K.hstrand[hi_];
+    for (int g = 0; g < G; ++g) {
+      if (!attaches(qlo, qhi, hs, g)) continue;
+      const int len = C.loc_len[g], l1 = C.loc_lo[g];
+      const int h1 = max(0, qlo - l1);
+      const int h2 = min(len - 1, qhi - l1);
+      const int start = min(h1, len);
+      int stop = h2 + 1;                         // site[h1:h2+1], python slice rules
+      if (stop < 0) { stop += len; if (stop < 0) stop = 0; }
+      C.alo[off] = start;
+      C.ahi[off] = stop;                         // empty when stop <= start
+      C.ahit[off] = i;
+      C.aloc[off] = g;
+      C.acl[off] = K.taxon[hi_];
+      C.asc[off] = K.score[hi_];
+      ++off;
+    }
+  }
+  __syncthreads();
+  const int64_t persist_mark = ar.used;
+
+  // ---- annotation transfer (orgscorer.py:383-392): per (locus, system) the last hit in
+  // file order whose score equals the running maximum >= threshold ---------------------
+  if (nsys > 0) {
+    uint64_t* abest = ar.take<uint64_t>((int64_t)G * nsys);
+    int* aidx = ar.take<int>((int64_t)G * nsys);
+    if (!ar.fits()) {
+      if (tid == 0) { ctl.overflow = 1; ctl.need = ar.used + (int64_t)A1 * (48 + 8 * G) + 8192; }
+      __syncthreads();
+      return;
+    }
+    for (int i = tid; i < G * nsys; i += kBlock) { abest[i] = 0; aidx[i] = -1; }
+    __syncthreads();
+    for (int a = tid; a < A; a += kBlock) {
+      const uint32_t m = K.sysmask[C.h0 + C.ahit[a]];
+      const double s = C.asc[a];
+      if (m == 0 || !(s >= P.annot_ref)) continue;
+      for (int b = 0; b < nsys; ++b)
+        if (m & (1u << b)) atomicMax((unsigned long long*)&abest[C.aloc[a] * nsys + b], dbits(s));
+    }
+    __syncthreads();
+    for (int a = tid; a < A; a += kBlock) {
+      const uint32_t m = K.sysmask[C.h0 + C.ahit[a]];
+      const double s = C.asc[a];
+      if (m == 0 || !(s >= P.annot_ref)) continue;
+      for (int b = 0; b < nsys; ++b)
+        if ((m & (1u << b)) && abest[C.aloc[a] * nsys + b] == dbits(s))
+          atomicMax(&aidx[C.aloc[a] * nsys + b], C.ahit[a]);
+    }
+    __syncthreads();
+    for (int i = tid; i < G * nsys; i += kBlock)
+      K.annot[C.l0 * nsys + i] = aidx[i] >= 0 ? (int)(C.h0 + aidx[i]) : -1;
+    __syncthreads();
+    ar.used = persist_mark;
+  }
+
+  // ---- initial jumps (orgscorer.py:955-957) ---------------------------------------
+  if (P.jump > 0) {
+    for (int a = tid; a < A; a += kBlock) {
+      int x = C.acl[a];
+      for (int j = 0; j < P.jump; ++j) x = K.parent[x];
+      C.acl[a] = x;
+    }
+  }
+  __syncthreads();
+
+  int iteration = 1;
+  bool first = true;
+  int64_t pair_evals = 0;
+  double* my_lsum = lsum[w];
+
+  for (;;) {
+    // ================= build the gene-score matrix of this level ===================
+    ar.used = persist_mark;
+    int npow = 1;
+    while (npow < A1) npow <<= 1;
+    C.keys = ar.take<uint64_t>(npow);
+    C.seg_start = ar.take<int>(A1 + 1);
+    C.seg_cl = ar.take<int>(A1 + 1);
+    C.cl_id = ar.take<int>(A1 + 1);
+    if (!ar.fits()) {
+      if (tid == 0) { ctl.overflow = 1; ctl.need = ar.used + (int64_t)A1 * (48 + 8 * G) + 8192; }
+      __syncthreads();
+      return;
+    }
+    for (int t = tid; t < npow; t += kBlock) {
+      uint64_t key = kKeyPad;
+      if (t < A)
+        key = ((uint64_t)(uint32_t)C.acl[t] << 40) | ((uint64_t)C.aloc[t] << 24) | (uint64_t)t;
+      else if (t < A1)
+        key = ((uint64_t)(uint32_t)K.unknown << 40) | ((uint64_t)kLocVirtual << 24) | 0xFFFFFFull;
+      C.keys[t] = key;
+    }
+    __syncthreads();
+    bitonic_sort(C.keys, npow);
+    // segments = distinct (clade, locus); clades = distinct clade (sorted = name order)
+    {
+      const int per = (A1 + kBlock - 1) / kBlock;
+      const int b = min(A1, tid * per), e = min(A1, b + per);
+      int ns = 0, nc = 0;
+      for (int t = b; t < e; ++t) {
+        const uint64_t k = C.keys[t];
+        if (t == 0 || (k >> 24) != (C.keys[t - 1] >> 24)) ++ns;
+        if (t == 0 || (k >> 40) != (C.keys[t - 1] >> 40)) ++nc;
+      }
+      int ps, pc, ts, tc;
+      block_scan2(ns, nc, &ps, &pc, &ts, &tc, ctl);
+      int si = ps - 1, ci = pc - 1;
+      for (int t = b; t < e; ++t) {
+        const uint64_t k = C.keys[t];
+        if (t == 0 || (k >> 40) != (C.keys[t - 1] >> 40)) {
+          ++ci;
+          const int id = (int)(k >> 40);
+          C.cl_id[ci] = id;
+          if (id == K.unknown) ctl.p_unk = ci;
+        }
+        if (t == 0 || (k >> 24) != (C.keys[t - 1] >> 24)) {
+          ++si;
+          C.seg_start[si] = t;
+          C.seg_cl[si] = ci;
+        }
+      }
+      if (tid == 0) {
+        ctl.S_n = ts;
+        ctl.P = tc;
+        C.seg_start[ts] = A1;
+      }
+    }
+    __syncthreads();
+    const int S_n = ctl.S_n, Pn = ctl.P;
+    C.S = ar.take<double>((int64_t)Pn * G);
+    C.cl_sibp = ar.take<int>(Pn);
+    C.cl_rank = ar.take<double>(Pn);
+    C.cl_crit = ar.take<double>(Pn);
+    C.cl_flag = ar.take<int>(Pn);
+    C.pot = ar.take<int>(Pn);
+    C.mask = ar.take<uint64_t>(Pn);
+    C.mem1 = ar.take<int>(Pn);
+    C.mem2 = ar.take<int>(Pn);
+    C.bm1 = ar.take<unsigned>((Pn + 31) / 32);
+    C.bm2 = ar.take<unsigned>((Pn + 31) / 32);
+    C.best_syn = ar.take<uint8_t>(G);
+    if (!ar.fits()) {
+      if (tid == 0) { ctl.overflow = 1; ctl.need = ar.used + (int64_t)A1 * (48 + 8 * G) + 8192; }
+      __syncthreads();
+      return;
+    }
+    for (int i = tid; i < Pn * G; i += kBlock) C.S[i] = 0.0;
+    for (int p = tid; p < Pn; p += kBlock) C.cl_sibp[p] = K.sibp[C.cl_id[p]];
+    for (int g = tid; g < G; g += kBlock) C.maxes[g] = 0;
+    if (tid == 0) ctl.root_present = 0;
+    __syncthreads();
+    for (int p = tid; p < Pn; p += kBlock)
+      if (C.cl_id[p] == K.root) ctl.root_present = 1;
+    // ---- site-score means (orgscorer.py:399-406), one wave per segment ---------------
+    for (int s = w; s < S_n; s += kWaves) {
+      const int kb = C.seg_start[s], ke = C.seg_start[s + 1];
+      const int g = (int)((C.keys[kb] >> 24) & 0xFFFF);
+      if (g == kLocVirtual) continue;
+      const double total = wave_site_sum(C, g, kb, ke, my_lsum);
+      if (lane_id() == 0) C.S[(int64_t)C.seg_cl[s] * G + g] = total / (double)C.loc_len[g];
+    }
+    __syncthreads();
+    // ---- per-locus max over known clades, weak loci (:407-427) ----------------------
+    for (int i = tid; i < Pn * G; i += kBlock) {
+      if (C.cl_id[i / G] == K.unknown) continue;
+      const double v = C.S[i];
+      if (v > 0.0) atomicMax((unsigned long long*)&C.maxes[i % G], dbits(v));
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int Gu = 0;
+      for (int g = 0; g < G; ++g) {
+        const double m = __longlong_as_double((long long)C.maxes[g]);
+        int ig = 0;
+        if (P.weak == 0) ig = !(m >= P.kmin);
+        else if (P.weak == 2) C.S[(int64_t)ctl.p_unk * G + g] = 1.0 - m;
+        C.ign[g] = ig;
+        if (!ig) C.um[Gu++] = g;
+      }
+      ctl.Gu = Gu;
+      ctl.all_ignored = (Gu == 0);
+    }
+    __syncthreads();
+    const int Gu = ctl.Gu;
+    if (first) {
+      first = false;
+      if (ctl.all_ignored) return;   // skipped contig (orgscorer.py:959) -> unclassified
+    }
+    if (Gu == 0) {                   // np.min of an empty array upstream
+      if (tid == 0) ctl.status = WF_E_EMPTYMASK;
+      __syncthreads();
+      break;
+    }
+
+    // ================= explain_one (orgscorer.py:585-597) ============================
+    {
+      double br = -__builtin_inf();
+      long long bk = -1;
+      for (int p = tid; p < Pn; p += kBlock) {
+        const double* row = C.S + (int64_t)p * G;
+        double crit = row[C.um[0]];
+        for (int u = 1; u < Gu; ++u) { double v = row[C.um[u]]; crit = v < crit ? v : crit; }
+        const double rank = np_sum(Gu, [&](int u) { return row[C.um[u]]; }) / (double)Gu;
+        const int opt = crit >= P.k1;
+        C.cl_crit[p] = crit;
+        C.cl_rank[p] = rank;
+        C.cl_flag[p] = opt;
+        if (opt && better(rank, p, br, bk)) { br = rank; bk = p; }
+      }
+      block_argmax(br, bk, ctl);
+      if (bk >= 0) {
+        // meld_one (:621-631): options within --range of the best
+        const int bp = (int)bk;
+        if (tid == 0) ctl.cnt = 0;
+        __syncthreads();
+        if (P.dis1 == 1) {
+          for (int p = tid; p < Pn; p += kBlock)
+            if (C.cl_flag[p] && (br - C.cl_rank[p]) <= P.range) {
+              const int slot = atomicAdd(&ctl.cnt, 1);
+              C.mem1[slot] = C.cl_id[p];
+            }
+        }
+        __syncthreads();
+        const int m = ctl.cnt;
+        if (P.dis1 == 1 && m == 0) {   // negative --range: get_lca() of nothing raises upstream
+          if (tid == 0) K.status[c] = WF_E_BADINPUT;
+          return;
+        }
+        const int lca = (P.dis1 == 1) ? block_lca(K, C.mem1, m, ctl) : C.cl_id[bp];
+        for (int i = tid; i < m; i += kBlock) K.meld[C.mbase + i] = C.mem1[i];
+        for (int g = tid; g < G; g += kBlock) {  // set_synteny_one (:495-509) of the best
+          const double s = C.S[(int64_t)bp * G + g];
+          K.syn[C.l0 + g] = C.ign[g] ? '~' : (s >= P.k1 ? 'A' : '!');
+        }
+        if (tid == 0) {
+          K.call[c] = WF_CALL_NO_LGT;
+          K.crit[c] = C.cl_crit[bp];
+          K.rank[c] = br;
+          K.c1[c] = lca;
+          K.c2[c] = -1;
+          K.nm1[c] = m;
+          K.iters[c] = (int16_t)iteration;
+          K.pair_evals[c] = pair_evals;
+        }
+        return;
+      }
+    }
+
+    // ================= explain_two (orgscorer.py:599-619) ============================
+    {
+      // potential clades: max over ALL loci >= k2 (:603-605)
+      int flag_local = 0;
+      const int per = (Pn + kBlock - 1) / kBlock;
+      const int pb0 = min(Pn, tid * per), pe0 = min(Pn, pb0 + per);
+      for (int p = pb0; p < pe0; ++p) {
+        const double* row = C.S + (int64_t)p * G;
+        double mx = row[0];
+        for (int g = 1; g < G; ++g) mx = row[g] > mx ? row[g] : mx;
+        C.cl_flag[p] = mx >= P.k2;
+        flag_local += C.cl_flag[p];
+      }
+      int Pp;
+      int pos = block_scan(flag_local, &Pp, ctl);
+      for (int p = pb0; p < pe0; ++p)
+        if (C.cl_flag[p]) C.pot[pos++] = p;
+      pair_evals += (int64_t)Pp * (Pp - 1) / 2;
+      const bool use_mask = Gu <= 64;
+      const uint64_t full = (Gu >= 64) ? ~0ull : ((1ull << Gu) - 1ull);
+      __syncthreads();
+      if (use_mask) {
+        for (int i = tid; i < Pp; i += kBlock) {
+          const double* row = C.S + (int64_t)C.pot[i] * G;
+          uint64_t m = 0;
+          for (int u = 0; u < Gu; ++u)
+            if (row[C.um[u]] >= P.k2) m |= 1ull << u;
+          C.mask[i] = m;
+        }
+      }
+      __syncthreads();
+      // pass 1: best pair over all pairs clade1 < clade2 (name order == index order)
+      double br = -__builtin_inf();
+      long long bk = -1;
+      auto candidate = [&](int i, int j) -> bool {
+        if (use_mask) return (C.mask[i] | C.mask[j]) == full;
+        return pair_crit(C, C.pot[i], C.pot[j], Gu) >= P.k2;
+      };
+      for (int i = w; i < Pp; i += kWaves) {
+        for (int j = i + 1 + lane_id(); j < Pp; j += 64) {
+          if (!candidate(i, j)) continue;
+          const double r = pair_rank(C, C.pot[i], C.pot[j], Gu);
+          const long long key = (long long)i * Pp + j;
+          if (better(r, key, br, bk)) { br = r; bk = key; }
+        }
+      }
+      block_argmax(br, bk, ctl);
+      bool have_ok = false;
+      if (bk >= 0) {
+        const int bi = (int)(bk / Pp), bj = (int)(bk % Pp);
+        for (int i = tid; i < (Pn + 31) / 32; i += kBlock) { C.bm1[i] = 0; C.bm2[i] = 0; }
+        if (tid == 0) {
+          OptEval e = eval_two(K, C, Pn, C.pot[bi], C.pot[bj], nullptr, C.best_syn);
+          ctl.best_ok = e.ok; ctl.best_dir = e.dir;
+          ctl.best_c1p = e.c1p; ctl.best_c2p = e.c2p;
+          ctl.best_crit = pair_crit(C, C.pot[bi], C.pot[bj], Gu);
+          ctl.n_in = 0; ctl.all_ok = 1; ctl.all_same = 1;
+        }
+        __syncthreads();
+        // pass 2: options within --range of the best get the LGT filters (:636-639)
+        for (int i = w; i < Pp; i += kWaves) {
+          for (int j = i + 1 + lane_id(); j < Pp; j += 64) {
+            if (!candidate(i, j)) continue;
+            const double r = pair_rank(C, C.pot[i], C.pot[j], Gu);
+            if (!((br - r) <= P.range)) continue;
+            OptEval e = eval_two(K, C, Pn, C.pot[i], C.pot[j], C.best_syn, nullptr);
+            atomicAdd(&ctl.n_in, 1);
+            if (!e.ok) atomicAnd(&ctl.all_ok, 0);
+            if (!e.same) atomicAnd(&ctl.all_same, 0);
+            atomicOr(&C.bm1[e.c1p >> 5], 1u << (e.c1p & 31));
+            atomicOr(&C.bm2[e.c2p >> 5], 1u << (e.c2p & 31));
+          }
+        }
+        __syncthreads();
+        // meld_two (:640-669)
+        if (tid == 0) {
+          int kind;   // 0 none, 1 best as is, 2 meld, 3 unchecked best, 4 upstream crash
+          if (ctl.n_in == 0) kind = (P.dis2 == 0) ? 3 : (P.dis2 == 1 ? 0 : 4);  // --range < 0
+          else if (ctl.n_in == 1 || P.dis2 == 0) kind = 1;
+          else if (P.dis2 == 1) kind = 0;
+          else kind = (ctl.all_ok && ctl.all_same) ? 2 : 0;
+          ctl.res_kind = kind;
+          ctl.cnt = 0;
+          ctl.cnt2 = 0;
+        }
+        __syncthreads();
+        const int kind = ctl.res_kind;
+        if (kind == 4) {
+          if (tid == 0) K.status[c] = WF_E_BADINPUT;
+          return;
+        }
+        int lca1 = -1, lca2v = -1, m1 = 0, m2 = 0;
+        if (kind == 2) {
+          for (int p = tid; p < Pn; p += kBlock) {
+            if (C.bm1[p >> 5] & (1u << (p & 31))) C.mem1[atomicAdd(&ctl.cnt, 1)] = C.cl_id[p];
+            if (C.bm2[p >> 5] & (1u << (p & 31))) C.mem2[atomicAdd(&ctl.cnt2, 1)] = C.cl_id[p];
+          }
+          __syncthreads();
+          m1 = ctl.cnt;
+          m2 = ctl.cnt2;
+          __syncthreads();
+          lca1 = block_lca(K, C.mem1, m1, ctl);
+          lca2v = block_lca(K, C.mem2, m2, ctl);
+          bool keep = true;
+          if (!P.allow_lca) {
+            const int nl = lca2(K, lca1, lca2v);
+            keep = !(nl == lca1 || nl == lca2v);
+          }
+          have_ok = keep;   // melded options are all OK
+        } else if (kind == 1) {
+          have_ok = ctl.best_ok != 0;
+        } else if (kind == 3) {
+          have_ok = true;
+        }
+        if (have_ok) {
+          for (int g = tid; g < G; g += kBlock) K.syn[C.l0 + g] = C.best_syn[g];
+          if (kind == 2) {
+            for (int i = tid; i < m1; i += kBlock) K.meld[C.mbase + i] = C.mem1[i];
+            for (int i = tid; i < m2; i += kBlock) K.meld[C.mbase + m1 + i] = C.mem2[i];
+          }
+          if (tid == 0) {
+            K.call[c] = WF_CALL_LGT;
+            K.crit[c] = ctl.best_crit;
+            K.rank[c] = br;
+            K.dir[c] = (int8_t)ctl.best_dir;
+            K.c1[c] = (kind == 2) ? lca1 : C.cl_id[ctl.best_c1p];
+            K.c2[c] = (kind == 2) ? lca2v : C.cl_id[ctl.best_c2p];
+            K.nm1[c] = (kind == 2) ? m1 : 0;
+            K.nm2[c] = (kind == 2) ? m2 : 0;
+            K.iters[c] = (int16_t)iteration;
+            K.pair_evals[c] = pair_evals;
+          }
+          return;
+        }
+      }
+    }
+
+    // ================= roll-up (orgscorer.py:571-581) ================================
+    if (Pn == 0 || ctl.root_present) break;
+    for (int a = tid; a < A; a += kBlock) C.acl[a] = K.parent[C.acl[a]];
+    ++iteration;
+    if (iteration > kMaxIter) {
+      if (tid == 0) ctl.status = WF_E_RUNAWAY;
+      __syncthreads();
+      break;
+    }
+    __syncthreads();
+  }
+  // unclassified after evaluation
+  if (tid == 0) {
+    K.iters[c] = (int16_t)min(iteration, 32767);
+    K.pair_evals[c] = pair_evals;
+    K.status[c] = ctl.status;
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kBlock) void k_contig_lds(KArgs K) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ Ctl ctl;
+  __shared__ double lsum[kWaves][kLeafSlots];
+  const int c = blockIdx.x;
+  process_contig<false>(K, c, smem, K.lds_bytes, ctl, lsum);
+  __syncthreads();
+  if (threadIdx.x == 0 && ctl.overflow) {
+    if (ctl.status != 0) {
+      K.status[c] = ctl.status;
+    } else {
+      const int slot = atomicAdd(K.ovf_count, 1);
+      K.ovf_list[slot] = c;
+      K.status[c] = kPending;
+      K.need[c] = ctl.need;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_contig_big(KArgs K) {
+  __shared__ Ctl ctl;
+  __shared__ double lsum[kWaves][kLeafSlots];
+  const int count = *K.work_count;
+  char* base = K.big_ws + (int64_t)blockIdx.x * K.slot_bytes;
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int c = K.work_list[i];
+    process_contig<true>(K, c, base, K.slot_bytes, ctl, lsum);
+    __syncthreads();
+    if (threadIdx.x == 0 && ctl.overflow) {
+      K.status[c] = ctl.status != 0 ? ctl.status : WF_E_NOMEM;
+      K.need[c] = ctl.need;
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_lds_kernel(const KArgs& k, hipStream_t s) {
+  if (k.n_contigs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_contig_lds, dim3(k.n_contigs), dim3(kBlock), (size_t)k.lds_bytes, s, k);
+  return hipGetLastError();
+}
+
+hipError_t launch_big_kernel(const KArgs& k, int grid, hipStream_t s) {
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_contig_big, dim3(grid), dim3(kBlock), 0, s, k);
+  return hipGetLastError();
+}
+
+}  // namespace wf

@@ -1,0 +1,202 @@
+"""Host driver: HostBatch -> libwaafle_hip -> per-contig result records.
+
+`score(batch, tax, params, gpus=N)` shards contigs over N devices (contiguous ranges
+balanced by an estimated cost; contigs are independent, so there is no exchange step
+and no collective) and runs one HIP context per device from its own host thread
+(ctypes releases the GIL for the duration of wf_score).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import lib as L
+
+DIS_ONE = {"report-best": 0, "meld": 1}
+DIS_TWO = {"report-best": 0, "jump": 1, "meld": 2}
+LEVEL = {"off": 0, "lenient": 1, "strict": 2}
+WEAK = {"ignore": 0, "penalize": 1, "assign-unknown": 2}
+
+
+def params_struct(p):
+    """argparse-style dict (cli.param_dict) -> wf_params."""
+    return L.WfParams(
+        k1=float(p["one_clade_threshold"]), k2=float(p["two_clade_threshold"]),
+        range=float(p["range"]), min_overlap=float(p["min_overlap"]),
+        min_scov=float(p["min_scov"]), ambiguous_fraction=float(p["ambiguous_fraction"]),
+        disambiguate_one=DIS_ONE[p["disambiguate_one"]],
+        disambiguate_two=DIS_TWO[p["disambiguate_two"]],
+        jump_taxonomy=int(p["jump_taxonomy"] or 0), allow_lca=int(bool(p["allow_lca"])),
+        ambiguous_threshold=LEVEL[p["ambiguous_threshold"]],
+        sister_penalty=LEVEL[p["sister_penalty"]],
+        clade_genes=-1 if p["clade_genes"] is None else int(p["clade_genes"]),
+        clade_leaves=-1 if p["clade_leaves"] is None else int(p["clade_leaves"]),
+        weak_loci=WEAK[p["weak_loci"]], annotation_threshold=LEVEL[p["annotation_threshold"]],
+        stranded=int(bool(p["stranded"])))
+
+
+@dataclass
+class Results:
+    call: np.ndarray
+    crit: np.ndarray
+    rank: np.ndarray
+    clade1: np.ndarray
+    clade2: np.ndarray
+    direction: np.ndarray
+    iterations: np.ndarray
+    synteny: np.ndarray
+    n_meld1: np.ndarray
+    n_meld2: np.ndarray
+    meld: np.ndarray
+    annot_hit: np.ndarray
+    pair_evals: np.ndarray
+    status: np.ndarray
+    need_bytes: np.ndarray
+
+    @classmethod
+    def empty(cls, n, n_hits, n_loci, n_sys):
+        return cls(call=np.zeros(n, np.int8), crit=np.zeros(n, np.float64),
+                   rank=np.zeros(n, np.float64), clade1=np.zeros(n, np.int32),
+                   clade2=np.zeros(n, np.int32), direction=np.zeros(n, np.int8),
+                   iterations=np.zeros(n, np.int16), synteny=np.zeros(n_loci, np.uint8),
+                   n_meld1=np.zeros(n, np.int32), n_meld2=np.zeros(n, np.int32),
+                   meld=np.zeros(2 * n_hits + 2 * n, np.int32),
+                   annot_hit=np.zeros(n_loci * n_sys, np.int32),
+                   pair_evals=np.zeros(n, np.int64), status=np.zeros(n, np.int32),
+                   need_bytes=np.zeros(n, np.int64))
+
+    def struct(self):
+        return L.WfResult(*[L.ptr(getattr(self, f)) for f, _ in L.WfResult._fields_])
+
+    @classmethod
+    def concat(cls, parts, hit_bases):
+        out = {}
+        for f in cls.__dataclass_fields__:
+            out[f] = np.concatenate([getattr(p, f) for p in parts])
+        # annotation winners are batch hit indices: rebase shard-local ones
+        ann = [np.where(p.annot_hit >= 0, p.annot_hit + b, -1).astype(np.int32)
+               for p, b in zip(parts, hit_bases)]
+        out["annot_hit"] = np.concatenate(ann) if ann else np.zeros(0, np.int32)
+        return cls(**out)
+
+
+def batch_struct(b):
+    return L.WfBatch(
+        n_contigs=b.n_contigs, n_systems=len(b.systems), n_hits=b.n_hits, n_loci=b.n_loci,
+        max_hits=b.max_hits, max_loci=b.max_loci, device_resident=0, _pad=0,
+        hit_off=L.ptr(b.hit_off), hit_qlo=L.ptr(b.hit_qlo), hit_qhi=L.ptr(b.hit_qhi),
+        hit_taxon=L.ptr(b.hit_taxon), hit_strand=L.ptr(b.hit_strand),
+        hit_score=L.ptr(b.hit_score), hit_scov=L.ptr(b.hit_scov),
+        hit_sysmask=L.ptr(b.hit_sysmask), loc_off=L.ptr(b.loc_off),
+        loc_start=L.ptr(b.loc_start), loc_end=L.ptr(b.loc_end), loc_strand=L.ptr(b.loc_strand))
+
+
+def taxonomy_struct(t):
+    return L.WfTaxonomy(n=len(t.names), parent=L.ptr(t.parent), depth=L.ptr(t.depth),
+                        sib_parent=L.ptr(t.sib_parent), leaf_count=L.ptr(t.leaf_count),
+                        root=t.root, unknown=t.unknown)
+
+
+class GpuScorer:
+    """One libwaafle_hip context on one device."""
+
+    def __init__(self, device=0, lds_bytes=None):
+        self.lib = L.load()
+        h = C.c_void_p()
+        rc = self.lib.wf_init(int(device), C.byref(h))
+        if rc != L.WF_OK:
+            raise L.WaafleHipError(rc, "wf_init(device={}) failed".format(device))
+        self.h = h
+        self.device = device
+        if lds_bytes:
+            self._check(self.lib.wf_set_lds_bytes(self.h, int(lds_bytes)))
+
+    def _check(self, rc):
+        if rc != L.WF_OK:
+            raise L.WaafleHipError(rc, self.lib.wf_last_error(self.h).decode())
+
+    def set_taxonomy(self, tax):
+        self._tax = taxonomy_struct(tax)
+        self._check(self.lib.wf_set_taxonomy(self.h, C.byref(self._tax)))
+
+    def score(self, batch, params):
+        res = Results.empty(batch.n_contigs, batch.n_hits, batch.n_loci, len(batch.systems))
+        bs, ps, rs = batch_struct(batch), params_struct(params), res.struct()
+        rc = self.lib.wf_score(self.h, C.byref(bs), C.byref(ps), C.byref(rs))
+        if rc != L.WF_OK:
+            bad = np.nonzero(res.status)[0]
+            msg = self.lib.wf_last_error(self.h).decode()
+            err = L.WaafleHipError(rc, msg)
+            err.contigs = bad
+            err.results = res
+            raise err
+        return res
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.wf_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def contig_cost(batch):
+    """Cost estimate per contig for balancing shards: hits x loci (attach + site work)."""
+    return np.diff(batch.hit_off).astype(np.float64) * np.maximum(
+        1, np.diff(batch.loc_off)).astype(np.float64) + 1.0
+
+
+def shard_bounds(cost, parts):
+    """Contiguous ranges with ~equal summed cost."""
+    n = len(cost)
+    if parts <= 1 or n == 0:
+        return [(0, n)]
+    cum = np.cumsum(cost)
+    total = cum[-1]
+    cuts = [0]
+    for k in range(1, parts):
+        cuts.append(int(np.searchsorted(cum, total * k / parts)))
+    cuts.append(n)
+    cuts = sorted(set(min(max(c, 0), n) for c in cuts))
+    return [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a] or [(0, n)]
+
+
+def score(batch, tax, params, gpus=1, lds_bytes=None):
+    gpus = max(1, int(gpus))
+    if gpus == 1:
+        s = GpuScorer(0, lds_bytes)
+        try:
+            s.set_taxonomy(tax)
+            return s.score(batch, params)
+        finally:
+            s.close()
+    bounds = shard_bounds(contig_cost(batch), gpus)
+    parts = [None] * len(bounds)
+    errors = []
+
+    def work(k, a, b):
+        try:
+            s = GpuScorer(k, lds_bytes)
+            try:
+                s.set_taxonomy(tax)
+                parts[k] = s.score(batch.slice(a, b), params)
+            finally:
+                s.close()
+        except Exception as exc:   # re-raised on the main thread
+            errors.append(exc)
+
+    threads = [threading.Thread(target=work, args=(k, a, b)) for k, (a, b) in enumerate(bounds)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+    return Results.concat(parts, [int(batch.hit_off[a]) for a, _ in bounds])

@@ -1,0 +1,110 @@
+"""ctypes binding of libwaafle_hip.so (include/waafle_hip.h).
+
+The product path has no CPU fallback: if the in-tree library is missing or cannot be
+loaded, `load()` raises.  Build it with `python -m waafle_amd.build`.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libwaafle_hip.so")
+
+WF_OK, WF_E_BADINPUT, WF_E_HIP, WF_E_RUNAWAY, WF_E_NOMEM, WF_E_STATE, WF_E_EMPTYMASK = \
+    0, -1, -2, -3, -4, -5, -6
+CALL_UNCLASSIFIED, CALL_NO_LGT, CALL_LGT = 0, 1, 2
+
+_P = C.c_void_p
+
+
+class WfTaxonomy(C.Structure):
+    _fields_ = [("n", C.c_int32), ("parent", _P), ("depth", _P), ("sib_parent", _P),
+                ("leaf_count", _P), ("root", C.c_int32), ("unknown", C.c_int32)]
+
+
+class WfParams(C.Structure):
+    _fields_ = [("k1", C.c_double), ("k2", C.c_double), ("range", C.c_double),
+                ("min_overlap", C.c_double), ("min_scov", C.c_double),
+                ("ambiguous_fraction", C.c_double), ("disambiguate_one", C.c_int32),
+                ("disambiguate_two", C.c_int32), ("jump_taxonomy", C.c_int32),
+                ("allow_lca", C.c_int32), ("ambiguous_threshold", C.c_int32),
+                ("sister_penalty", C.c_int32), ("clade_genes", C.c_int32),
+                ("clade_leaves", C.c_int32), ("weak_loci", C.c_int32),
+                ("annotation_threshold", C.c_int32), ("stranded", C.c_int32)]
+
+
+class WfBatch(C.Structure):
+    _fields_ = [("n_contigs", C.c_int32), ("n_systems", C.c_int32), ("n_hits", C.c_int64),
+                ("n_loci", C.c_int64), ("max_hits", C.c_int32), ("max_loci", C.c_int32),
+                ("device_resident", C.c_int32), ("_pad", C.c_int32),
+                ("hit_off", _P), ("hit_qlo", _P), ("hit_qhi", _P), ("hit_taxon", _P),
+                ("hit_strand", _P), ("hit_score", _P), ("hit_scov", _P), ("hit_sysmask", _P),
+                ("loc_off", _P), ("loc_start", _P), ("loc_end", _P), ("loc_strand", _P)]
+
+
+class WfResult(C.Structure):
+    _fields_ = [("call", _P), ("crit", _P), ("rank", _P), ("clade1", _P), ("clade2", _P),
+                ("direction", _P), ("iterations", _P), ("synteny", _P), ("n_meld1", _P),
+                ("n_meld2", _P), ("meld", _P), ("annot_hit", _P), ("pair_evals", _P),
+                ("status", _P), ("need_bytes", _P)]
+
+
+class WfTiming(C.Structure):
+    _fields_ = [("lds_kernel_ms", C.c_double), ("big_kernel_ms", C.c_double),
+                ("launches", C.c_int64), ("overflow_contigs", C.c_int64)]
+
+
+# every symbol the header declares, with its ctypes signature
+SIGNATURES = {
+    "wf_abi_version": (C.c_int, []),
+    "wf_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "wf_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "wf_free": (None, [C.c_void_p]),
+    "wf_last_error": (C.c_char_p, [C.c_void_p]),
+    "wf_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "wf_set_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
+    "wf_set_taxonomy": (C.c_int, [C.c_void_p, C.POINTER(WfTaxonomy)]),
+    "wf_score": (C.c_int, [C.c_void_p, C.POINTER(WfBatch), C.POINTER(WfParams),
+                           C.POINTER(WfResult)]),
+    "wf_synchronize": (C.c_int, [C.c_void_p]),
+    "wf_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "wf_timing_read": (C.c_int, [C.c_void_p, C.POINTER(WfTiming)]),
+}
+
+_lib = None
+
+
+class WaafleHipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libwaafle_hip error {}: {}".format(code, msg))
+        self.code = code
+
+
+def load(path=LIB_PATH):
+    """Load the in-tree HIP library (raises if it is absent -- no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError("{} not built: run `python -m waafle_amd.build` "
+                          "(the MI355X path has no CPU fallback)".format(path))
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.wf_abi_version() != 1:
+        raise ImportError("libwaafle_hip ABI mismatch")
+    _lib = lib
+    return lib
+
+
+def device_count():
+    lib = load()
+    n = C.c_int(0)
+    lib.wf_device_count(C.byref(n))
+    return n.value
+
+
+def ptr(a):
+    """Host numpy array -> void* (array must stay alive for the call)."""
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None

@@ -1,0 +1,52 @@
+"""`waafle_orgscorer` drop-in CLI (orgscorer.py:900-966) running on MI355X.
+
+    python -m waafle_amd.orgscorer contigs.fna hits.blastout genes.gff taxonomy.tsv [flags]
+
+Writes <basename>.lgt.tsv / .no_lgt.tsv / .unclassified.tsv exactly as the reference.
+"""
+import os
+import sys
+import time
+
+from . import cli, engine, inputs, lib, output
+
+
+def die(*args):
+    inputs.say(*(["LETHAL ERROR:"] + list(args)))
+    sys.exit("EXITING.")
+
+
+def main(argv=None):
+    args = cli.build_parser().parse_args(argv)
+    if args.write_details:
+        die("--write-details is not supported by this build (it raises on Python 3 upstream)")
+    say = (lambda *a: None) if args.quiet else inputs.say
+    t0 = time.time()
+    say("Loading inputs.")
+    try:
+        batch, tax = inputs.load_inputs(args.contigs, args.blastout, args.gff, args.taxonomy,
+                                        args.min_gene_length, warn=inputs.say)
+    except (inputs.InputError, ValueError) as exc:
+        die(str(exc))
+    if args.basename is None:
+        args.basename = inputs.basename_of(args.contigs)
+    say("Analyzing {:,} contigs ({:,} hits, {:,} loci) on {} GPU(s).".format(
+        batch.n_contigs, batch.n_hits, batch.n_loci, args.gpus))
+    t1 = time.time()
+    try:
+        res = engine.score(batch, tax, cli.param_dict(args), gpus=args.gpus)
+    except lib.WaafleHipError as exc:
+        if exc.code == lib.WF_E_RUNAWAY and len(getattr(exc, "contigs", ())):
+            die("  Warning: Runaway taxonomic recursion for",
+                batch.contig_names[int(exc.contigs[0])])
+        die(str(exc))
+    t2 = time.time()
+    say("Initializing outputs.")
+    rows = output.render(batch, tax, res)
+    output.write(rows, args.outdir, args.basename)
+    say("Finished successfully (parse {:.2f}s, score {:.3f}s, write {:.2f}s).".format(
+        t1 - t0, t2 - t1, time.time() - t2))
+
+
+if __name__ == "__main__":
+    main()

@@ -243,3 +243,56 @@ def write_text(data, outdir, basename="synth"):
         for child, parent in data.tax.edges:
             fh.write("{}\t{}\n".format(child, parent))
     return paths
+
+
+# ---------------------------------------------------------------------------
+# direct packing (identical arrays to parsing the text rendering)
+# ---------------------------------------------------------------------------
+
+def to_batch(data, min_gene_length=200.0, with_codes=True):
+    """SynthData -> (HostBatch, TaxonomyTables) without going through text files."""
+    from .inputs import HostBatch, derive_hit_values
+    from .taxonomy import TaxonomyTables
+
+    sp = data.tax.species
+    used = np.unique(data.hit_clade)
+    tax = TaxonomyTables(data.tax.edges, extra_names={sp[int(c)] for c in used})
+    clade_to_id = np.full(len(sp), -1, dtype=np.int32)
+    for c in used.tolist():
+        clade_to_id[c] = tax.index[sp[c]]
+    N = data.n_contigs
+    hit_off = np.zeros(N + 1, dtype=np.int64)
+    np.cumsum(np.bincount(data.hit_contig, minlength=N), out=hit_off[1:])
+    pident = data.pident_milli / 1000.0
+    scov, score = derive_hit_values(data.qlen, data.slen, data.qstart, data.qend, data.sstart,
+                                    data.send, pident, data.minus)
+    keep = (np.abs(data.loc_end - data.loc_start) + 1) >= min_gene_length
+    loc_contig = data.loc_contig[keep]
+    loc_off = np.zeros(N + 1, dtype=np.int64)
+    np.cumsum(np.bincount(loc_contig, minlength=N), out=loc_off[1:])
+    ls, le, lst = data.loc_start[keep], data.loc_end[keep], data.loc_strand[keep]
+    codes = []
+    if with_codes:
+        codes = ["{}:{}:{}".format(a, b, chr(c)) for a, b, c in
+                 zip(ls.tolist(), le.tolist(), lst.tolist())]
+    # one annotation system ("UniProt"), value "U<clade>x<gene mod 50>", interned in
+    # first-appearance order like the parser does
+    vkey = data.hit_clade * 50 + data.hit_gene % 50
+    uniq, first, inv = np.unique(vkey, return_index=True, return_inverse=True)
+    rank = np.empty(len(uniq), dtype=np.int32)
+    rank[np.argsort(first, kind="stable")] = np.arange(len(uniq), dtype=np.int32)
+    value_ids = rank[inv].reshape(-1, 1).astype(np.int32)
+    values = [None] * len(uniq)
+    for k, u in zip(rank.tolist(), uniq.tolist()):
+        values[k] = "U{}x{}".format(u // 50, u % 50)
+    batch = HostBatch(
+        contig_names=list(data.contig_names), contig_lengths=data.contig_lengths.copy(),
+        hit_off=hit_off, hit_qlo=np.minimum(data.qstart, data.qend).astype(np.int32),
+        hit_qhi=np.maximum(data.qstart, data.qend).astype(np.int32),
+        hit_taxon=clade_to_id[data.hit_clade], hit_strand=data.minus.astype(np.int8),
+        hit_score=score, hit_scov=scov, hit_sysmask=np.ones(data.n_hits, dtype=np.uint32),
+        loc_off=loc_off, loc_start=ls.astype(np.int32), loc_end=le.astype(np.int32),
+        loc_strand=np.where(lst == ord("-"), 1, np.where(lst == ord("+"), 0, 2)).astype(np.int8),
+        loc_codes=codes, systems=["UniProt"], annot_value_ids=value_ids,
+        annot_values=[values], hit_row=np.arange(data.n_hits, dtype=np.int64))
+    return batch, tax
