@@ -60,3 +60,41 @@ def run_oracle(paths, flags):
     from waafle_amd import cli
     params = orc.Params(**cli.param_dict(cli.parse_flags(flags)))
     return orc.run(*paths, params)
+
+
+class _Hit:
+    pass
+
+
+def oracle_hits_from_batch(b, tax):
+    """In-memory oracle hits for a packed batch (scores are already exact floats)."""
+    groups = []
+    for c, name in enumerate(b.contig_names):
+        hs = []
+        for i in range(int(b.hit_off[c]), int(b.hit_off[c + 1])):
+            h = _Hit()
+            h.qstart, h.qend = int(b.hit_qlo[i]), int(b.hit_qhi[i])
+            h.strand = "-" if b.hit_strand[i] else "+"
+            h.scov_mod = float(b.hit_scov[i])
+            h.score = float(b.hit_score[i])
+            h.taxon = tax.names[int(b.hit_taxon[i])]
+            vid = int(b.annot_value_ids[i, 0])
+            h.annotations = {"UniProt": b.annot_values[0][vid]} if vid >= 0 else {}
+            h.order = int(b.hit_row[i])
+            hs.append(h)
+        if hs:
+            groups.append((name, hs))
+    return groups
+
+
+def oracle_loci_from_batch(b):
+    groups = []
+    for c, name in enumerate(b.contig_names):
+        ls = []
+        for l in range(int(b.loc_off[c]), int(b.loc_off[c + 1])):
+            st = {0: "+", 1: "-"}.get(int(b.loc_strand[l]), ".")
+            ls.append(orc.GeneLocus([name, "x", "gene", str(int(b.loc_start[l])),
+                                     str(int(b.loc_end[l])), ".", st, "0", "."]))
+        if ls:
+            groups.append((name, ls))
+    return groups
