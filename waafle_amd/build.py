@@ -25,23 +25,31 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
-def up_to_date():
-    if not os.path.exists(LIB):
+STAMPS_LIB = os.path.join(HERE, "libwaafle_hip_stamps.so")   # diagnostic build only
+
+
+def up_to_date(lib=LIB):
+    if not os.path.exists(lib):
         return False
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force=False, verbose=True):
-    if not force and up_to_date():
-        return LIB
-    cmd = [hipcc()] + FLAGS + SOURCES + ["-o", LIB + ".tmp"]
+def build(force=False, verbose=True, stamps=False):
+    """Build the product library (or, with stamps=True, the per-phase timing variant)."""
+    lib = STAMPS_LIB if stamps else LIB
+    if not force and up_to_date(lib):
+        return lib
+    extra = ["-DWF_STAMPS"] if stamps else []
+    cmd = [hipcc()] + FLAGS + extra + SOURCES + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+    if "--stamps" in sys.argv:
+        build(force="--force" in sys.argv, stamps=True)

@@ -30,7 +30,7 @@ struct wf_ctx {
   DevBuf ovf_list, ovf_count;
   DevBuf retry_list, retry_count;
   DevBuf big_ws;
-  int64_t lds_bytes = 48 * 1024;
+  int64_t lds_bytes = 36 * 1024;   // 4 workgroups per CU (160 KiB LDS)
   int big_slots = 512;
   // staging for host-resident batches
   DevBuf b_hit_off, b_qlo, b_qhi, b_taxon, b_hstrand, b_score, b_scov, b_sysmask;

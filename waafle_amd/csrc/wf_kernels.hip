@@ -21,6 +21,24 @@ namespace wf {
 namespace {
 
 constexpr uint64_t kKeyPad = ~0ull;
+
+// Diagnostic build only (-DWF_STAMPS): thread 0 accumulates shader-clock deltas per phase,
+// always taken right after a workgroup barrier.  Never compiled into the product build.
+#ifdef WF_STAMPS
+__device__ unsigned long long g_stamps[32];
+#define STAMP_INIT() unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
+#define STAMP(i)                                                                    \
+  do {                                                                              \
+    if (threadIdx.x == 0) {                                                         \
+      unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+      atomicAdd(&g_stamps[i], now_ - t_last_);                                      \
+      t_last_ = now_;                                                               \
+    }                                                                               \
+  } while (0)
+#else
+#define STAMP_INIT() do {} while (0)
+#define STAMP(i) do {} while (0)
+#endif
 constexpr int kLocVirtual = 0xFFFF;     // locus field of the virtual "Unknown" key
 
 struct Ctl {
@@ -192,34 +210,47 @@ __device__ int block_lca(const KArgs& K, const int* list, int m, Ctl& ctl) {
 // --------------------------------------------------------------------------
 
 // Leaves of numpy's pairwise sum over one buffer [off0, off0+cl): emitted left to right
-// as (start, length, number of parent additions completed right after this leaf).
+// as (start, length, number of parent additions completed right after this leaf).  The
+// frame stack is a shift register (static indices) so it stays in VGPRs; depth <= 8.
 __device__ int gen_leaves(int off0, int cl, int4* out) {
-  int foff[16], flen[16], fst[16];
+  int so[8], sl[8], ss[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { so[i] = 0; sl[i] = 0; ss[i] = 0; }
+  auto push = [&](int o, int l) {
+#pragma unroll
+    for (int i = 7; i > 0; --i) { so[i] = so[i - 1]; sl[i] = sl[i - 1]; ss[i] = ss[i - 1]; }
+    so[0] = o; sl[0] = l; ss[0] = 0;
+  };
+  auto pop = [&]() {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) { so[i] = so[i + 1]; sl[i] = sl[i + 1]; ss[i] = ss[i + 1]; }
+  };
   int sp = 1, cnt = 0;
-  foff[0] = off0; flen[0] = cl; fst[0] = 0;
+  so[0] = off0; sl[0] = cl; ss[0] = 0;
   while (sp > 0) {
-    int t = sp - 1;
-    if (flen[t] > kLeafMax && fst[t] == 0) {
-      int h = flen[t] / 2;
+    if (sl[0] > kLeafMax && ss[0] == 0) {
+      int h = sl[0] / 2;
       h -= h % 8;
-      fst[t] = 1;
-      foff[sp] = foff[t]; flen[sp] = h; fst[sp] = 0;
+      ss[0] = 1;
+      push(so[0], h);
       ++sp;
       continue;
     }
-    int lo = foff[t], ll = flen[t], adds = 0;
+    const int lo = so[0], ll = sl[0];
+    int adds = 0;
+    pop();
     --sp;
     while (sp > 0) {
-      int u = sp - 1;
-      if (fst[u] == 1) {
-        int h = flen[u] / 2;
+      if (ss[0] == 1) {
+        int h = sl[0] / 2;
         h -= h % 8;
-        fst[u] = 2;
-        foff[sp] = foff[u] + h; flen[sp] = flen[u] - h; fst[sp] = 0;
+        ss[0] = 2;
+        push(so[0] + h, sl[0] - h);
         ++sp;
         break;
       }
       ++adds;
+      pop();
       --sp;
     }
     if (out) out[cnt] = make_int4(lo, ll, adds, 0);
@@ -232,20 +263,6 @@ __device__ int leaves_of_length(int n) {
   int cnt = 0;
   for (int o = 0; o < n; o += kNpyBuf) cnt += gen_leaves(o, min(kNpyBuf, n - o), nullptr);
   return cnt;
-}
-
-__device__ double combine_leaves(const int4* lv, int nl, const double* ls) {
-  double stk[16];
-  int sp = 0;
-  for (int i = 0; i < nl; ++i) {
-    stk[sp++] = ls[i];
-    for (int a = 0; a < lv[i].z; ++a) {
-      double r = stk[--sp];
-      double l = stk[--sp];
-      stk[sp++] = l + r;
-    }
-  }
-  return stk[0];
 }
 
 // One leaf (<= 128 elements) exactly as numpy's pairwise_sum inner block.
@@ -330,6 +347,8 @@ struct Contig {
   int *ign, *um;
   // per level
   uint64_t* keys;
+  int *slo, *shi;        // attachment site ranges in sorted-key order
+  double* ssc;
   int *seg_start, *seg_cl, *cl_id, *cl_sibp, *cl_flag, *pot, *mem1, *mem2;
   double *S, *cl_rank, *cl_crit;
   uint64_t* mask;
@@ -337,67 +356,159 @@ struct Contig {
   uint8_t* best_syn;
 };
 
-// Exact site-score mean of one (clade, locus) segment, computed by one wave:
-// 8 leaves x 8 strided accumulators per pass, leaf sums combined in numpy's tree order.
-__device__ double wave_site_sum(const Contig& C, int g, int kb, int ke, double* lsum) {
-  const int lane = lane_id(), grp = lane >> 3, ch = lane & 7;
+// Shift-register stack of partial sums for numpy's pairwise tree.  Static indexing keeps
+// it in VGPRs; 8 entries cover the deepest tree of one 8192-element buffer (depth 7).
+struct SumStack {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0, s5 = 0.0, s6 = 0.0, s7 = 0.0;
+  __device__ __forceinline__ void push(double v) {
+    s7 = s6; s6 = s5; s5 = s4; s4 = s3; s3 = s2; s2 = s1; s1 = s0; s0 = v;
+  }
+  __device__ __forceinline__ void add_top() {   // (left) + (right), left pushed first
+    s0 = s1 + s0;
+    s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = s7;
+  }
+};
+
+// Sequential float64 sum of `cnt` copies of v, starting from 0.0 (the value a strided
+// accumulator reaches over `cnt` covered sites of a constant run; zeros add nothing).
+__device__ __forceinline__ double seqsum(double v, int cnt) {
+  double r = 0.0;
+  for (int i = 0; i < cnt; ++i) r += v;
+  return r;
+}
+
+__device__ __forceinline__ double leaf_tree(double r0, double r1, double r2, double r3, double r4,
+                                            double r5, double r6, double r7) {
+  return ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+}
+
+// Number of t in [0, m) with base + 8t < bound.
+__device__ __forceinline__ int below(int base, int bound, int m) {
+  const int d = bound - base;
+  return d <= 0 ? 0 : min(m, (d + 7) >> 3);
+}
+
+constexpr int kRegAtt = 4;   // attachments of a segment held in registers
+
+// Exact np.mean of one (clade, locus) site array (orgscorer.py:399-406), one thread.
+// Site x holds max(0, max{score_a : lo_a <= x < hi_a}) over the segment's attachments
+// (C.slo/shi/ssc[kb..ke), attachment data gathered into key order).  The sum follows numpy
+// exactly: 8192-element buffers added from 0.0; per buffer the pairwise tree of
+// <=128-element leaves (gen_leaves), each leaf summed by 8 strided accumulators combined
+// as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus a sequential tail.  Closed forms used are
+// bit-identical: when the site values are one constant v over a leaf body of 8m sites,
+// every accumulator equals seqsum(v, m) and their tree is exactly 8*seqsum(v, m)
+// (doubling is exact); a single attachment gives accumulator j = seqsum(v, covered_j).
+__device__ double segment_mean(const Contig& C, int g, int kb, int ke) {
   const int n = C.loc_len[g];
   const int4* lv = C.leaves + C.leaf_off[g];
-  const int nl_total = C.leaf_off[g + 1] - C.leaf_off[g];
+  const int nl = C.leaf_off[g + 1] - C.leaf_off[g];
   const int k = ke - kb;
-  int lo0 = 0, hi0 = 0;
-  double sc0 = 0.0;
-  if (k == 1) {
-    int a = (int)(C.keys[kb] & 0xFFFFFFull);
-    lo0 = C.alo[a]; hi0 = C.ahi[a]; sc0 = C.asc[a];
+  const bool reg = k <= kRegAtt;
+  const int full_bufs = n / kNpyBuf;
+  int lo[kRegAtt], hi[kRegAtt];
+  double sc[kRegAtt];
+#pragma unroll
+  for (int i = 0; i < kRegAtt; ++i) {
+    const bool use = reg && kb + i < ke;
+    lo[i] = use ? C.slo[kb + i] : 0;
+    hi[i] = use ? C.shi[kb + i] : 0;     // lo == hi: never covers
+    sc[i] = use ? C.ssc[kb + i] : 0.0;
   }
   auto V = [&](int x) -> double {
-    if (k == 1) return (x >= lo0 && x < hi0) ? sc0 : 0.0;
     double v = 0.0;
-    for (int t = kb; t < ke; ++t) {
-      int a = (int)(C.keys[t] & 0xFFFFFFull);
-      if (x >= C.alo[a] && x < C.ahi[a]) {
-        double s = C.asc[a];
-        v = s > v ? s : v;
-      }
+    if (reg) {
+#pragma unroll
+      for (int i = 0; i < kRegAtt; ++i)
+        if (x >= lo[i] && x < hi[i]) v = sc[i] > v ? sc[i] : v;
+    } else {
+      for (int t = kb; t < ke; ++t)
+        if (x >= C.slo[t] && x < C.shi[t]) { const double s = C.ssc[t]; v = s > v ? s : v; }
     }
     return v;
   };
+  SumStack stk;
   double total = 0.0;
-  int leaf0 = 0;
-  for (int o = 0; o < n; o += kNpyBuf) {
-    const int cl = min(kNpyBuf, n - o);
-    const int nl = (cl == kNpyBuf) ? 64 : nl_total - leaf0;
-    for (int base = 0; base < nl; base += 8) {
-      const int leaf = base + grp;
-      double r = 0.0;
-      int st = 0, ln = 0;
-      if (leaf < nl) {
-        int4 e = lv[leaf0 + leaf];
-        st = e.x; ln = e.y;
-        const int m = ln >> 3;
-        if (m > 0) {
-          const int x = st + ch;
-          r = V(x);
-          for (int t = 1; t < m; ++t) r += V(x + 8 * t);
+  double cF = -1.0, cT = 0.0;
+  int cm = -1;
+  for (int j = 0; j < nl; ++j) {
+    const int4 e = lv[j];
+    const int st = e.x, ln = e.y, m = ln >> 3, body = m << 3, be = st + body;
+    double leaf = 0.0;
+    if (m > 0) {
+      // envelope over the leaf body: F = max score covering all of it; partial ones above F
+      double F = 0.0, pmax = 0.0;
+      bool part = false;
+      if (reg) {
+#pragma unroll
+        for (int i = 0; i < kRegAtt; ++i) {
+          const bool ne = lo[i] < hi[i];
+          if (ne && lo[i] <= st && be <= hi[i]) F = sc[i] > F ? sc[i] : F;
+          else if (ne && lo[i] < be && hi[i] > st) { part = true; pmax = sc[i] > pmax ? sc[i] : pmax; }
+        }
+      } else {
+        for (int t = kb; t < ke; ++t) {
+          const int l = C.slo[t], h = C.shi[t];
+          const double s = C.ssc[t];
+          if (l < h && l <= st && be <= h) F = s > F ? s : F;
+          else if (l < h && l < be && h > st) { part = true; pmax = s > pmax ? s : pmax; }
         }
       }
-      r += __shfl_xor(r, 1, 64);
-      r += __shfl_xor(r, 2, 64);
-      r += __shfl_xor(r, 4, 64);
-      if (ch == 0 && leaf < nl) {
-        for (int x = st + (ln & ~7); x < st + ln; ++x) r += V(x);
-        lsum[leaf] = r;
+      if (!part || !(pmax > F)) {
+        if (F > 0.0) {
+          if (F != cF || m != cm) { cT = seqsum(F, m); cF = F; cm = m; }
+          leaf = 8.0 * cT;
+        }
+      } else {
+        // strided accumulator c over positions st+c+8t: the envelope is constant between
+        // attachment boundaries, so add it run by run (0.0 adds are exact no-ops)
+        double r[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int base = st + c;
+          double acc = 0.0;
+          if (reg) {
+            int ta[kRegAtt], tb[kRegAtt];
+#pragma unroll
+            for (int i = 0; i < kRegAtt; ++i) { ta[i] = below(base, lo[i], m); tb[i] = below(base, hi[i], m); }
+            int t = 0;
+            while (t < m) {
+              double v = 0.0;
+              int nxt = m;
+#pragma unroll
+              for (int i = 0; i < kRegAtt; ++i) {
+                if (ta[i] <= t && t < tb[i]) { v = sc[i] > v ? sc[i] : v; nxt = min(nxt, tb[i]); }
+                else if (ta[i] > t) nxt = min(nxt, ta[i]);
+              }
+              if (v > 0.0) { for (; t < nxt; ++t) acc += v; } else { t = nxt; }
+            }
+          } else {
+            int t = 0;
+            while (t < m) {
+              double v = 0.0;
+              int nxt = m;
+              for (int q = kb; q < ke; ++q) {
+                const int ta = below(base, C.slo[q], m), tb = below(base, C.shi[q], m);
+                if (ta <= t && t < tb) { const double s = C.ssc[q]; v = s > v ? s : v; nxt = min(nxt, tb); }
+                else if (ta > t) nxt = min(nxt, ta);
+              }
+              if (v > 0.0) { for (; t < nxt; ++t) acc += v; } else { t = nxt; }
+            }
+          }
+          r[c] = acc;
+        }
+        leaf = leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0) total += combine_leaves(lv + leaf0, nl, lsum);
-    __builtin_amdgcn_wave_barrier();
-    leaf0 += nl;
+    for (int x = be; x < st + ln; ++x) leaf += V(x);
+    stk.push(leaf);
+    for (int a = 0; a < e.z; ++a) stk.add_top();
+    if (j == nl - 1 || (((j + 1) & 63) == 0 && ((j + 1) >> 6) <= full_bufs)) {
+      total += stk.s0;                            // one buffer done (numpy NPY_BUFSIZE)
+      stk.s0 = 0.0;
+    }
   }
-  return total;
+  return total / (double)n;
 }
 
 // --- two-clade option evaluation (orgscorer.py:511-545, 678-744), one thread ---------
@@ -514,8 +625,7 @@ __device__ double pair_crit(const Contig& C, int pa, int pb, int Gu) {
 // --------------------------------------------------------------------------
 
 template <bool BIG>
-__device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap, Ctl& ctl,
-                               double (*lsum)[kLeafSlots]) {
+__device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap, Ctl& ctl) {
   const int tid = threadIdx.x, w = wave_id();
   const DevParams& P = K.p;
   const int nsys = K.n_sys;
@@ -536,7 +646,8 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
   }
   for (int i = tid; i < G * nsys; i += kBlock) K.annot[C.l0 * nsys + i] = -1;
   if (H == 0 || G == 0) return;  // never evaluated -> unclassified (orgscorer.py:959)
-
+  STAMP_INIT();
+  STAMP(20);
   Arena ar{abase, acap, 0};
   // ---- loci and their pairwise-sum leaf tables ------------------------------------
   C.loc_lo = ar.take<int>(G);
@@ -566,6 +677,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     ctl.cnt = C.leaf_off[G];
   }
   __syncthreads();
+  STAMP(0);
   const int NL = ctl.cnt;
   C.leaves = ar.take<int4>(NL);
 
@@ -587,6 +699,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
   }
   int A;
   int off = block_scan(local, &A, ctl);
+  STAMP(1);
   const int virt = (P.weak == 2) ? 1 : 0;       // assign-unknown adds "Unknown" (:416-418)
   const int A1 = A + virt;
   C.alo = ar.take<int>(A);
@@ -633,6 +746,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     }
   }
   __syncthreads();
+  STAMP(2);
   const int64_t persist_mark = ar.used;
 
   // ---- annotation transfer (orgscorer.py:383-392): per (locus, system) the last hit in
@@ -679,11 +793,11 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     }
   }
   __syncthreads();
+  STAMP(3);
 
   int iteration = 1;
   bool first = true;
   int64_t pair_evals = 0;
-  double* my_lsum = lsum[w];
 
   for (;;) {
     // ================= build the gene-score matrix of this level ===================
@@ -694,6 +808,9 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     C.seg_start = ar.take<int>(A1 + 1);
     C.seg_cl = ar.take<int>(A1 + 1);
     C.cl_id = ar.take<int>(A1 + 1);
+    C.slo = ar.take<int>(A1 + 1);
+    C.shi = ar.take<int>(A1 + 1);
+    C.ssc = ar.take<double>(A1 + 1);
     if (!ar.fits()) {
       if (tid == 0) { ctl.overflow = 1; ctl.need = ar.used + (int64_t)A1 * (48 + 8 * G) + 8192; }
       __syncthreads();
@@ -708,7 +825,10 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
       C.keys[t] = key;
     }
     __syncthreads();
+    STAMP(4);
     bitonic_sort(C.keys, npow);
+    STAMP(5);
+    STAMP(21);
     // segments = distinct (clade, locus); clades = distinct clade (sorted = name order)
     {
       const int per = (A1 + kBlock - 1) / kBlock;
@@ -735,6 +855,8 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
           C.seg_start[si] = t;
           C.seg_cl[si] = ci;
         }
+        const int a = (int)(k & 0xFFFFFFull);
+        if (a < A) { C.slo[t] = C.alo[a]; C.shi[t] = C.ahi[a]; C.ssc[t] = C.asc[a]; }
       }
       if (tid == 0) {
         ctl.S_n = ts;
@@ -743,6 +865,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
       }
     }
     __syncthreads();
+    STAMP(6);
     const int S_n = ctl.S_n, Pn = ctl.P;
     C.S = ar.take<double>((int64_t)Pn * G);
     C.cl_sibp = ar.take<int>(Pn);
@@ -766,17 +889,18 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     for (int g = tid; g < G; g += kBlock) C.maxes[g] = 0;
     if (tid == 0) ctl.root_present = 0;
     __syncthreads();
+    STAMP(7);
     for (int p = tid; p < Pn; p += kBlock)
       if (C.cl_id[p] == K.root) ctl.root_present = 1;
-    // ---- site-score means (orgscorer.py:399-406), one wave per segment ---------------
-    for (int s = w; s < S_n; s += kWaves) {
+    // ---- site-score means (orgscorer.py:399-406), one thread per segment -------------
+    for (int s = tid; s < S_n; s += kBlock) {
       const int kb = C.seg_start[s], ke = C.seg_start[s + 1];
       const int g = (int)((C.keys[kb] >> 24) & 0xFFFF);
       if (g == kLocVirtual) continue;
-      const double total = wave_site_sum(C, g, kb, ke, my_lsum);
-      if (lane_id() == 0) C.S[(int64_t)C.seg_cl[s] * G + g] = total / (double)C.loc_len[g];
+      C.S[(int64_t)C.seg_cl[s] * G + g] = segment_mean(C, g, kb, ke);
     }
     __syncthreads();
+    STAMP(8);
     // ---- per-locus max over known clades, weak loci (:407-427) ----------------------
     for (int i = tid; i < Pn * G; i += kBlock) {
       if (C.cl_id[i / G] == K.unknown) continue;
@@ -798,6 +922,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
       ctl.all_ignored = (Gu == 0);
     }
     __syncthreads();
+    STAMP(9);
     const int Gu = ctl.Gu;
     if (first) {
       first = false;
@@ -825,6 +950,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
         if (opt && better(rank, p, br, bk)) { br = rank; bk = p; }
       }
       block_argmax(br, bk, ctl);
+      STAMP(10);
       if (bk >= 0) {
         // meld_one (:621-631): options within --range of the best
         const int bp = (int)bk;
@@ -849,6 +975,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
           const double s = C.S[(int64_t)bp * G + g];
           K.syn[C.l0 + g] = C.ign[g] ? '~' : (s >= P.k1 ? 'A' : '!');
         }
+        STAMP(11);
         if (tid == 0) {
           K.call[c] = WF_CALL_NO_LGT;
           K.crit[c] = C.cl_crit[bp];
@@ -1000,6 +1127,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
       }
     }
 
+    STAMP(12);
     // ================= roll-up (orgscorer.py:571-581) ================================
     if (Pn == 0 || ctl.root_present) break;
     for (int a = tid; a < A; a += kBlock) C.acl[a] = K.parent[C.acl[a]];
@@ -1021,12 +1149,11 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock) void k_contig_lds(KArgs K) {
+__global__ __launch_bounds__(kBlock, 4) void k_contig_lds(KArgs K) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
-  __shared__ double lsum[kWaves][kLeafSlots];
   const int c = blockIdx.x;
-  process_contig<false>(K, c, smem, K.lds_bytes, ctl, lsum);
+  process_contig<false>(K, c, smem, K.lds_bytes, ctl);
   __syncthreads();
   if (threadIdx.x == 0 && ctl.overflow) {
     if (ctl.status != 0) {
@@ -1040,14 +1167,13 @@ __global__ __launch_bounds__(kBlock) void k_contig_lds(KArgs K) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_contig_big(KArgs K) {
+__global__ __launch_bounds__(kBlock, 2) void k_contig_big(KArgs K) {
   __shared__ Ctl ctl;
-  __shared__ double lsum[kWaves][kLeafSlots];
   const int count = *K.work_count;
   char* base = K.big_ws + (int64_t)blockIdx.x * K.slot_bytes;
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const int c = K.work_list[i];
-    process_contig<true>(K, c, base, K.slot_bytes, ctl, lsum);
+    process_contig<true>(K, c, base, K.slot_bytes, ctl);
     __syncthreads();
     if (threadIdx.x == 0 && ctl.overflow) {
       K.status[c] = ctl.status != 0 ? ctl.status : WF_E_NOMEM;
@@ -1069,4 +1195,15 @@ hipError_t launch_big_kernel(const KArgs& k, int grid, hipStream_t s) {
   return hipGetLastError();
 }
 
+#ifdef WF_STAMPS
+extern "C" int wf_stamps_read(unsigned long long* out, int n) {
+  if (n > 32) n = 32;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess
+             ? 0 : -2;
+}
+extern "C" int wf_stamps_reset(void) {
+  unsigned long long z[32] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) == hipSuccess ? 0 : -2;
+}
+#endif
 }  // namespace wf
