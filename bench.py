@@ -33,6 +33,7 @@ def parse_args():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--contigs", type=int, default=None, help="override contigs per GPU")
     ap.add_argument("--lds-bytes", type=int, default=None)
+    ap.add_argument("--threads", type=int, default=None, help="threads per contig (64/128/256)")
     ap.add_argument("--cpu-sample", type=int, default=1500,
                     help="contigs timed on the CPU oracle (rank 0, N=1); 0 disables")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_cfg2.json"))
@@ -134,6 +135,8 @@ def main():
     chk = lambda rc: (_ for _ in ()).throw(RuntimeError(so.wf_last_error(h).decode())) if rc else None
     if args.lds_bytes:
         chk(so.wf_set_lds_bytes(h, args.lds_bytes))
+    if args.threads:
+        chk(so.wf_set_workgroup(h, args.threads))
     tstruct = engine.taxonomy_struct(tax)
     chk(so.wf_set_taxonomy(h, C.byref(tstruct)))
     stream = torch.cuda.current_stream(dev)

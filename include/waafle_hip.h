@@ -140,6 +140,8 @@ void wf_free(wf_ctx* ctx);
 const char* wf_last_error(const wf_ctx* ctx);
 int wf_set_stream(wf_ctx* ctx, void* hip_stream);     /* NULL = the context's own stream */
 int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes);     /* dynamic LDS per workgroup */
+int wf_set_workgroup(wf_ctx* ctx, int threads);       /* threads per contig: 64, 128, 256 */
+int wf_set_tier2_lds_bytes(wf_ctx* ctx, int64_t bytes); /* LDS of the overflow tier */
 int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* tax);
 int wf_score(wf_ctx* ctx, const wf_batch* batch, const wf_params* params, wf_result* out);
 int wf_synchronize(wf_ctx* ctx);

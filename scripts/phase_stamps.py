@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--contigs", type=int, default=None)
     ap.add_argument("--lds-bytes", type=int, default=None)
+    ap.add_argument("--threads", type=int, default=None)
     a = ap.parse_args()
     path = build.build(stamps=True, verbose=False)
     L._lib = None
@@ -35,7 +36,7 @@ def main():
     data = synth.generate(seed=int(a.config[-1]), **spec)
     batch, tax = synth.to_batch(data, with_codes=False)
     params = cli.param_dict(cli.parse_flags([]))
-    s = engine.GpuScorer(0, a.lds_bytes)
+    s = engine.GpuScorer(0, a.lds_bytes, a.threads)
     s.set_taxonomy(tax)
     s.score(batch, params)            # warm-up
     so.wf_stamps_reset()

@@ -160,11 +160,15 @@ def test_full_size_cfg2_properties(scorer):
     a = scorer.score(batch, params)
     b = scorer.score(batch, params)
     assert_same_results(a, b, batch)
-    small = engine.GpuScorer(0, lds_bytes=8192)      # most contigs overflow LDS
-    small.set_taxonomy(tax)
-    c = small.score(batch, params)
-    small.close()
-    assert_same_results(a, c, batch)
+    for kw in (dict(lds_bytes=8192),                          # tier 1 -> tier 2
+               dict(lds_bytes=8192, tier2_lds_bytes=8192),    # -> tier 3 (HBM workspace)
+               dict(threads=256, lds_bytes=36864),            # 4 waves per contig
+               dict(threads=128, lds_bytes=24576)):
+        small = engine.GpuScorer(0, **kw)
+        small.set_taxonomy(tax)
+        c = small.score(batch, params)
+        small.close()
+        assert_same_results(a, c, batch)
     bounds = engine.shard_bounds(engine.contig_cost(batch), 4)
     parts = [scorer.score(batch.slice(x, y), params) for x, y in bounds]
     d = engine.Results.concat(parts, [int(batch.hit_off[x]) for x, _ in bounds])

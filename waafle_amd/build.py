@@ -35,12 +35,13 @@ def up_to_date(lib=LIB):
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
-def build(force=False, verbose=True, stamps=False):
-    """Build the product library (or, with stamps=True, the per-phase timing variant)."""
-    lib = STAMPS_LIB if stamps else LIB
+def build(force=False, verbose=True, stamps=False, defines=(), out=None):
+    """Build the product library (or, with stamps=True, the per-phase timing variant;
+    `defines` + `out` build an experimental variant for sweeps)."""
+    lib = out or (STAMPS_LIB if stamps else LIB)
     if not force and up_to_date(lib):
         return lib
-    extra = ["-DWF_STAMPS"] if stamps else []
+    extra = (["-DWF_STAMPS"] if stamps else []) + ["-D" + d for d in defines]
     cmd = [hipcc()] + FLAGS + extra + SOURCES + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -50,6 +51,12 @@ def build(force=False, verbose=True, stamps=False):
 
 
 if __name__ == "__main__":
+    for arg in sys.argv[1:]:
+        if arg.startswith("--variant="):      # --variant=NAME:DEF1,DEF2 -> libwaafle_hip_NAME.so
+            name, defs = arg.split("=", 1)[1].split(":", 1)
+            build(force=True, defines=defs.split(","),
+                  out=os.path.join(HERE, "libwaafle_hip_{}.so".format(name)))
+            sys.exit(0)
     build(force="--force" in sys.argv)
     if "--stamps" in sys.argv:
         build(force="--force" in sys.argv, stamps=True)

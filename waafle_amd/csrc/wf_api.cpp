@@ -27,10 +27,15 @@ struct wf_ctx {
   int32_t tax_n = 0, root = -1, unknown = -1;
   DevBuf parent, depth, sibp, leaves;
   // overflow work list + counter
-  DevBuf ovf_list, ovf_count;
+  DevBuf ovf_list, ovf2_list, ovf_count;
   DevBuf retry_list, retry_count;
   DevBuf big_ws;
-  int64_t lds_bytes = 36 * 1024;   // 4 workgroups per CU (160 KiB LDS)
+  DevBuf kargs;                    // device copies of the per-tier kernel argument blocks
+  std::vector<wf::KArgs> kargs_host;
+  int64_t lds_bytes = 24 * 1024;   // tier 1: two waves per contig (VGPR-bound: 4 per CU)
+  int lds_threads = 128;
+  int64_t lds2_bytes = 76 * 1024;  // tier 2: 256 threads, 2 workgroups per CU
+  int tier2_grid = 512;
   int big_slots = 512;
   // staging for host-resident batches
   DevBuf b_hit_off, b_qlo, b_qhi, b_taxon, b_hstrand, b_score, b_scov, b_sysmask;
@@ -198,8 +203,10 @@ int wf_init(int device, wf_ctx** out) {
   }
   ctx->stream = ctx->own_stream;
   hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess)
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
     ctx->big_slots = std::max(64, prop.multiProcessorCount * 2);
+    ctx->tier2_grid = std::max(64, prop.multiProcessorCount * 2);
+  }
   *out = ctx;
   return WF_OK;
 }
@@ -209,6 +216,7 @@ void wf_free(wf_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->ovf_list,
+                    &ctx->ovf2_list, &ctx->kargs,
                     &ctx->ovf_count, &ctx->retry_list, &ctx->retry_count, &ctx->big_ws,
                     &ctx->b_hit_off, &ctx->b_qlo, &ctx->b_qhi, &ctx->b_taxon, &ctx->b_hstrand,
                     &ctx->b_score, &ctx->b_scov, &ctx->b_sysmask, &ctx->b_loc_off,
@@ -232,9 +240,25 @@ int wf_set_stream(wf_ctx* ctx, void* hip_stream) {
 
 int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes) {
   if (!ctx) return WF_E_BADINPUT;
-  if (bytes < 4096 || bytes > 150 * 1024)
-    return fail(ctx, WF_E_BADINPUT, "LDS budget %lld out of [4096, 153600]", (long long)bytes);
+  if (bytes < 4096 || bytes > 152 * 1024)
+    return fail(ctx, WF_E_BADINPUT, "LDS budget %lld out of [4096, 155648]", (long long)bytes);
   ctx->lds_bytes = bytes;
+  return WF_OK;
+}
+
+int wf_set_workgroup(wf_ctx* ctx, int threads) {
+  if (!ctx) return WF_E_BADINPUT;
+  if (threads != 64 && threads != 128 && threads != 256)
+    return fail(ctx, WF_E_BADINPUT, "threads per contig must be 64, 128 or 256");
+  ctx->lds_threads = threads;
+  return WF_OK;
+}
+
+int wf_set_tier2_lds_bytes(wf_ctx* ctx, int64_t bytes) {
+  if (!ctx) return WF_E_BADINPUT;
+  if (bytes < 4096 || bytes > 152 * 1024)
+    return fail(ctx, WF_E_BADINPUT, "LDS budget %lld out of [4096, 155648]", (long long)bytes);
+  ctx->lds2_bytes = bytes;
   return WF_OK;
 }
 
@@ -309,26 +333,44 @@ static int check_batch(wf_ctx* ctx, const wf_batch* b, const wf_params* p, const
   return WF_OK;
 }
 
+// Tier 1 (one wave per contig, small LDS) -> tier 2 (256 threads, large LDS, persistent
+// over tier 1's overflow list) -> tier 3 (HBM workspace slots, persistent over tier 2's
+// overflow list).  Everything is enqueued on the context stream; no host synchronisation.
 static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   int rc;
-  // overflow list
-  if ((rc = ensure(ctx, ctx->ovf_list, sizeof(int32_t) * (size_t)std::max(b->n_contigs, 1))) ||
+  const size_t list_bytes = sizeof(int32_t) * (size_t)std::max(b->n_contigs, 1);
+  if ((rc = ensure(ctx, ctx->ovf_list, list_bytes)) || (rc = ensure(ctx, ctx->ovf2_list, list_bytes)) ||
       (rc = ensure(ctx, ctx->ovf_count, 64)))
     return rc;
-  K.ovf_list = static_cast<int32_t*>(ctx->ovf_list.p);
-  K.ovf_count = static_cast<int32_t*>(ctx->ovf_count.p);
-  K.work_list = K.ovf_list;
-  K.work_count = K.ovf_count;
-  HIP_TRY(ctx, hipMemsetAsync(K.ovf_count, 0, sizeof(int32_t), ctx->stream));
-  // HBM workspace for overflow contigs
+  int32_t* counts = static_cast<int32_t*>(ctx->ovf_count.p);
+  HIP_TRY(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(int32_t), ctx->stream));
   const int64_t slot = slot_estimate(b);
   const int slots = std::min(ctx->big_slots, std::max(b->n_contigs, 1));
   if ((rc = ensure(ctx, ctx->big_ws, (size_t)slot * slots))) return rc;
   K.big_ws = static_cast<char*>(ctx->big_ws.p);
   K.slot_bytes = slot;
-  K.lds_bytes = ctx->lds_bytes;
   K.root = ctx->root;
   K.unknown = ctx->unknown;
+
+  wf::KArgs k1 = K, k2 = K, k3 = K;
+  k1.lds_bytes = ctx->lds_bytes;
+  k1.lds_threads = ctx->lds_threads;
+  k1.ovf_list = static_cast<int32_t*>(ctx->ovf_list.p);
+  k1.ovf_count = counts;
+  k2.lds_bytes = ctx->lds2_bytes;
+  k2.lds_threads = 256;
+  k2.work_list = k1.ovf_list;
+  k2.work_count = counts;
+  k2.ovf_list = static_cast<int32_t*>(ctx->ovf2_list.p);
+  k2.ovf_count = counts + 1;
+  k3.work_list = k2.ovf_list;
+  k3.work_count = counts + 1;
+  K = k3;   // the host-mode retry loop reuses the tier-3 arguments
+  if ((rc = ensure(ctx, ctx->kargs, 4 * sizeof(wf::KArgs)))) return rc;
+  wf::KArgs* dk = static_cast<wf::KArgs*>(ctx->kargs.p);
+  ctx->kargs_host.assign({k1, k2, k3});
+  HIP_TRY(ctx, hipMemcpyAsync(dk, ctx->kargs_host.data(), 3 * sizeof(wf::KArgs),
+                              hipMemcpyHostToDevice, ctx->stream));
 
   std::pair<int, int> el{-1, -1}, eb{-1, -1};
   if (ctx->timing) {
@@ -338,10 +380,13 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
     eb = ctx->ev_big.back();
   }
   if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
-  HIP_TRY(ctx, wf::launch_lds_kernel(K, ctx->stream));
+  HIP_TRY(ctx, wf::launch_lds_kernel(k1, dk, ctx->stream));
   if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
   if (eb.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[eb.first], ctx->stream));
-  HIP_TRY(ctx, wf::launch_big_kernel(K, slots, ctx->stream));
+  HIP_TRY(ctx, wf::launch_lds_list_kernel(k2, dk + 1,
+                                          std::min(ctx->tier2_grid, std::max(b->n_contigs, 1)),
+                                          ctx->stream));
+  HIP_TRY(ctx, wf::launch_big_kernel(dk + 2, slots, ctx->stream));
   if (eb.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[eb.second], ctx->stream));
   ++ctx->launches;
   return WF_OK;
@@ -435,7 +480,12 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
     K.work_count = static_cast<const int32_t*>(ctx->retry_count.p);
     K.big_ws = static_cast<char*>(ctx->big_ws.p);
     K.slot_bytes = need;
-    HIP_TRY(ctx, wf::launch_big_kernel(K, slots, ctx->stream));
+    wf::KArgs* dk = static_cast<wf::KArgs*>(ctx->kargs.p) + 3;
+    ctx->kargs_host.assign({K});
+    HIP_TRY(ctx, hipMemcpyAsync(dk, ctx->kargs_host.data(), sizeof(wf::KArgs),
+                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, wf::launch_big_kernel(dk, slots, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if ((rc = download(ctx, r->status, K.status, N)) ||
         (rc = download(ctx, r->need_bytes, K.need, N)))
       return rc;

@@ -41,10 +41,12 @@ struct KArgs {
   // overflow work list (filled by the LDS kernel, drained by the HBM-workspace kernel)
   int32_t* ovf_list; int32_t* ovf_count;
   const int32_t* work_list; const int32_t* work_count;   // list the big kernel drains
-  char* big_ws; int64_t slot_bytes; int64_t lds_bytes;
+  char* big_ws; int64_t slot_bytes; int64_t lds_bytes; int lds_threads;
 };
 
-hipError_t launch_lds_kernel(const KArgs& k, hipStream_t s);
-hipError_t launch_big_kernel(const KArgs& k, int grid, hipStream_t s);
+// `dk` points to a device copy of the host-side `k` (enqueued before the launch).
+hipError_t launch_lds_kernel(const KArgs& k, const KArgs* dk, hipStream_t s);
+hipError_t launch_lds_list_kernel(const KArgs& k, const KArgs* dk, int grid, hipStream_t s);
+hipError_t launch_big_kernel(const KArgs* dk, int grid, hipStream_t s);
 
 }  // namespace wf

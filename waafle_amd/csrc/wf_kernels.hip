@@ -46,6 +46,7 @@ struct Ctl {
   int overflow, status, cnt, cnt2, p_unk, root_present, all_ignored;
   int n_in, all_ok, all_same, best_ok, best_dir, best_c1p, best_c2p;
   int lca1, lca2, res_kind, lca_out;
+  int cls_cnt[5], cls_off[5];
   double best_r, best_crit;
   long long best_k;
   int64_t need;
@@ -78,7 +79,8 @@ __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_
 // --------------------------------------------------------------------------
 
 // Exclusive prefix sum of one int per thread; *total receives the block sum.
-__device__ int block_scan(int v, int* total, Ctl& ctl) {
+template <int NT>
+__device__ __forceinline__ int block_scan(int v, int* total, Ctl& ctl) {
   const int lane = lane_id(), w = wave_id();
   int x = v;
 #pragma unroll
@@ -90,7 +92,7 @@ __device__ int block_scan(int v, int* total, Ctl& ctl) {
   __syncthreads();
   int base = 0, tot = 0;
 #pragma unroll
-  for (int i = 0; i < kWaves; ++i) {
+  for (int i = 0; i < NT / 64; ++i) {
     int t = ctl.red_i[i];
     base += (i < w) ? t : 0;
     tot += t;
@@ -101,7 +103,8 @@ __device__ int block_scan(int v, int* total, Ctl& ctl) {
 }
 
 // Two exclusive prefix sums at once.
-__device__ void block_scan2(int v1, int v2, int* p1, int* p2, int* t1, int* t2, Ctl& ctl) {
+template <int NT>
+__device__ __forceinline__ void block_scan2(int v1, int v2, int* p1, int* p2, int* t1, int* t2, Ctl& ctl) {
   const int lane = lane_id(), w = wave_id();
   int x = v1, y = v2;
 #pragma unroll
@@ -113,7 +116,7 @@ __device__ void block_scan2(int v1, int v2, int* p1, int* p2, int* t1, int* t2, 
   __syncthreads();
   int b1 = 0, b2 = 0, s1 = 0, s2 = 0;
 #pragma unroll
-  for (int i = 0; i < kWaves; ++i) {
+  for (int i = 0; i < NT / 64; ++i) {
     int a = ctl.red_i[i], b = ctl.red_j[i];
     if (i < w) { b1 += a; b2 += b; }
     s1 += a;
@@ -132,7 +135,8 @@ __device__ __forceinline__ bool better(double r2, long long k2, double r, long l
   return k2 >= 0 && (k < 0 || r2 > r || (r2 == r && k2 > k));
 }
 
-__device__ void block_argmax(double& r, long long& k, Ctl& ctl) {
+template <int NT>
+__device__ __forceinline__ void block_argmax(double& r, long long& k, Ctl& ctl) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     double r2 = __shfl_xor(r, off, 64);
@@ -144,7 +148,7 @@ __device__ void block_argmax(double& r, long long& k, Ctl& ctl) {
   if (threadIdx.x == 0) {
     double br = ctl.red_r[0];
     long long bk = ctl.red_k[0];
-    for (int i = 1; i < kWaves; ++i)
+    for (int i = 1; i < NT / 64; ++i)
       if (better(ctl.red_r[i], ctl.red_k[i], br, bk)) { br = ctl.red_r[i]; bk = ctl.red_k[i]; }
     ctl.best_r = br;
     ctl.best_k = bk;
@@ -154,11 +158,11 @@ __device__ void block_argmax(double& r, long long& k, Ctl& ctl) {
   k = ctl.best_k;
 }
 
-template <class T>
-__device__ void bitonic_sort(T* keys, int n) {
+template <int NT, class T>
+__device__ __forceinline__ void bitonic_sort(T* keys, int n) {
   for (int k = 2; k <= n; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += kBlock) {
+      for (int i = threadIdx.x; i < n; i += NT) {
         int ixj = i ^ j;
         if (ixj > i) {
           T a = keys[i], b = keys[ixj];
@@ -175,7 +179,7 @@ __device__ void bitonic_sort(T* keys, int n) {
 // taxonomy helpers (utils.py:401-411)
 // --------------------------------------------------------------------------
 
-__device__ int lca2(const KArgs& K, int a, int b) {
+__device__ __forceinline__ int lca2(const KArgs& K, int a, int b) {
   if (a < 0) return b;
   if (b < 0) return a;
   int da = K.depth[a], db = K.depth[b];
@@ -186,7 +190,7 @@ __device__ int lca2(const KArgs& K, int a, int b) {
 }
 
 // LCA of list[0..m) (clade ids); wave 0 folds, result broadcast through ctl.
-__device__ int block_lca(const KArgs& K, const int* list, int m, Ctl& ctl) {
+__device__ __forceinline__ int block_lca(const KArgs& K, const int* list, int m, Ctl& ctl) {
   if (m <= 0) return -1;
   if (m == 1) return list[0];
   if (wave_id() == 0) {
@@ -209,24 +213,31 @@ __device__ int block_lca(const KArgs& K, const int* list, int m, Ctl& ctl) {
 // numpy pairwise summation order
 // --------------------------------------------------------------------------
 
+constexpr int kMaxDepth = 7;   // internal-node depths of one <=8192-element buffer: 0..6
+constexpr int kGroupMax = 64;  // leaves combined by lane shuffles (one 8192 buffer = 64)
+
 // Leaves of numpy's pairwise sum over one buffer [off0, off0+cl): emitted left to right
 // as (start, length, number of parent additions completed right after this leaf).  The
 // frame stack is a shift register (static indices) so it stays in VGPRs; depth <= 8.
-__device__ int gen_leaves(int off0, int cl, int4* out) {
-  int so[8], sl[8], ss[8];
+// If `sched` is given (kMaxDepth rows of `stride` bytes, pre-set to -1) it also records
+// the combine schedule: sched[d][i] = j when leaf i is the leftmost leaf of an internal
+// node at depth d whose right child starts at leaf j.
+__device__ int gen_leaves(int off0, int cl, int4* out, int8_t* sched = nullptr, int stride = 0) {
+  int so[8], sl[8], ss[8], sf[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) { so[i] = 0; sl[i] = 0; ss[i] = 0; }
+  for (int i = 0; i < 8; ++i) { so[i] = 0; sl[i] = 0; ss[i] = 0; sf[i] = 0; }
+  int cnt = 0;
   auto push = [&](int o, int l) {
 #pragma unroll
-    for (int i = 7; i > 0; --i) { so[i] = so[i - 1]; sl[i] = sl[i - 1]; ss[i] = ss[i - 1]; }
-    so[0] = o; sl[0] = l; ss[0] = 0;
+    for (int i = 7; i > 0; --i) { so[i] = so[i - 1]; sl[i] = sl[i - 1]; ss[i] = ss[i - 1]; sf[i] = sf[i - 1]; }
+    so[0] = o; sl[0] = l; ss[0] = 0; sf[0] = cnt;
   };
   auto pop = [&]() {
 #pragma unroll
-    for (int i = 0; i < 7; ++i) { so[i] = so[i + 1]; sl[i] = sl[i + 1]; ss[i] = ss[i + 1]; }
+    for (int i = 0; i < 7; ++i) { so[i] = so[i + 1]; sl[i] = sl[i + 1]; ss[i] = ss[i + 1]; sf[i] = sf[i + 1]; }
   };
-  int sp = 1, cnt = 0;
-  so[0] = off0; sl[0] = cl; ss[0] = 0;
+  int sp = 1;
+  so[0] = off0; sl[0] = cl; ss[0] = 0; sf[0] = 0;
   while (sp > 0) {
     if (sl[0] > kLeafMax && ss[0] == 0) {
       int h = sl[0] / 2;
@@ -240,11 +251,14 @@ __device__ int gen_leaves(int off0, int cl, int4* out) {
     int adds = 0;
     pop();
     --sp;
+    ++cnt;
     while (sp > 0) {
       if (ss[0] == 1) {
         int h = sl[0] / 2;
         h -= h % 8;
         ss[0] = 2;
+        if (sched && sp - 1 < kMaxDepth && sf[0] < stride)
+          sched[(sp - 1) * stride + sf[0]] = (int8_t)cnt;
         push(so[0] + h, sl[0] - h);
         ++sp;
         break;
@@ -253,8 +267,7 @@ __device__ int gen_leaves(int off0, int cl, int4* out) {
       pop();
       --sp;
     }
-    if (out) out[cnt] = make_int4(lo, ll, adds, 0);
-    ++cnt;
+    if (out) out[cnt - 1] = make_int4(lo, ll, adds, 0);
   }
   return cnt;
 }
@@ -340,6 +353,8 @@ struct Contig {
   int H, G;
   // persistent
   int *loc_lo, *loc_len, *loc_st, *leaf_off;
+  int *loc_grp, *loc_steps, *sched_off;   // lane-group size, combine steps, schedule offset
+  int8_t* sched;
   int4* leaves;
   int *alo, *ahi, *ahit, *aloc, *acl;
   double* asc;
@@ -347,10 +362,8 @@ struct Contig {
   int *ign, *um;
   // per level
   uint64_t* keys;
-  int *slo, *shi;        // attachment site ranges in sorted-key order
-  double* ssc;
-  int *seg_start, *seg_cl, *cl_id, *cl_sibp, *cl_flag, *pot, *mem1, *mem2;
-  double *S, *cl_rank, *cl_crit;
+  int *seg_start, *seg_cl, *cl_id, *pot, *mem1, *mem2, *sorder;
+  double* S;
   uint64_t* mask;
   unsigned *bm1, *bm2;
   uint8_t* best_syn;
@@ -390,125 +403,195 @@ __device__ __forceinline__ int below(int base, int bound, int m) {
 
 constexpr int kRegAtt = 4;   // attachments of a segment held in registers
 
-// Exact np.mean of one (clade, locus) site array (orgscorer.py:399-406), one thread.
-// Site x holds max(0, max{score_a : lo_a <= x < hi_a}) over the segment's attachments
-// (C.slo/shi/ssc[kb..ke), attachment data gathered into key order).  The sum follows numpy
-// exactly: 8192-element buffers added from 0.0; per buffer the pairwise tree of
-// <=128-element leaves (gen_leaves), each leaf summed by 8 strided accumulators combined
-// as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) plus a sequential tail.  Closed forms used are
-// bit-identical: when the site values are one constant v over a leaf body of 8m sites,
-// every accumulator equals seqsum(v, m) and their tree is exactly 8*seqsum(v, m)
-// (doubling is exact); a single attachment gives accumulator j = seqsum(v, covered_j).
-__device__ double segment_mean(const Contig& C, int g, int kb, int ke) {
-  const int n = C.loc_len[g];
-  const int4* lv = C.leaves + C.leaf_off[g];
-  const int nl = C.leaf_off[g + 1] - C.leaf_off[g];
-  const int k = ke - kb;
-  const bool reg = k <= kRegAtt;
-  const int full_bufs = n / kNpyBuf;
+// The attachments of one (clade, locus) segment -- sorted keys [kb, ke) -- and the exact
+// numpy value of one pairwise-sum leaf of its site array.  Site x holds
+// max(0, max{score_a : lo_a <= x < hi_a}).
+struct SegAtt {
+  int kb, ke;
+  bool reg;
   int lo[kRegAtt], hi[kRegAtt];
   double sc[kRegAtt];
+
+  __device__ __forceinline__ void load(const Contig& C, int kb_, int ke_) {
+    kb = kb_; ke = ke_;
+    reg = ke - kb <= kRegAtt;
 #pragma unroll
-  for (int i = 0; i < kRegAtt; ++i) {
-    const bool use = reg && kb + i < ke;
-    lo[i] = use ? C.slo[kb + i] : 0;
-    hi[i] = use ? C.shi[kb + i] : 0;     // lo == hi: never covers
-    sc[i] = use ? C.ssc[kb + i] : 0.0;
+    for (int i = 0; i < kRegAtt; ++i) {
+      const bool use = reg && kb + i < ke;
+      const int a = use ? (int)(C.keys[kb + i] & 0xFFFFFFull) : 0;
+      lo[i] = use ? C.alo[a] : 0;
+      hi[i] = use ? C.ahi[a] : 0;          // lo == hi: never covers
+      sc[i] = use ? C.asc[a] : 0.0;
+    }
   }
-  auto V = [&](int x) -> double {
+  __device__ __forceinline__ void get(const Contig& C, int t, int& l, int& h, double& v) const {
+    const int a = (int)(C.keys[t] & 0xFFFFFFull);
+    l = C.alo[a]; h = C.ahi[a]; v = C.asc[a];
+  }
+  __device__ __forceinline__ double value_at(const Contig& C, int x) const {
     double v = 0.0;
     if (reg) {
 #pragma unroll
       for (int i = 0; i < kRegAtt; ++i)
         if (x >= lo[i] && x < hi[i]) v = sc[i] > v ? sc[i] : v;
     } else {
-      for (int t = kb; t < ke; ++t)
-        if (x >= C.slo[t] && x < C.shi[t]) { const double s = C.ssc[t]; v = s > v ? s : v; }
+      for (int t = kb; t < ke; ++t) {
+        int l, h; double s;
+        get(C, t, l, h, s);
+        if (x >= l && x < h) v = s > v ? s : v;
+      }
     }
     return v;
-  };
-  SumStack stk;
-  double total = 0.0;
-  double cF = -1.0, cT = 0.0;
-  int cm = -1;
-  for (int j = 0; j < nl; ++j) {
-    const int4 e = lv[j];
-    const int st = e.x, ln = e.y, m = ln >> 3, body = m << 3, be = st + body;
-    double leaf = 0.0;
-    if (m > 0) {
-      // envelope over the leaf body: F = max score covering all of it; partial ones above F
-      double F = 0.0, pmax = 0.0;
-      bool part = false;
-      if (reg) {
+  }
+  // numpy's leaf: 8 strided accumulators over the body of 8m sites, combined as
+  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail added in order.  Accumulator c
+  // adds the sites st+c+8t, t = 0..m-1, sequentially from 0.0.  All closed forms below are
+  // bit-identical to that sequence (adding +0.0 to a non-negative partial sum is exact and
+  // a constant v added k times from 0.0 is seqsum(v, k)):
+  //  - constant envelope F over the body: every r_c = seqsum(F, m), and r summed by the
+  //    tree is 8*seqsum(F, m) (each level doubles exactly);
+  //  - one nonzero run s over a zero background (a hit boundary inside the leaf, ~97% of
+  //    the non-constant leaves): r_c = seqsum(s, k_c), where k_c = the sites of run in
+  //    lane c's stride spans at most 3 adjacent values;
+  //  - otherwise the envelope's runs are walked once in site order and each run's value
+  //    is added k_c times to every accumulator (interleaved, no per-accumulator search).
+  template <bool REG>
+  __device__ __forceinline__ void att(const Contig& C, int i, int& l, int& h, double& v) const {
+    if (REG) { l = lo[i]; h = hi[i]; v = sc[i]; } else get(C, kb + i, l, h, v);
+  }
+  template <bool REG>
+  __device__ __forceinline__ double body_sum(const Contig& C, int st, int m) const {
+    const int be = st + (m << 3);
+    const int na = REG ? kRegAtt : ke - kb;
+    double F = 0.0;
 #pragma unroll
-        for (int i = 0; i < kRegAtt; ++i) {
-          const bool ne = lo[i] < hi[i];
-          if (ne && lo[i] <= st && be <= hi[i]) F = sc[i] > F ? sc[i] : F;
-          else if (ne && lo[i] < be && hi[i] > st) { part = true; pmax = sc[i] > pmax ? sc[i] : pmax; }
-        }
-      } else {
-        for (int t = kb; t < ke; ++t) {
-          const int l = C.slo[t], h = C.shi[t];
-          const double s = C.ssc[t];
-          if (l < h && l <= st && be <= h) F = s > F ? s : F;
-          else if (l < h && l < be && h > st) { part = true; pmax = s > pmax ? s : pmax; }
-        }
-      }
-      if (!part || !(pmax > F)) {
-        if (F > 0.0) {
-          if (F != cF || m != cm) { cT = seqsum(F, m); cF = F; cm = m; }
-          leaf = 8.0 * cT;
-        }
-      } else {
-        // strided accumulator c over positions st+c+8t: the envelope is constant between
-        // attachment boundaries, so add it run by run (0.0 adds are exact no-ops)
-        double r[8];
+    for (int i = 0; i < na; ++i) {
+      int l, h; double v;
+      att<REG>(C, i, l, h, v);
+      if (l < h && l <= st && be <= h) F = v > F ? v : F;
+    }
+    int npos = 0, plo = 0, phi = 0;
+    double ps = 0.0;
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int base = st + c;
-          double acc = 0.0;
-          if (reg) {
-            int ta[kRegAtt], tb[kRegAtt];
-#pragma unroll
-            for (int i = 0; i < kRegAtt; ++i) { ta[i] = below(base, lo[i], m); tb[i] = below(base, hi[i], m); }
-            int t = 0;
-            while (t < m) {
-              double v = 0.0;
-              int nxt = m;
-#pragma unroll
-              for (int i = 0; i < kRegAtt; ++i) {
-                if (ta[i] <= t && t < tb[i]) { v = sc[i] > v ? sc[i] : v; nxt = min(nxt, tb[i]); }
-                else if (ta[i] > t) nxt = min(nxt, ta[i]);
-              }
-              if (v > 0.0) { for (; t < nxt; ++t) acc += v; } else { t = nxt; }
-            }
-          } else {
-            int t = 0;
-            while (t < m) {
-              double v = 0.0;
-              int nxt = m;
-              for (int q = kb; q < ke; ++q) {
-                const int ta = below(base, C.slo[q], m), tb = below(base, C.shi[q], m);
-                if (ta <= t && t < tb) { const double s = C.ssc[q]; v = s > v ? s : v; nxt = min(nxt, tb); }
-                else if (ta > t) nxt = min(nxt, ta);
-              }
-              if (v > 0.0) { for (; t < nxt; ++t) acc += v; } else { t = nxt; }
-            }
-          }
-          r[c] = acc;
-        }
-        leaf = leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+    for (int i = 0; i < na; ++i) {
+      int l, h; double v;
+      att<REG>(C, i, l, h, v);
+      if (l < h && l < be && h > st && !(l <= st && be <= h) && v > F) {
+        ++npos; plo = l; phi = h; ps = v;
       }
     }
-    for (int x = be; x < st + ln; ++x) leaf += V(x);
-    stk.push(leaf);
+    if (npos == 0) return F > 0.0 ? 8.0 * seqsum(F, m) : 0.0;
+    double r[8];
+    if (npos == 1 && !(F > 0.0)) {
+      int k[8], kmin = m;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        k[c] = below(st + c, phi, m) - below(st + c, plo, m);
+        kmin = min(kmin, k[c]);
+      }
+      const double s0 = seqsum(ps, kmin), s1 = s0 + ps, s2 = s1 + ps;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) r[c] = k[c] == kmin ? s0 : (k[c] == kmin + 1 ? s1 : s2);
+      return leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r[c] = 0.0;
+    for (int x = st; x < be;) {
+      double v = 0.0;
+      int nx = be;
+#pragma unroll
+      for (int i = 0; i < na; ++i) {
+        int l, h; double s;
+        att<REG>(C, i, l, h, s);
+        if (l < h) {
+          if (l <= x && x < h) { v = s > v ? s : v; nx = min(nx, h); }
+          else if (l > x) nx = min(nx, l);
+        }
+      }
+      if (v > 0.0) {
+        int k[8], kmax = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          k[c] = below(st + c, nx, m) - below(st + c, x, m);
+          kmax = max(kmax, k[c]);
+        }
+        for (int q = 0; q < kmax; ++q) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) r[c] = q < k[c] ? r[c] + v : r[c];
+        }
+      }
+      x = nx;
+    }
+    return leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+  }
+  __device__ __forceinline__ double leaf(const Contig& C, int st, int ln) const {
+    const int m = ln >> 3, be = st + (m << 3);
+    double res = 0.0;
+    if (m > 0) res = reg ? body_sum<true>(C, st, m) : body_sum<false>(C, st, m);
+    for (int x = be; x < st + ln; ++x) res += value_at(C, x);
+    return res;
+  }
+};
+
+// Exact np.mean of one (clade, locus) site array (orgscorer.py:399-406) by one thread:
+// leaves in order, combined on a shift-register stack; 8192-element buffers added from
+// 0.0 (numpy NPY_BUFSIZE).  Used for loci too long for the lane-parallel path.
+__device__ __forceinline__ double segment_mean(const Contig& C, int g, int kb, int ke) {
+  const int n = C.loc_len[g];
+  const int4* lv = C.leaves + C.leaf_off[g];
+  const int nl = C.leaf_off[g + 1] - C.leaf_off[g];
+  const int full_bufs = n / kNpyBuf;
+  SegAtt at;
+  at.load(C, kb, ke);
+  SumStack stk;
+  double total = 0.0;
+  for (int j = 0; j < nl; ++j) {
+    const int4 e = lv[j];
+    stk.push(at.leaf(C, e.x, e.y));
     for (int a = 0; a < e.z; ++a) stk.add_top();
     if (j == nl - 1 || (((j + 1) & 63) == 0 && ((j + 1) >> 6) <= full_bufs)) {
-      total += stk.s0;                            // one buffer done (numpy NPY_BUFSIZE)
+      total += stk.s0;
       stk.s0 = 0.0;
     }
   }
   return total / (double)n;
+}
+
+// Lane-parallel site means: a group of gs lanes (8/16/32/64) takes one segment whose locus
+// has <= gs leaves in a single numpy buffer; lane i computes leaf i, then the pairwise
+// tree is combined bottom-up with lane shuffles following the locus' schedule (lane i
+// adds lane j's partial sum when i starts an internal node whose right child starts at
+// j), so every addition is numpy's (left + right).  `list` holds the class's segments.
+template <int NW>
+__device__ __forceinline__ void site_means_grouped(const Contig& C, const int* list, int count, int gs) {
+  const int lane = lane_id(), w = wave_id();
+  const int per_round = 64 / gs, gi = lane / gs, li = lane % gs;
+  for (int base = w * per_round; base < count; base += NW * per_round) {
+    const int idx = base + gi;
+    const bool has = idx < count;
+    const int s = has ? list[idx] : 0;
+    const int kb = has ? C.seg_start[s] : 0, ke = has ? C.seg_start[s + 1] : 0;
+    const int g = has ? (int)((C.keys[kb] >> 24) & 0xFFFF) : 0;
+    const int nl = has ? C.leaf_off[g + 1] - C.leaf_off[g] : 0;
+    double v = 0.0;
+    if (has && li < nl) {
+      SegAtt at;
+      at.load(C, kb, ke);
+      const int4 e = C.leaves[C.leaf_off[g] + li];
+      v = at.leaf(C, e.x, e.y);
+    }
+    const int steps = has ? C.loc_steps[g] : 0;
+    int maxsteps = steps;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) maxsteps = max(maxsteps, __shfl_xor(maxsteps, off, 64));
+    const int8_t* sch = C.sched + (has ? C.sched_off[g] : 0);
+    for (int d = maxsteps - 1; d >= 0; --d) {
+      const int src = (has && d < steps) ? (int)sch[d * gs + li] : -1;
+      const double o = __shfl(v, src >= 0 ? gi * gs + src : lane, 64);
+      if (src >= 0) v = v + o;
+    }
+    if (has && li == 0) C.S[(int64_t)C.seg_cl[s] * C.G + g] = v / (double)C.loc_len[g];
+  }
 }
 
 // --- two-clade option evaluation (orgscorer.py:511-545, 678-744), one thread ---------
@@ -528,7 +611,7 @@ __device__ __forceinline__ uint8_t two_char(const KArgs& K, const Contig& C, int
   return '!';
 }
 
-__device__ OptEval eval_two(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
+__device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
                             const uint8_t* best, uint8_t* out) {
   const DevParams& P = K.p;
   const int G = C.G;
@@ -589,8 +672,8 @@ __device__ OptEval eval_two(const KArgs& K, const Contig& C, int Pcount, int pa,
       else if (c == 'A' && !e.dir) need = py;
       else continue;
       for (int q = 0; q < Pcount; ++q) {
-        if (C.cl_sibp[q] != need) continue;
-        int s = C.cl_id[q];
+        const int s = C.cl_id[q];
+        if (K.sibp[s] != need) continue;
         if (s == X || s == Y) continue;
         if (C.S[(int64_t)q * G + g] >= P.sister_thr) { e.ok = 0; break; }
       }
@@ -599,7 +682,7 @@ __device__ OptEval eval_two(const KArgs& K, const Contig& C, int Pcount, int pa,
   return e;
 }
 
-__device__ double pair_rank(const Contig& C, int pa, int pb, int Gu) {
+__device__ __forceinline__ double pair_rank(const Contig& C, int pa, int pb, int Gu) {
   const double* ra = C.S + (int64_t)pa * C.G;
   const double* rb = C.S + (int64_t)pb * C.G;
   return np_sum(Gu, [&](int u) {
@@ -608,7 +691,7 @@ __device__ double pair_rank(const Contig& C, int pa, int pb, int Gu) {
          }) / (double)Gu;
 }
 
-__device__ double pair_crit(const Contig& C, int pa, int pb, int Gu) {
+__device__ __forceinline__ double pair_crit(const Contig& C, int pa, int pb, int Gu) {
   const double* ra = C.S + (int64_t)pa * C.G;
   const double* rb = C.S + (int64_t)pb * C.G;
   double m = 0.0;
@@ -624,8 +707,9 @@ __device__ double pair_crit(const Contig& C, int pa, int pb, int Gu) {
 // the contig workgroup
 // --------------------------------------------------------------------------
 
-template <bool BIG>
-__device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap, Ctl& ctl) {
+template <int NT, bool BIG>
+__device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap, Ctl& ctl) {
+  constexpr int NW = NT / 64;
   const int tid = threadIdx.x, w = wave_id();
   const DevParams& P = K.p;
   const int nsys = K.n_sys;
@@ -644,7 +728,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     K.iters[c] = 0; K.nm1[c] = 0; K.nm2[c] = 0; K.pair_evals[c] = 0; K.status[c] = 0;
     K.need[c] = 0;
   }
-  for (int i = tid; i < G * nsys; i += kBlock) K.annot[C.l0 * nsys + i] = -1;
+  for (int i = tid; i < G * nsys; i += NT) K.annot[C.l0 * nsys + i] = -1;
   if (H == 0 || G == 0) return;  // never evaluated -> unclassified (orgscorer.py:959)
   STAMP_INIT();
   STAMP(20);
@@ -654,6 +738,9 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
   C.loc_len = ar.take<int>(G);
   C.loc_st = ar.take<int>(G);
   C.leaf_off = ar.take<int>(G + 1);
+  C.loc_grp = ar.take<int>(G);
+  C.loc_steps = ar.take<int>(G);
+  C.sched_off = ar.take<int>(G + 1);
   C.maxes = ar.take<uint64_t>(G);
   C.ign = ar.take<int>(G);
   C.um = ar.take<int>(G);
@@ -662,24 +749,35 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     __syncthreads();
     return;
   }
-  for (int g = tid; g < G; g += kBlock) {
+  for (int g = tid; g < G; g += NT) {
     int s = K.lstart[C.l0 + g], e = K.lend[C.l0 + g];
     int lo = min(s, e), hi = max(s, e);
     C.loc_lo[g] = lo;
     C.loc_len[g] = hi - lo + 1;                 // len(Locus) (utils.py:321-322)
     C.loc_st[g] = K.lstrand[C.l0 + g];
-    C.leaf_off[g + 1] = leaves_of_length(hi - lo + 1);
+    const int n = hi - lo + 1, nl = leaves_of_length(n);
+    C.leaf_off[g + 1] = nl;
+    // lane-group size for the parallel site means (0: serial path)
+    const int gs = (n > kNpyBuf || nl > kGroupMax) ? 0 : nl <= 8 ? 8 : nl <= 16 ? 16 : nl <= 32 ? 32 : 64;
+    C.loc_grp[g] = gs;
+    C.sched_off[g + 1] = kMaxDepth * gs;
   }
   __syncthreads();
   if (tid == 0) {
     C.leaf_off[0] = 0;
-    for (int g = 0; g < G; ++g) C.leaf_off[g + 1] += C.leaf_off[g];
+    C.sched_off[0] = 0;
+    for (int g = 0; g < G; ++g) {
+      C.leaf_off[g + 1] += C.leaf_off[g];
+      C.sched_off[g + 1] += C.sched_off[g];
+    }
     ctl.cnt = C.leaf_off[G];
+    ctl.cnt2 = C.sched_off[G];
   }
   __syncthreads();
   STAMP(0);
-  const int NL = ctl.cnt;
+  const int NL = ctl.cnt, NSCH = ctl.cnt2;
   C.leaves = ar.take<int4>(NL);
+  C.sched = ar.take<int8_t>(NSCH);
 
   // ---- attach hits to loci: count (orgscorer.py:359-369, :559-564; utils.py:487-500) ---
   auto attaches = [&](int qlo, int qhi, int hs, int g) -> bool {
@@ -691,23 +789,24 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     return (double)ov / (double)den >= P.min_overlap;
   };
   int local = 0;
-  for (int i = tid; i < H; i += kBlock) {
+  for (int i = tid; i < H; i += NT) {
     const int64_t hi_ = C.h0 + i;
     if (!(K.scov[hi_] >= P.min_scov)) continue;
     const int qlo = K.qlo[hi_], qhi = K.qhi[hi_], hs = K.hstrand[hi_];
     for (int g = 0; g < G; ++g) local += attaches(qlo, qhi, hs, g) ? 1 : 0;
   }
   int A;
-  int off = block_scan(local, &A, ctl);
+  int off = block_scan<NT>(local, &A, ctl);
   STAMP(1);
   const int virt = (P.weak == 2) ? 1 : 0;       // assign-unknown adds "Unknown" (:416-418)
   const int A1 = A + virt;
   C.alo = ar.take<int>(A);
   C.ahi = ar.take<int>(A);
-  C.ahit = ar.take<int>(A);
   C.aloc = ar.take<int>(A);
   C.acl = ar.take<int>(A);
   C.asc = ar.take<double>(A);
+  const int64_t persist_mark = ar.used;
+  C.ahit = ar.take<int>(A);                     // temporary: annotations only
   if (!ar.fits() || A >= (1 << 24) || G >= kLocVirtual) {
     if (tid == 0) {
       ctl.overflow = 1;
@@ -717,14 +816,23 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     __syncthreads();
     return;
   }
-  // leaf tables
-  for (int g = tid; g < G; g += kBlock) {
+  // leaf tables and combine schedules
+  for (int i = tid; i < NSCH; i += NT) C.sched[i] = -1;
+  __syncthreads();
+  for (int g = tid; g < G; g += NT) {
     int k = C.leaf_off[g];
-    const int n = C.loc_len[g];
-    for (int o = 0; o < n; o += kNpyBuf) k += gen_leaves(o, min(kNpyBuf, n - o), C.leaves + k);
+    const int n = C.loc_len[g], gs = C.loc_grp[g];
+    int8_t* sch = gs ? C.sched + C.sched_off[g] : nullptr;
+    for (int o = 0; o < n; o += kNpyBuf)
+      k += gen_leaves(o, min(kNpyBuf, n - o), C.leaves + k, sch, gs);
+    int steps = 0;
+    for (int d = 0; d < kMaxDepth && sch; ++d)
+      for (int i = 0; i < gs; ++i)
+        if (sch[d * gs + i] >= 0) steps = d + 1;
+    C.loc_steps[g] = steps;
   }
   // ---- attach: fill, with the python-slice site range (orgscorer.py:371-382) ---------
-  for (int i = tid; i < H; i += kBlock) {
+  for (int i = tid; i < H; i += NT) {
     const int64_t hi_ = C.h0 + i;
     if (!(K.scov[hi_] >= P.min_scov)) continue;
     const int qlo = K.qlo[hi_], qhi = K.qhi[hi_], hs = K.hstrand[hi_];
@@ -747,11 +855,11 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
   }
   __syncthreads();
   STAMP(2);
-  const int64_t persist_mark = ar.used;
 
   // ---- annotation transfer (orgscorer.py:383-392): per (locus, system) the last hit in
   // file order whose score equals the running maximum >= threshold ---------------------
   if (nsys > 0) {
+    ar.used = persist_mark + (int64_t)A * 4 + 16;
     uint64_t* abest = ar.take<uint64_t>((int64_t)G * nsys);
     int* aidx = ar.take<int>((int64_t)G * nsys);
     if (!ar.fits()) {
@@ -759,9 +867,9 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
       __syncthreads();
       return;
     }
-    for (int i = tid; i < G * nsys; i += kBlock) { abest[i] = 0; aidx[i] = -1; }
+    for (int i = tid; i < G * nsys; i += NT) { abest[i] = 0; aidx[i] = -1; }
     __syncthreads();
-    for (int a = tid; a < A; a += kBlock) {
+    for (int a = tid; a < A; a += NT) {
       const uint32_t m = K.sysmask[C.h0 + C.ahit[a]];
       const double s = C.asc[a];
       if (m == 0 || !(s >= P.annot_ref)) continue;
@@ -769,7 +877,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
         if (m & (1u << b)) atomicMax((unsigned long long*)&abest[C.aloc[a] * nsys + b], dbits(s));
     }
     __syncthreads();
-    for (int a = tid; a < A; a += kBlock) {
+    for (int a = tid; a < A; a += NT) {
       const uint32_t m = K.sysmask[C.h0 + C.ahit[a]];
       const double s = C.asc[a];
       if (m == 0 || !(s >= P.annot_ref)) continue;
@@ -778,7 +886,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
           atomicMax(&aidx[C.aloc[a] * nsys + b], C.ahit[a]);
     }
     __syncthreads();
-    for (int i = tid; i < G * nsys; i += kBlock)
+    for (int i = tid; i < G * nsys; i += NT)
       K.annot[C.l0 * nsys + i] = aidx[i] >= 0 ? (int)(C.h0 + aidx[i]) : -1;
     __syncthreads();
     ar.used = persist_mark;
@@ -786,7 +894,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
 
   // ---- initial jumps (orgscorer.py:955-957) ---------------------------------------
   if (P.jump > 0) {
-    for (int a = tid; a < A; a += kBlock) {
+    for (int a = tid; a < A; a += NT) {
       int x = C.acl[a];
       for (int j = 0; j < P.jump; ++j) x = K.parent[x];
       C.acl[a] = x;
@@ -807,16 +915,15 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     C.keys = ar.take<uint64_t>(npow);
     C.seg_start = ar.take<int>(A1 + 1);
     C.seg_cl = ar.take<int>(A1 + 1);
+    C.sorder = ar.take<int>(A1 + 1);
+    const int64_t dead_end = ar.used;             // keys + segments: dead after site means
     C.cl_id = ar.take<int>(A1 + 1);
-    C.slo = ar.take<int>(A1 + 1);
-    C.shi = ar.take<int>(A1 + 1);
-    C.ssc = ar.take<double>(A1 + 1);
     if (!ar.fits()) {
       if (tid == 0) { ctl.overflow = 1; ctl.need = ar.used + (int64_t)A1 * (48 + 8 * G) + 8192; }
       __syncthreads();
       return;
     }
-    for (int t = tid; t < npow; t += kBlock) {
+    for (int t = tid; t < npow; t += NT) {
       uint64_t key = kKeyPad;
       if (t < A)
         key = ((uint64_t)(uint32_t)C.acl[t] << 40) | ((uint64_t)C.aloc[t] << 24) | (uint64_t)t;
@@ -826,12 +933,12 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     }
     __syncthreads();
     STAMP(4);
-    bitonic_sort(C.keys, npow);
+    bitonic_sort<NT>(C.keys, npow);
     STAMP(5);
     STAMP(21);
     // segments = distinct (clade, locus); clades = distinct clade (sorted = name order)
     {
-      const int per = (A1 + kBlock - 1) / kBlock;
+      const int per = (A1 + NT - 1) / NT;
       const int b = min(A1, tid * per), e = min(A1, b + per);
       int ns = 0, nc = 0;
       for (int t = b; t < e; ++t) {
@@ -840,7 +947,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
         if (t == 0 || (k >> 40) != (C.keys[t - 1] >> 40)) ++nc;
       }
       int ps, pc, ts, tc;
-      block_scan2(ns, nc, &ps, &pc, &ts, &tc, ctl);
+      block_scan2<NT>(ns, nc, &ps, &pc, &ts, &tc, ctl);
       int si = ps - 1, ci = pc - 1;
       for (int t = b; t < e; ++t) {
         const uint64_t k = C.keys[t];
@@ -855,8 +962,6 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
           C.seg_start[si] = t;
           C.seg_cl[si] = ci;
         }
-        const int a = (int)(k & 0xFFFFFFull);
-        if (a < A) { C.slo[t] = C.alo[a]; C.shi[t] = C.ahi[a]; C.ssc[t] = C.asc[a]; }
       }
       if (tid == 0) {
         ctl.S_n = ts;
@@ -868,41 +973,70 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     STAMP(6);
     const int S_n = ctl.S_n, Pn = ctl.P;
     C.S = ar.take<double>((int64_t)Pn * G);
-    C.cl_sibp = ar.take<int>(Pn);
-    C.cl_rank = ar.take<double>(Pn);
-    C.cl_crit = ar.take<double>(Pn);
-    C.cl_flag = ar.take<int>(Pn);
-    C.pot = ar.take<int>(Pn);
-    C.mask = ar.take<uint64_t>(Pn);
-    C.mem1 = ar.take<int>(Pn);
-    C.mem2 = ar.take<int>(Pn);
-    C.bm1 = ar.take<unsigned>((Pn + 31) / 32);
-    C.bm2 = ar.take<unsigned>((Pn + 31) / 32);
-    C.best_syn = ar.take<uint8_t>(G);
+    {
+      // explain scratch: overlays the sort keys / segment tables when they fit (both are
+      // dead once the gene-score matrix exists), else follows S
+      Arena ex{abase, acap, persist_mark};
+      const int64_t need_ex = (int64_t)Pn * 20 + 8 * ((Pn + 31) / 32) + G + 6 * 16;
+      if (persist_mark + need_ex > dead_end) ex.used = ar.used;
+      C.pot = ex.take<int>(Pn);
+      C.mask = ex.take<uint64_t>(Pn);
+      C.mem1 = ex.take<int>(Pn);
+      C.mem2 = ex.take<int>(Pn);
+      C.bm1 = ex.take<unsigned>((Pn + 31) / 32);
+      C.bm2 = ex.take<unsigned>((Pn + 31) / 32);
+      C.best_syn = ex.take<uint8_t>(G);
+      if (ex.used > ar.used) ar.used = ex.used;
+    }
     if (!ar.fits()) {
       if (tid == 0) { ctl.overflow = 1; ctl.need = ar.used + (int64_t)A1 * (48 + 8 * G) + 8192; }
       __syncthreads();
       return;
     }
-    for (int i = tid; i < Pn * G; i += kBlock) C.S[i] = 0.0;
-    for (int p = tid; p < Pn; p += kBlock) C.cl_sibp[p] = K.sibp[C.cl_id[p]];
-    for (int g = tid; g < G; g += kBlock) C.maxes[g] = 0;
+    for (int i = tid; i < Pn * G; i += NT) C.S[i] = 0.0;
+    for (int g = tid; g < G; g += NT) C.maxes[g] = 0;
     if (tid == 0) ctl.root_present = 0;
     __syncthreads();
     STAMP(7);
-    for (int p = tid; p < Pn; p += kBlock)
+    for (int p = tid; p < Pn; p += NT)
       if (C.cl_id[p] == K.root) ctl.root_present = 1;
-    // ---- site-score means (orgscorer.py:399-406), one thread per segment -------------
-    for (int s = tid; s < S_n; s += kBlock) {
+    // ---- site-score means (orgscorer.py:399-406) -------------------------------------
+    // segments grouped by their locus' lane-group class (8/16/32/64 lanes; 4 = serial)
+    if (tid < 5) ctl.cls_cnt[tid] = 0;
+    __syncthreads();
+    auto seg_class = [&](int s) -> int {
+      const int g = (int)((C.keys[C.seg_start[s]] >> 24) & 0xFFFF);
+      if (g == kLocVirtual) return -1;
+      const int gs = C.loc_grp[g];
+      return gs == 8 ? 0 : gs == 16 ? 1 : gs == 32 ? 2 : gs == 64 ? 3 : 4;
+    };
+    for (int s = tid; s < S_n; s += NT) {
+      const int cls = seg_class(s);
+      if (cls >= 0) atomicAdd(&ctl.cls_cnt[cls], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int acc = 0;
+      for (int q = 0; q < 5; ++q) { ctl.cls_off[q] = acc; acc += ctl.cls_cnt[q]; ctl.cls_cnt[q] = 0; }
+    }
+    __syncthreads();
+    for (int s = tid; s < S_n; s += NT) {
+      const int cls = seg_class(s);
+      if (cls >= 0) C.sorder[ctl.cls_off[cls] + atomicAdd(&ctl.cls_cnt[cls], 1)] = s;
+    }
+    __syncthreads();
+    for (int q = 0; q < 4; ++q)
+      site_means_grouped<NW>(C, C.sorder + ctl.cls_off[q], ctl.cls_cnt[q], 8 << q);
+    for (int i = tid; i < ctl.cls_cnt[4]; i += NT) {
+      const int s = C.sorder[ctl.cls_off[4] + i];
       const int kb = C.seg_start[s], ke = C.seg_start[s + 1];
       const int g = (int)((C.keys[kb] >> 24) & 0xFFFF);
-      if (g == kLocVirtual) continue;
       C.S[(int64_t)C.seg_cl[s] * G + g] = segment_mean(C, g, kb, ke);
     }
     __syncthreads();
     STAMP(8);
     // ---- per-locus max over known clades, weak loci (:407-427) ----------------------
-    for (int i = tid; i < Pn * G; i += kBlock) {
+    for (int i = tid; i < Pn * G; i += NT) {
       if (C.cl_id[i / G] == K.unknown) continue;
       const double v = C.S[i];
       if (v > 0.0) atomicMax((unsigned long long*)&C.maxes[i % G], dbits(v));
@@ -936,20 +1070,21 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
 
     // ================= explain_one (orgscorer.py:585-597) ============================
     {
+      // Contig.score (:447-461) for one clade: (min, np.mean) of its masked row
+      auto score_one = [&](int p, double& crit, double& rank) {
+        const double* row = C.S + (int64_t)p * G;
+        crit = row[C.um[0]];
+        for (int u = 1; u < Gu; ++u) { const double v = row[C.um[u]]; crit = v < crit ? v : crit; }
+        rank = np_sum(Gu, [&](int u) { return row[C.um[u]]; }) / (double)Gu;
+      };
       double br = -__builtin_inf();
       long long bk = -1;
-      for (int p = tid; p < Pn; p += kBlock) {
-        const double* row = C.S + (int64_t)p * G;
-        double crit = row[C.um[0]];
-        for (int u = 1; u < Gu; ++u) { double v = row[C.um[u]]; crit = v < crit ? v : crit; }
-        const double rank = np_sum(Gu, [&](int u) { return row[C.um[u]]; }) / (double)Gu;
-        const int opt = crit >= P.k1;
-        C.cl_crit[p] = crit;
-        C.cl_rank[p] = rank;
-        C.cl_flag[p] = opt;
-        if (opt && better(rank, p, br, bk)) { br = rank; bk = p; }
+      for (int p = tid; p < Pn; p += NT) {
+        double crit, rank;
+        score_one(p, crit, rank);
+        if (crit >= P.k1 && better(rank, p, br, bk)) { br = rank; bk = p; }
       }
-      block_argmax(br, bk, ctl);
+      block_argmax<NT>(br, bk, ctl);
       STAMP(10);
       if (bk >= 0) {
         // meld_one (:621-631): options within --range of the best
@@ -957,11 +1092,14 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
         if (tid == 0) ctl.cnt = 0;
         __syncthreads();
         if (P.dis1 == 1) {
-          for (int p = tid; p < Pn; p += kBlock)
-            if (C.cl_flag[p] && (br - C.cl_rank[p]) <= P.range) {
+          for (int p = tid; p < Pn; p += NT) {
+            double crit, rank;
+            score_one(p, crit, rank);
+            if (crit >= P.k1 && (br - rank) <= P.range) {
               const int slot = atomicAdd(&ctl.cnt, 1);
               C.mem1[slot] = C.cl_id[p];
             }
+          }
         }
         __syncthreads();
         const int m = ctl.cnt;
@@ -970,15 +1108,17 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
           return;
         }
         const int lca = (P.dis1 == 1) ? block_lca(K, C.mem1, m, ctl) : C.cl_id[bp];
-        for (int i = tid; i < m; i += kBlock) K.meld[C.mbase + i] = C.mem1[i];
-        for (int g = tid; g < G; g += kBlock) {  // set_synteny_one (:495-509) of the best
+        for (int i = tid; i < m; i += NT) K.meld[C.mbase + i] = C.mem1[i];
+        for (int g = tid; g < G; g += NT) {  // set_synteny_one (:495-509) of the best
           const double s = C.S[(int64_t)bp * G + g];
           K.syn[C.l0 + g] = C.ign[g] ? '~' : (s >= P.k1 ? 'A' : '!');
         }
         STAMP(11);
         if (tid == 0) {
+          double crit, rank;
+          score_one(bp, crit, rank);
           K.call[c] = WF_CALL_NO_LGT;
-          K.crit[c] = C.cl_crit[bp];
+          K.crit[c] = crit;
           K.rank[c] = br;
           K.c1[c] = lca;
           K.c2[c] = -1;
@@ -994,25 +1134,25 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     {
       // potential clades: max over ALL loci >= k2 (:603-605)
       int flag_local = 0;
-      const int per = (Pn + kBlock - 1) / kBlock;
+      const int per = (Pn + NT - 1) / NT;
       const int pb0 = min(Pn, tid * per), pe0 = min(Pn, pb0 + per);
-      for (int p = pb0; p < pe0; ++p) {
+      auto potential = [&](int p) -> bool {
         const double* row = C.S + (int64_t)p * G;
         double mx = row[0];
         for (int g = 1; g < G; ++g) mx = row[g] > mx ? row[g] : mx;
-        C.cl_flag[p] = mx >= P.k2;
-        flag_local += C.cl_flag[p];
-      }
+        return mx >= P.k2;
+      };
+      for (int p = pb0; p < pe0; ++p) flag_local += potential(p) ? 1 : 0;
       int Pp;
-      int pos = block_scan(flag_local, &Pp, ctl);
+      int pos = block_scan<NT>(flag_local, &Pp, ctl);
       for (int p = pb0; p < pe0; ++p)
-        if (C.cl_flag[p]) C.pot[pos++] = p;
+        if (potential(p)) C.pot[pos++] = p;
       pair_evals += (int64_t)Pp * (Pp - 1) / 2;
       const bool use_mask = Gu <= 64;
       const uint64_t full = (Gu >= 64) ? ~0ull : ((1ull << Gu) - 1ull);
       __syncthreads();
       if (use_mask) {
-        for (int i = tid; i < Pp; i += kBlock) {
+        for (int i = tid; i < Pp; i += NT) {
           const double* row = C.S + (int64_t)C.pot[i] * G;
           uint64_t m = 0;
           for (int u = 0; u < Gu; ++u)
@@ -1028,7 +1168,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
         if (use_mask) return (C.mask[i] | C.mask[j]) == full;
         return pair_crit(C, C.pot[i], C.pot[j], Gu) >= P.k2;
       };
-      for (int i = w; i < Pp; i += kWaves) {
+      for (int i = w; i < Pp; i += NW) {
         for (int j = i + 1 + lane_id(); j < Pp; j += 64) {
           if (!candidate(i, j)) continue;
           const double r = pair_rank(C, C.pot[i], C.pot[j], Gu);
@@ -1036,11 +1176,11 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
           if (better(r, key, br, bk)) { br = r; bk = key; }
         }
       }
-      block_argmax(br, bk, ctl);
+      block_argmax<NT>(br, bk, ctl);
       bool have_ok = false;
       if (bk >= 0) {
         const int bi = (int)(bk / Pp), bj = (int)(bk % Pp);
-        for (int i = tid; i < (Pn + 31) / 32; i += kBlock) { C.bm1[i] = 0; C.bm2[i] = 0; }
+        for (int i = tid; i < (Pn + 31) / 32; i += NT) { C.bm1[i] = 0; C.bm2[i] = 0; }
         if (tid == 0) {
           OptEval e = eval_two(K, C, Pn, C.pot[bi], C.pot[bj], nullptr, C.best_syn);
           ctl.best_ok = e.ok; ctl.best_dir = e.dir;
@@ -1050,7 +1190,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
         }
         __syncthreads();
         // pass 2: options within --range of the best get the LGT filters (:636-639)
-        for (int i = w; i < Pp; i += kWaves) {
+        for (int i = w; i < Pp; i += NW) {
           for (int j = i + 1 + lane_id(); j < Pp; j += 64) {
             if (!candidate(i, j)) continue;
             const double r = pair_rank(C, C.pot[i], C.pot[j], Gu);
@@ -1083,7 +1223,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
         }
         int lca1 = -1, lca2v = -1, m1 = 0, m2 = 0;
         if (kind == 2) {
-          for (int p = tid; p < Pn; p += kBlock) {
+          for (int p = tid; p < Pn; p += NT) {
             if (C.bm1[p >> 5] & (1u << (p & 31))) C.mem1[atomicAdd(&ctl.cnt, 1)] = C.cl_id[p];
             if (C.bm2[p >> 5] & (1u << (p & 31))) C.mem2[atomicAdd(&ctl.cnt2, 1)] = C.cl_id[p];
           }
@@ -1105,10 +1245,10 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
           have_ok = true;
         }
         if (have_ok) {
-          for (int g = tid; g < G; g += kBlock) K.syn[C.l0 + g] = C.best_syn[g];
+          for (int g = tid; g < G; g += NT) K.syn[C.l0 + g] = C.best_syn[g];
           if (kind == 2) {
-            for (int i = tid; i < m1; i += kBlock) K.meld[C.mbase + i] = C.mem1[i];
-            for (int i = tid; i < m2; i += kBlock) K.meld[C.mbase + m1 + i] = C.mem2[i];
+            for (int i = tid; i < m1; i += NT) K.meld[C.mbase + i] = C.mem1[i];
+            for (int i = tid; i < m2; i += NT) K.meld[C.mbase + m1 + i] = C.mem2[i];
           }
           if (tid == 0) {
             K.call[c] = WF_CALL_LGT;
@@ -1130,7 +1270,7 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
     STAMP(12);
     // ================= roll-up (orgscorer.py:571-581) ================================
     if (Pn == 0 || ctl.root_present) break;
-    for (int a = tid; a < A; a += kBlock) C.acl[a] = K.parent[C.acl[a]];
+    for (int a = tid; a < A; a += NT) C.acl[a] = K.parent[C.acl[a]];
     ++iteration;
     if (iteration > kMaxIter) {
       if (tid == 0) ctl.status = WF_E_RUNAWAY;
@@ -1149,31 +1289,50 @@ __device__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap,
 
 }  // namespace
 
-__global__ __launch_bounds__(kBlock, 4) void k_contig_lds(KArgs K) {
+// Tiers 1 and 2: state in LDS.  Tier 1 (LIST = false) runs one workgroup per contig of the
+// batch -- NT = 64, one wave per contig, suits the small contigs of typical assemblies.
+// Tier 2 (LIST = true, NT = 256, a larger LDS budget) drains the contigs tier 1 could not
+// hold, as a persistent grid over the work list.  Whatever still does not fit goes to the
+// tier-3 HBM-workspace kernel.
+// Kernel arguments live in device memory (one KArgs block per tier, uploaded per call) so
+// every field is a scalar load; a by-value struct argument whose address is taken would be
+// copied to scratch and re-read from there on every access.
+#ifndef WF_LDS_OCC
+#define WF_LDS_OCC 2   // min waves per SIMD the register allocator must leave room for
+#endif
+template <int NT, bool LIST>
+__global__ __launch_bounds__(NT, WF_LDS_OCC) void k_contig_lds(const KArgs* __restrict__ kp) {
+  const KArgs& K = *kp;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
-  const int c = blockIdx.x;
-  process_contig<false>(K, c, smem, K.lds_bytes, ctl);
-  __syncthreads();
-  if (threadIdx.x == 0 && ctl.overflow) {
-    if (ctl.status != 0) {
-      K.status[c] = ctl.status;
-    } else {
-      const int slot = atomicAdd(K.ovf_count, 1);
-      K.ovf_list[slot] = c;
-      K.status[c] = kPending;
-      K.need[c] = ctl.need;
+  const int count = LIST ? *K.work_count : K.n_contigs;
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int c = LIST ? K.work_list[i] : i;
+    process_contig<NT, false>(K, c, smem, K.lds_bytes, ctl);
+    __syncthreads();
+    if (threadIdx.x == 0 && ctl.overflow) {
+      if (ctl.status != 0) {
+        K.status[c] = ctl.status;
+      } else {
+        const int slot = atomicAdd(K.ovf_count, 1);
+        K.ovf_list[slot] = c;
+        K.status[c] = kPending;
+        K.need[c] = ctl.need;
+      }
     }
+    __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(kBlock, 2) void k_contig_big(KArgs K) {
+// Tier 3: the same contig program on a per-workgroup HBM workspace slot.
+__global__ __launch_bounds__(kBlock, 2) void k_contig_big(const KArgs* __restrict__ kp) {
+  const KArgs& K = *kp;
   __shared__ Ctl ctl;
   const int count = *K.work_count;
   char* base = K.big_ws + (int64_t)blockIdx.x * K.slot_bytes;
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const int c = K.work_list[i];
-    process_contig<true>(K, c, base, K.slot_bytes, ctl);
+    process_contig<kBlock, true>(K, c, base, K.slot_bytes, ctl);
     __syncthreads();
     if (threadIdx.x == 0 && ctl.overflow) {
       K.status[c] = ctl.status != 0 ? ctl.status : WF_E_NOMEM;
@@ -1183,15 +1342,33 @@ __global__ __launch_bounds__(kBlock, 2) void k_contig_big(KArgs K) {
   }
 }
 
-hipError_t launch_lds_kernel(const KArgs& k, hipStream_t s) {
-  if (k.n_contigs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_contig_lds, dim3(k.n_contigs), dim3(kBlock), (size_t)k.lds_bytes, s, k);
+template <int NT, bool LIST>
+static hipError_t launch_lds(const KArgs& k, const KArgs* dk, int grid, hipStream_t s) {
+  if (k.lds_bytes > 64 * 1024) {
+    static hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&k_contig_lds<NT, LIST>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+    if (attr != hipSuccess) return attr;
+  }
+  hipLaunchKernelGGL((k_contig_lds<NT, LIST>), dim3(grid), dim3(NT), (size_t)k.lds_bytes, s, dk);
   return hipGetLastError();
 }
 
-hipError_t launch_big_kernel(const KArgs& k, int grid, hipStream_t s) {
+hipError_t launch_lds_kernel(const KArgs& k, const KArgs* dk, hipStream_t s) {
+  if (k.n_contigs <= 0) return hipSuccess;
+  if (k.lds_threads == 64) return launch_lds<64, false>(k, dk, k.n_contigs, s);
+  if (k.lds_threads == 128) return launch_lds<128, false>(k, dk, k.n_contigs, s);
+  return launch_lds<256, false>(k, dk, k.n_contigs, s);
+}
+
+hipError_t launch_lds_list_kernel(const KArgs& k, const KArgs* dk, int grid, hipStream_t s) {
   if (grid <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_contig_big, dim3(grid), dim3(kBlock), 0, s, k);
+  return launch_lds<256, true>(k, dk, grid, s);
+}
+
+hipError_t launch_big_kernel(const KArgs* dk, int grid, hipStream_t s) {
+  if (grid <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_contig_big, dim3(grid), dim3(kBlock), 0, s, dk);
   return hipGetLastError();
 }
 

@@ -103,7 +103,7 @@ def taxonomy_struct(t):
 class GpuScorer:
     """One libwaafle_hip context on one device."""
 
-    def __init__(self, device=0, lds_bytes=None):
+    def __init__(self, device=0, lds_bytes=None, threads=None, tier2_lds_bytes=None):
         self.lib = L.load()
         h = C.c_void_p()
         rc = self.lib.wf_init(int(device), C.byref(h))
@@ -113,6 +113,10 @@ class GpuScorer:
         self.device = device
         if lds_bytes:
             self._check(self.lib.wf_set_lds_bytes(self.h, int(lds_bytes)))
+        if threads:
+            self._check(self.lib.wf_set_workgroup(self.h, int(threads)))
+        if tier2_lds_bytes:
+            self._check(self.lib.wf_set_tier2_lds_bytes(self.h, int(tier2_lds_bytes)))
 
     def _check(self, rc):
         if rc != L.WF_OK:

@@ -62,6 +62,8 @@ SIGNATURES = {
     "wf_last_error": (C.c_char_p, [C.c_void_p]),
     "wf_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "wf_set_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
+    "wf_set_workgroup": (C.c_int, [C.c_void_p, C.c_int]),
+    "wf_set_tier2_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
     "wf_set_taxonomy": (C.c_int, [C.c_void_p, C.POINTER(WfTaxonomy)]),
     "wf_score": (C.c_int, [C.c_void_p, C.POINTER(WfBatch), C.POINTER(WfParams),
                            C.POINTER(WfResult)]),
