@@ -82,7 +82,7 @@ def to_device(batch, torch, dev):
     return t
 
 
-def cpu_baseline(data, batch, tax, n_sample):
+def cpu_baseline(data, batch, tax, n_sample, config):
     """Time the oracle (a Python/numpy port of the reference) on the first n_sample
     contigs of the same workload, inputs pre-parsed (same scope as the GPU value)."""
     from oracle import orgscorer_oracle as orc
@@ -101,17 +101,16 @@ def cpu_baseline(data, batch, tax, n_sample):
     return {"value": n_sample / dt, "unit": "contigs/s", "cores": 1, "kind": "port",
             "sample": "first {} contigs of the {} workload, oracle (Python/numpy restatement "
                       "of waafle_orgscorer) on 1 host core, inputs pre-parsed; {:.1f} s".format(
-                          n_sample, "cfg2", dt)}
+                          n_sample, config, dt)}
 
 
 def main():
     args = parse_args()
     import torch
     from waafle_amd import cli, engine, lib as L, synth
+    from waafle_amd import dist as wdist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = wdist.rank_env()
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -186,11 +185,7 @@ def main():
     t1 = time.perf_counter()
     tm = L.WfTiming()
     chk(so.wf_timing_read(h, C.byref(tm)))
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = wdist.max_over_ranks(t1 - t0, dist, dev)
 
     calls = out["call"].cpu().numpy()
     pairs = int(out["pair_evals"].cpu().numpy().sum())
@@ -232,7 +227,8 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        result["cpu_baseline"] = cpu_baseline(data, batch, tax, min(args.cpu_sample, N))
+        result["cpu_baseline"] = cpu_baseline(data, batch, tax, min(args.cpu_sample, N),
+                                              args.config)
     if rank == 0:
         print(json.dumps(result))
     so.wf_free(h)

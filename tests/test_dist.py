@@ -1,0 +1,97 @@
+"""N>1 plumbing on CPU: two gloo ranks run the product's sharding / gather / timing code
+(waafle_amd.dist) with the oracle standing in for the device scorer (test-only)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from waafle_amd import dist as wdist
+from waafle_amd import engine, lib as L
+
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _oracle_scorer(data, tax):
+    from oracle import orgscorer_oracle as orc
+    from oracle_bridge import oracle_hits_from_batch, oracle_loci_from_batch, oracle_results
+    from waafle_amd import cli
+    params = orc.Params(**cli.param_dict(cli.parse_flags([])))
+    otax = orc.Taxonomy(data.tax.edges)
+
+    def score(sub):
+        lengths = dict(zip(sub.contig_names, sub.contig_lengths.tolist()))
+        contigs = orc.score_contigs(lengths, oracle_loci_from_batch(sub),
+                                    oracle_hits_from_batch(sub, tax), otax, params)
+        return oracle_results(contigs, sub, tax)
+    return score
+
+
+def _worker(rank, port, outdir, fail_rank):
+    import torch.distributed as dist
+    from waafle_amd import synth
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        data = synth.generate(n=40, genes=5, clades=30, seed=7)
+        batch, tax = synth.to_batch(data, with_codes=False)
+        inner = _oracle_scorer(data, tax)
+
+        def score(sub):
+            if rank == fail_rank:
+                err = L.WaafleHipError(L.WF_E_RUNAWAY, "runaway")
+                err.contigs = np.array([1])
+                raise err
+            return inner(sub)
+        try:
+            res = wdist.score_ranked(batch, tax, None, score, dist)
+            outcome = "ok"
+        except L.WaafleHipError as exc:
+            res, outcome = None, "err:{}:{}".format(exc.code, list(exc.contigs))
+        t = wdist.max_over_ranks(1.0 + rank, dist)
+        if rank == 0:
+            full = inner(batch) if res is not None else None
+            np.savez(os.path.join(outdir, "r0.npz"), outcome=outcome, tmax=t,
+                     **({} if res is None else {
+                         "got_" + f: getattr(res, f) for f in res.__dataclass_fields__}),
+                     **({} if full is None else {
+                         "want_" + f: getattr(full, f) for f in full.__dataclass_fields__}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(tmp_path, fail_rank=-1):
+    mp.start_processes(_worker, args=(_free_port(), str(tmp_path), fail_rank), nprocs=WORLD,
+                       join=True, start_method="spawn")
+    return np.load(os.path.join(tmp_path, "r0.npz"))
+
+
+def test_rank_bounds_cover_and_balance():
+    cost = np.array([5, 1, 1, 1, 1, 1, 5, 1], np.float64)
+    b = wdist.rank_bounds(cost, 2)
+    assert b[0][0] == 0 and b[-1][1] == len(cost) and b[0][1] == b[1][0]
+    assert wdist.rank_bounds(cost[:1], 4) == [(0, 1), (1, 1), (1, 1), (1, 1)]
+    assert wdist.rank_bounds(np.zeros(0), 3) == [(0, 0)] * 3
+
+
+def test_two_rank_gloo_shards_match_unsharded(tmp_path):
+    r = _run(tmp_path)
+    assert str(r["outcome"]) == "ok"
+    assert float(r["tmax"]) == 2.0                    # max over ranks, not rank 0's value
+    for f in engine.Results.__dataclass_fields__:
+        np.testing.assert_array_equal(r["got_" + f], r["want_" + f], err_msg=f)
+
+
+def test_two_rank_gloo_error_reaches_every_rank(tmp_path):
+    r = _run(tmp_path, fail_rank=1)
+    # rank 1's shard-local contig 1 is reported as a batch contig index (>= its shard base)
+    kind, code, contigs = str(r["outcome"]).split(":")
+    assert kind == "err" and int(code) == L.WF_E_RUNAWAY
+    assert eval(contigs)[0] > 1

@@ -79,6 +79,10 @@ class WaafleHipError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("libwaafle_hip error {}: {}".format(code, msg))
         self.code = code
+        self.msg = msg
+
+    def __reduce__(self):   # picklable across ranks (keeps the failing contig indices)
+        return (type(self), (self.code, self.msg), {"contigs": getattr(self, "contigs", ())})
 
 
 def load(path=LIB_PATH):

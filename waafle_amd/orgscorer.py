@@ -9,6 +9,7 @@ import sys
 import time
 
 from . import cli, engine, inputs, lib, output
+from . import dist as wdist
 
 
 def die(*args):
@@ -33,14 +34,35 @@ def main(argv=None):
     say("Analyzing {:,} contigs ({:,} hits, {:,} loci) on {} GPU(s).".format(
         batch.n_contigs, batch.n_hits, batch.n_loci, args.gpus))
     t1 = time.time()
+    rank, world, local = wdist.rank_env()
+    group = None
+    if world > 1:   # launched by torch.distributed.run: one process per GPU
+        import torch
+        import torch.distributed as group
+        torch.cuda.set_device(local)
+        group.init_process_group("nccl", device_id=torch.device("cuda", local))
     try:
-        res = engine.score(batch, tax, cli.param_dict(args), gpus=args.gpus)
+        if group is None:
+            res = engine.score(batch, tax, cli.param_dict(args), gpus=args.gpus)
+        else:
+            scorer = engine.GpuScorer(local)
+            scorer.set_taxonomy(tax)
+            try:
+                res = wdist.score_ranked(batch, tax, cli.param_dict(args),
+                                         lambda sub: scorer.score(sub, cli.param_dict(args)),
+                                         group)
+            finally:
+                scorer.close()
     except lib.WaafleHipError as exc:
         if exc.code == lib.WF_E_RUNAWAY and len(getattr(exc, "contigs", ())):
             die("  Warning: Runaway taxonomic recursion for",
                 batch.contig_names[int(exc.contigs[0])])
         die(str(exc))
     t2 = time.time()
+    if group is not None:
+        group.destroy_process_group()
+        if rank != 0:
+            return
     say("Initializing outputs.")
     rows = output.render(batch, tax, res)
     output.write(rows, args.outdir, args.basename)
