@@ -34,6 +34,7 @@ def parse_args():
     ap.add_argument("--contigs", type=int, default=None, help="override contigs per GPU")
     ap.add_argument("--lds-bytes", type=int, default=None)
     ap.add_argument("--threads", type=int, default=None, help="threads per contig (64/128/256)")
+    ap.add_argument("--mode", default="fused", choices=["staged", "fused"])
     ap.add_argument("--cpu-sample", type=int, default=1500,
                     help="contigs timed on the CPU oracle (rank 0, N=1); 0 disables")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_cfg2.json"))
@@ -132,6 +133,7 @@ def main():
     h = C.c_void_p()
     assert so.wf_init(local, C.byref(h)) == 0, "wf_init failed"
     chk = lambda rc: (_ for _ in ()).throw(RuntimeError(so.wf_last_error(h).decode())) if rc else None
+    chk(so.wf_set_mode(h, engine.MODES[args.mode]))
     if args.lds_bytes:
         chk(so.wf_set_lds_bytes(h, args.lds_bytes))
     if args.threads:

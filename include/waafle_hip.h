@@ -38,6 +38,14 @@ enum wf_status {
 
 enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
 
+/* Execution form of wf_score (same results either way):
+ *  WF_MODE_STAGED: one flat kernel per phase over all contigs (hits, attachments,
+ *    a device radix sort per roll-up level, segments, per-contig decisions); synchronises
+ *    on the context stream between roll-up levels.
+ *  WF_MODE_FUSED (default): one workgroup carries a contig through every phase (LDS tiers + an HBM
+ *    workspace tier); fully asynchronous when the batch is device resident. */
+enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_FUSED = 1 };
+
 typedef struct wf_ctx wf_ctx;
 
 /* Interned taxonomy.  Ids are the ranks of all names (taxonomy file names, hit taxa,
@@ -142,6 +150,7 @@ int wf_set_stream(wf_ctx* ctx, void* hip_stream);     /* NULL = the context's ow
 int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes);     /* dynamic LDS per workgroup */
 int wf_set_workgroup(wf_ctx* ctx, int threads);       /* threads per contig: 64, 128, 256 */
 int wf_set_tier2_lds_bytes(wf_ctx* ctx, int64_t bytes); /* LDS of the overflow tier */
+int wf_set_mode(wf_ctx* ctx, int mode);               /* WF_MODE_STAGED / WF_MODE_FUSED */
 int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* tax);
 int wf_score(wf_ctx* ctx, const wf_batch* batch, const wf_params* params, wf_result* out);
 int wf_synchronize(wf_ctx* ctx);

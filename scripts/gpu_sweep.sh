@@ -5,7 +5,7 @@ timeout -k 10 900 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > $O/gp
 echo "pytest rc=$rc" >> $O/gpu_tests.log
 if [ $rc -ge 124 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py --cpu-sample 0 > $O/bench.json 2> $O/bench.err || exit $?
-timeout -k 10 600 python scripts/sweep.py ${GEOMS:+--geoms $GEOMS} > $O/sweep_occ4.txt 2>&1 || exit $?
+timeout -k 10 600 python scripts/sweep.py ${GEOMS:+--geoms $GEOMS} > $O/sweep_product.txt 2>&1 || exit $?
 if [ -n "${VARIANT:-}" ]; then
   timeout -k 10 600 python scripts/sweep.py --lib waafle_amd/libwaafle_hip_${VARIANT}.so ${GEOMS:+--geoms $GEOMS} > $O/sweep_${VARIANT}.txt 2>&1 || exit $?
 fi

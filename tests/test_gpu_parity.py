@@ -20,9 +20,10 @@ FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n
           "n_meld2", "annot_hit", "pair_evals", "iterations", "status")
 
 
-@pytest.fixture(scope="module")
-def scorer():
-    s = engine.GpuScorer(0)
+@pytest.fixture(scope="module", params=["staged", "fused"])
+def scorer(request):
+    s = engine.GpuScorer(0, mode=request.param)
+    s.mode = request.param
     yield s
     s.close()
 
@@ -160,10 +161,12 @@ def test_full_size_cfg2_properties(scorer):
     a = scorer.score(batch, params)
     b = scorer.score(batch, params)
     assert_same_results(a, b, batch)
-    for kw in (dict(lds_bytes=8192),                          # tier 1 -> tier 2
-               dict(lds_bytes=8192, tier2_lds_bytes=8192),    # -> tier 3 (HBM workspace)
-               dict(threads=256, lds_bytes=36864),            # 4 waves per contig
-               dict(threads=128, lds_bytes=24576)):
+    for kw in (dict(mode=scorer.mode, lds_bytes=8192),        # fused: tier 1 -> tier 2;
+                                                              # staged: HBM decision slots
+               dict(mode="fused", lds_bytes=8192, tier2_lds_bytes=8192),  # -> tier 3
+               dict(mode="fused", threads=256, lds_bytes=36864),  # 4 waves per contig
+               dict(mode="fused", threads=128, lds_bytes=24576),
+               dict(mode="staged")):
         small = engine.GpuScorer(0, **kw)
         small.set_taxonomy(tax)
         c = small.score(batch, params)

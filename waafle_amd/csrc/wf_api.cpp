@@ -47,6 +47,10 @@ struct wf_ctx {
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> ev_lds, ev_big;  // indices into ev_pool
   int64_t launches = 0, overflow_contigs = 0;
+  // path: WF_MODE_STAGED (flat kernels per phase) or WF_MODE_FUSED (workgroup per contig)
+  int mode = WF_MODE_FUSED;
+  bool lds_set = false;            // wf_set_lds_bytes called: also the staged decision arena
+  wf::StagedState* staged = nullptr;
 };
 
 namespace {
@@ -225,6 +229,7 @@ void wf_free(wf_ctx* ctx) {
                     &ctx->r_syn, &ctx->r_nm1, &ctx->r_nm2, &ctx->r_meld, &ctx->r_annot,
                     &ctx->r_pairs, &ctx->r_status, &ctx->r_need};
   for (DevBuf* b : bufs) release(*b);
+  if (ctx->staged) wf::staged_destroy(ctx->staged);
   for (hipEvent_t ev : ctx->ev_pool) hipEventDestroy(ev);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
   delete ctx;
@@ -243,6 +248,7 @@ int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes) {
   if (bytes < 4096 || bytes > 152 * 1024)
     return fail(ctx, WF_E_BADINPUT, "LDS budget %lld out of [4096, 155648]", (long long)bytes);
   ctx->lds_bytes = bytes;
+  ctx->lds_set = true;
   return WF_OK;
 }
 
@@ -259,6 +265,14 @@ int wf_set_tier2_lds_bytes(wf_ctx* ctx, int64_t bytes) {
   if (bytes < 4096 || bytes > 152 * 1024)
     return fail(ctx, WF_E_BADINPUT, "LDS budget %lld out of [4096, 155648]", (long long)bytes);
   ctx->lds2_bytes = bytes;
+  return WF_OK;
+}
+
+int wf_set_mode(wf_ctx* ctx, int mode) {
+  if (!ctx) return WF_E_BADINPUT;
+  if (mode != WF_MODE_STAGED && mode != WF_MODE_FUSED)
+    return fail(ctx, WF_E_BADINPUT, "mode must be WF_MODE_STAGED (0) or WF_MODE_FUSED (1)");
+  ctx->mode = mode;
   return WF_OK;
 }
 
@@ -338,6 +352,24 @@ static int check_batch(wf_ctx* ctx, const wf_batch* b, const wf_params* p, const
 // overflow list).  Everything is enqueued on the context stream; no host synchronisation.
 static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   int rc;
+  if (ctx->mode == WF_MODE_STAGED) {
+    K.root = ctx->root;
+    K.unknown = ctx->unknown;
+    if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
+    if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
+    std::pair<int, int> el{-1, -1};
+    if (ctx->timing) {
+      take_event_pair(ctx, ctx->ev_lds);
+      el = ctx->ev_lds.back();
+      HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
+    }
+    std::string err;
+    rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, ctx->stream, &err);
+    if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : WF_E_HIP, "%s", err.c_str());
+    if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
+    ++ctx->launches;
+    return WF_OK;
+  }
   const size_t list_bytes = sizeof(int32_t) * (size_t)std::max(b->n_contigs, 1);
   if ((rc = ensure(ctx, ctx->ovf_list, list_bytes)) || (rc = ensure(ctx, ctx->ovf2_list, list_bytes)) ||
       (rc = ensure(ctx, ctx->ovf_count, 64)))

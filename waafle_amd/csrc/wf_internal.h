@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace wf {
 
 constexpr int kBlock = 256;             // 4 waves of 64 lanes per contig workgroup
@@ -43,6 +45,38 @@ struct KArgs {
   const int32_t* work_list; const int32_t* work_count;   // list the big kernel drains
   char* big_ws; int64_t slot_bytes; int64_t lds_bytes; int lds_threads;
 };
+
+// Staged pipeline state (wf_staged.hip): flat kernels over all hits / attachments /
+// segments, a device radix sort per roll-up level, one decision workgroup per contig.
+struct SArgs {
+  KArgs k;                       // batch, taxonomy, params, results (k.big_ws: tier-3 slots)
+  int n_hits_i;                  // hits in the batch (int range checked on the host)
+  int key_lb, key_tb;            // key = crank << (tb + lb) | clade << lb | locus
+  const int32_t* hit_contig;     // [n_hits]
+  const int64_t* att_off;        // [n_hits + 1] exclusive scan of attachments per hit
+  int32_t *att_lo, *att_hi, *att_loc, *att_clade, *att_hit;
+  double* att_sc;
+  // current level
+  uint64_t* keys;  int32_t* vals;             // sorted (key, attachment) pairs
+  int32_t* flags;  int32_t* seg_id;           // segment starts / inclusive scan
+  int32_t* seg_start; int32_t* seg_crank; double* seg_mean;
+  const int32_t* act;  const int64_t* act_base;   // active contigs of this level
+  int32_t* act_next; int64_t* act_base_next;      // raised contigs (next level)
+  unsigned long long* counters;  // [0] next active, [1] next attachments, [2] big count
+  int32_t* big_list;             // contigs whose decision state needs an HBM slot
+  const int32_t* lut_off;        // [kNpyBuf + 2] numpy leaf table offsets by length
+  const int4* lut;               // (start, length, parent adds) per leaf
+  int64_t dec_lds_bytes;         // LDS arena of the decision workgroup
+};
+
+struct StagedState;
+StagedState* staged_create(int device);
+void staged_destroy(StagedState* st);
+void staged_set_lds(StagedState* st, int64_t bytes);
+// Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2 with
+// the message in *err (-1 bad input, -2 HIP failure).
+int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipStream_t s,
+                 std::string* err);
 
 // `dk` points to a device copy of the host-side `k` (enqueued before the launch).
 hipError_t launch_lds_kernel(const KArgs& k, const KArgs* dk, hipStream_t s);

@@ -1,707 +1,16 @@
-// HIP kernels for the waafle_orgscorer contig-scoring hot path (gfx950 / MI355X).
-//
-// One 256-thread workgroup scores one contig end to end: hit->locus attachment
-// (orgscorer.py:359-392), per-(clade, locus) site-score means in numpy's exact
-// pairwise float64 order (:394-429), the taxonomy roll-up loop (:431-445, :566-583),
-// the one-clade search + meld (:585-597, :621-631) and the all-pairs two-clade search
-// + meld + LGT filters (:599-619, :633-744).  The per-contig state lives in LDS
-// (k_contig_lds); contigs whose state does not fit the LDS budget are re-run by
-// k_contig_big with the same code on a per-workgroup HBM workspace slot.
-//
-// Exactness rules: device code is compiled with -ffp-contract=off (no fma fusion), fp64
-// division is IEEE-correct, and every float64 sum follows numpy's add.reduce order
-// (8192-element buffers added sequentially from 0.0; each buffer summed pairwise with
-// 128-element leaves of eight strided accumulators).
-#include "wf_internal.h"
-
-#include "waafle_hip.h"
+// HIP kernels for the waafle_orgscorer contig-scoring hot path (gfx950 / MI355X), fused
+// form: one workgroup scores one contig end to end -- hit->locus attachment
+// (orgscorer.py:359-392), per-(clade, locus) site-score means in numpy's exact pairwise
+// float64 order (:394-429), the taxonomy roll-up loop (:431-445, :566-583), the one-clade
+// search + meld (:585-597, :621-631) and the all-pairs two-clade search + meld + LGT
+// filters (:599-619, :633-744).  The per-contig state lives in LDS (k_contig_lds);
+// contigs whose state does not fit are re-run by k_contig_big with the same code on a
+// per-workgroup HBM workspace slot.
+#include "wf_device.h"
 
 namespace wf {
 
 namespace {
-
-constexpr uint64_t kKeyPad = ~0ull;
-
-// Diagnostic build only (-DWF_STAMPS): thread 0 accumulates shader-clock deltas per phase,
-// always taken right after a workgroup barrier.  Never compiled into the product build.
-#ifdef WF_STAMPS
-__device__ unsigned long long g_stamps[32];
-#define STAMP_INIT() unsigned long long t_last_ = __builtin_amdgcn_s_memtime()
-#define STAMP(i)                                                                    \
-  do {                                                                              \
-    if (threadIdx.x == 0) {                                                         \
-      unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
-      atomicAdd(&g_stamps[i], now_ - t_last_);                                      \
-      t_last_ = now_;                                                               \
-    }                                                                               \
-  } while (0)
-#else
-#define STAMP_INIT() do {} while (0)
-#define STAMP(i) do {} while (0)
-#endif
-constexpr int kLocVirtual = 0xFFFF;     // locus field of the virtual "Unknown" key
-
-struct Ctl {
-  int A, A1, npow, S_n, P, Gu, Pp;
-  int overflow, status, cnt, cnt2, p_unk, root_present, all_ignored;
-  int n_in, all_ok, all_same, best_ok, best_dir, best_c1p, best_c2p;
-  int lca1, lca2, res_kind, lca_out;
-  int cls_cnt[5], cls_off[5];
-  double best_r, best_crit;
-  long long best_k;
-  int64_t need;
-  double red_r[kWaves];
-  long long red_k[kWaves];
-  int red_i[kWaves];
-  int red_j[kWaves];
-};
-
-__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
-
-struct Arena {
-  char* base;
-  int64_t cap;
-  int64_t used;
-  template <class T>
-  __device__ __forceinline__ T* take(int64_t count) {
-    int64_t off = (used + 15) & ~int64_t(15);
-    used = off + count * (int64_t)sizeof(T);
-    return reinterpret_cast<T*>(base + off);
-  }
-  __device__ __forceinline__ bool fits() const { return used <= cap; }
-};
-
-__device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
-
-// --------------------------------------------------------------------------
-// block-wide primitives
-// --------------------------------------------------------------------------
-
-// Exclusive prefix sum of one int per thread; *total receives the block sum.
-template <int NT>
-__device__ __forceinline__ int block_scan(int v, int* total, Ctl& ctl) {
-  const int lane = lane_id(), w = wave_id();
-  int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) ctl.red_i[w] = x;
-  __syncthreads();
-  int base = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < NT / 64; ++i) {
-    int t = ctl.red_i[i];
-    base += (i < w) ? t : 0;
-    tot += t;
-  }
-  __syncthreads();
-  *total = tot;
-  return base + x - v;
-}
-
-// Two exclusive prefix sums at once.
-template <int NT>
-__device__ __forceinline__ void block_scan2(int v1, int v2, int* p1, int* p2, int* t1, int* t2, Ctl& ctl) {
-  const int lane = lane_id(), w = wave_id();
-  int x = v1, y = v2;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    int a = __shfl_up(x, d, 64), b = __shfl_up(y, d, 64);
-    if (lane >= d) { x += a; y += b; }
-  }
-  if (lane == 63) { ctl.red_i[w] = x; ctl.red_j[w] = y; }
-  __syncthreads();
-  int b1 = 0, b2 = 0, s1 = 0, s2 = 0;
-#pragma unroll
-  for (int i = 0; i < NT / 64; ++i) {
-    int a = ctl.red_i[i], b = ctl.red_j[i];
-    if (i < w) { b1 += a; b2 += b; }
-    s1 += a;
-    s2 += b;
-  }
-  __syncthreads();
-  *p1 = b1 + x - v1;
-  *p2 = b2 + y - v2;
-  *t1 = s1;
-  *t2 = s2;
-}
-
-// (rank, key) maximum; ties on rank go to the larger key (= later in enumeration order,
-// which is what `sorted(options, key=rank)[-1]` picks, orgscorer.py:623-624, 634-635).
-__device__ __forceinline__ bool better(double r2, long long k2, double r, long long k) {
-  return k2 >= 0 && (k < 0 || r2 > r || (r2 == r && k2 > k));
-}
-
-template <int NT>
-__device__ __forceinline__ void block_argmax(double& r, long long& k, Ctl& ctl) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    double r2 = __shfl_xor(r, off, 64);
-    long long k2 = __shfl_xor(k, off, 64);
-    if (better(r2, k2, r, k)) { r = r2; k = k2; }
-  }
-  if (lane_id() == 0) { ctl.red_r[wave_id()] = r; ctl.red_k[wave_id()] = k; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double br = ctl.red_r[0];
-    long long bk = ctl.red_k[0];
-    for (int i = 1; i < NT / 64; ++i)
-      if (better(ctl.red_r[i], ctl.red_k[i], br, bk)) { br = ctl.red_r[i]; bk = ctl.red_k[i]; }
-    ctl.best_r = br;
-    ctl.best_k = bk;
-  }
-  __syncthreads();
-  r = ctl.best_r;
-  k = ctl.best_k;
-}
-
-template <int NT, class T>
-__device__ __forceinline__ void bitonic_sort(T* keys, int n) {
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += NT) {
-        int ixj = i ^ j;
-        if (ixj > i) {
-          T a = keys[i], b = keys[ixj];
-          bool up = (i & k) == 0;
-          if ((a > b) == up) { keys[i] = b; keys[ixj] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// --------------------------------------------------------------------------
-// taxonomy helpers (utils.py:401-411)
-// --------------------------------------------------------------------------
-
-__device__ __forceinline__ int lca2(const KArgs& K, int a, int b) {
-  if (a < 0) return b;
-  if (b < 0) return a;
-  int da = K.depth[a], db = K.depth[b];
-  while (da > db) { a = K.parent[a]; --da; }
-  while (db > da) { b = K.parent[b]; --db; }
-  while (a != b) { a = K.parent[a]; b = K.parent[b]; }
-  return a;
-}
-
-// LCA of list[0..m) (clade ids); wave 0 folds, result broadcast through ctl.
-__device__ __forceinline__ int block_lca(const KArgs& K, const int* list, int m, Ctl& ctl) {
-  if (m <= 0) return -1;
-  if (m == 1) return list[0];
-  if (wave_id() == 0) {
-    int acc = -1;
-    for (int i = lane_id(); i < m; i += 64) acc = lca2(K, acc, list[i]);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      int o = __shfl_xor(acc, off, 64);
-      acc = lca2(K, acc, o);
-    }
-    if (lane_id() == 0) ctl.lca_out = acc;
-  }
-  __syncthreads();
-  int r = ctl.lca_out;
-  __syncthreads();
-  return r;
-}
-
-// --------------------------------------------------------------------------
-// numpy pairwise summation order
-// --------------------------------------------------------------------------
-
-constexpr int kMaxDepth = 7;   // internal-node depths of one <=8192-element buffer: 0..6
-constexpr int kGroupMax = 64;  // leaves combined by lane shuffles (one 8192 buffer = 64)
-
-// Leaves of numpy's pairwise sum over one buffer [off0, off0+cl): emitted left to right
-// as (start, length, number of parent additions completed right after this leaf).  The
-// frame stack is a shift register (static indices) so it stays in VGPRs; depth <= 8.
-// If `sched` is given (kMaxDepth rows of `stride` bytes, pre-set to -1) it also records
-// the combine schedule: sched[d][i] = j when leaf i is the leftmost leaf of an internal
-// node at depth d whose right child starts at leaf j.
-__device__ int gen_leaves(int off0, int cl, int4* out, int8_t* sched = nullptr, int stride = 0) {
-  int so[8], sl[8], ss[8], sf[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) { so[i] = 0; sl[i] = 0; ss[i] = 0; sf[i] = 0; }
-  int cnt = 0;
-  auto push = [&](int o, int l) {
-#pragma unroll
-    for (int i = 7; i > 0; --i) { so[i] = so[i - 1]; sl[i] = sl[i - 1]; ss[i] = ss[i - 1]; sf[i] = sf[i - 1]; }
-    so[0] = o; sl[0] = l; ss[0] = 0; sf[0] = cnt;
-  };
-  auto pop = [&]() {
-#pragma unroll
-    for (int i = 0; i < 7; ++i) { so[i] = so[i + 1]; sl[i] = sl[i + 1]; ss[i] = ss[i + 1]; sf[i] = sf[i + 1]; }
-  };
-  int sp = 1;
-  so[0] = off0; sl[0] = cl; ss[0] = 0; sf[0] = 0;
-  while (sp > 0) {
-    if (sl[0] > kLeafMax && ss[0] == 0) {
-      int h = sl[0] / 2;
-      h -= h % 8;
-      ss[0] = 1;
-      push(so[0], h);
-      ++sp;
-      continue;
-    }
-    const int lo = so[0], ll = sl[0];
-    int adds = 0;
-    pop();
-    --sp;
-    ++cnt;
-    while (sp > 0) {
-      if (ss[0] == 1) {
-        int h = sl[0] / 2;
-        h -= h % 8;
-        ss[0] = 2;
-        if (sched && sp - 1 < kMaxDepth && sf[0] < stride)
-          sched[(sp - 1) * stride + sf[0]] = (int8_t)cnt;
-        push(so[0] + h, sl[0] - h);
-        ++sp;
-        break;
-      }
-      ++adds;
-      pop();
-      --sp;
-    }
-    if (out) out[cnt - 1] = make_int4(lo, ll, adds, 0);
-  }
-  return cnt;
-}
-
-__device__ int leaves_of_length(int n) {
-  int cnt = 0;
-  for (int o = 0; o < n; o += kNpyBuf) cnt += gen_leaves(o, min(kNpyBuf, n - o), nullptr);
-  return cnt;
-}
-
-// One leaf (<= 128 elements) exactly as numpy's pairwise_sum inner block.
-template <class F>
-__device__ double serial_block(int o, int l, F f) {
-  if (l < 8) {
-    double r = 0.0;
-    for (int i = 0; i < l; ++i) r += f(o + i);
-    return r;
-  }
-  double r0 = f(o), r1 = f(o + 1), r2 = f(o + 2), r3 = f(o + 3);
-  double r4 = f(o + 4), r5 = f(o + 5), r6 = f(o + 6), r7 = f(o + 7);
-  int i = 8;
-  const int m = l - (l & 7);
-  for (; i < m; i += 8) {
-    r0 += f(o + i); r1 += f(o + i + 1); r2 += f(o + i + 2); r3 += f(o + i + 3);
-    r4 += f(o + i + 4); r5 += f(o + i + 5); r6 += f(o + i + 6); r7 += f(o + i + 7);
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < l; ++i) res += f(o + i);
-  return res;
-}
-
-template <class F>
-__device__ double serial_pairwise(int off0, int cl, F f) {
-  if (cl <= kLeafMax) return serial_block(off0, cl, f);
-  int foff[16], flen[16], fst[16];
-  double facc[16];
-  int sp = 1;
-  foff[0] = off0; flen[0] = cl; fst[0] = 0;
-  for (;;) {
-    int t = sp - 1;
-    if (flen[t] > kLeafMax && fst[t] == 0) {
-      int h = flen[t] / 2;
-      h -= h % 8;
-      fst[t] = 1;
-      foff[sp] = foff[t]; flen[sp] = h; fst[sp] = 0;
-      ++sp;
-      continue;
-    }
-    double val = serial_block(foff[t], flen[t], f);
-    --sp;
-    for (;;) {
-      if (sp == 0) return val;
-      int u = sp - 1;
-      if (fst[u] == 1) {
-        int h = flen[u] / 2;
-        h -= h % 8;
-        facc[u] = val;
-        fst[u] = 2;
-        foff[sp] = foff[u] + h; flen[sp] = flen[u] - h; fst[sp] = 0;
-        ++sp;
-        break;
-      }
-      val = facc[u] + val;
-      --sp;
-    }
-  }
-}
-
-// np.add.reduce over f(0..n) (one thread).
-template <class F>
-__device__ double np_sum(int n, F f) {
-  double total = 0.0;
-  for (int o = 0; o < n; o += kNpyBuf) total += serial_pairwise(o, min(kNpyBuf, n - o), f);
-  return total;
-}
-
-// --------------------------------------------------------------------------
-// per-contig state
-// --------------------------------------------------------------------------
-
-struct Contig {
-  int64_t h0, l0, mbase;
-  int H, G;
-  // persistent
-  int *loc_lo, *loc_len, *loc_st, *leaf_off;
-  int *loc_grp, *loc_steps, *sched_off;   // lane-group size, combine steps, schedule offset
-  int8_t* sched;
-  int4* leaves;
-  int *alo, *ahi, *ahit, *aloc, *acl;
-  double* asc;
-  uint64_t* maxes;
-  int *ign, *um;
-  // per level
-  uint64_t* keys;
-  int *seg_start, *seg_cl, *cl_id, *pot, *mem1, *mem2, *sorder;
-  double* S;
-  uint64_t* mask;
-  unsigned *bm1, *bm2;
-  uint8_t* best_syn;
-};
-
-// Shift-register stack of partial sums for numpy's pairwise tree.  Static indexing keeps
-// it in VGPRs; 8 entries cover the deepest tree of one 8192-element buffer (depth 7).
-struct SumStack {
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, s4 = 0.0, s5 = 0.0, s6 = 0.0, s7 = 0.0;
-  __device__ __forceinline__ void push(double v) {
-    s7 = s6; s6 = s5; s5 = s4; s4 = s3; s3 = s2; s2 = s1; s1 = s0; s0 = v;
-  }
-  __device__ __forceinline__ void add_top() {   // (left) + (right), left pushed first
-    s0 = s1 + s0;
-    s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = s7;
-  }
-};
-
-// Sequential float64 sum of `cnt` copies of v, starting from 0.0 (the value a strided
-// accumulator reaches over `cnt` covered sites of a constant run; zeros add nothing).
-__device__ __forceinline__ double seqsum(double v, int cnt) {
-  double r = 0.0;
-  for (int i = 0; i < cnt; ++i) r += v;
-  return r;
-}
-
-__device__ __forceinline__ double leaf_tree(double r0, double r1, double r2, double r3, double r4,
-                                            double r5, double r6, double r7) {
-  return ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-}
-
-// Number of t in [0, m) with base + 8t < bound.
-__device__ __forceinline__ int below(int base, int bound, int m) {
-  const int d = bound - base;
-  return d <= 0 ? 0 : min(m, (d + 7) >> 3);
-}
-
-constexpr int kRegAtt = 4;   // attachments of a segment held in registers
-
-// The attachments of one (clade, locus) segment -- sorted keys [kb, ke) -- and the exact
-// numpy value of one pairwise-sum leaf of its site array.  Site x holds
-// max(0, max{score_a : lo_a <= x < hi_a}).
-struct SegAtt {
-  int kb, ke;
-  bool reg;
-  int lo[kRegAtt], hi[kRegAtt];
-  double sc[kRegAtt];
-
-  __device__ __forceinline__ void load(const Contig& C, int kb_, int ke_) {
-    kb = kb_; ke = ke_;
-    reg = ke - kb <= kRegAtt;
-#pragma unroll
-    for (int i = 0; i < kRegAtt; ++i) {
-      const bool use = reg && kb + i < ke;
-      const int a = use ? (int)(C.keys[kb + i] & 0xFFFFFFull) : 0;
-      lo[i] = use ? C.alo[a] : 0;
-      hi[i] = use ? C.ahi[a] : 0;          // lo == hi: never covers
-      sc[i] = use ? C.asc[a] : 0.0;
-    }
-  }
-  __device__ __forceinline__ void get(const Contig& C, int t, int& l, int& h, double& v) const {
-    const int a = (int)(C.keys[t] & 0xFFFFFFull);
-    l = C.alo[a]; h = C.ahi[a]; v = C.asc[a];
-  }
-  __device__ __forceinline__ double value_at(const Contig& C, int x) const {
-    double v = 0.0;
-    if (reg) {
-#pragma unroll
-      for (int i = 0; i < kRegAtt; ++i)
-        if (x >= lo[i] && x < hi[i]) v = sc[i] > v ? sc[i] : v;
-    } else {
-      for (int t = kb; t < ke; ++t) {
-        int l, h; double s;
-        get(C, t, l, h, s);
-        if (x >= l && x < h) v = s > v ? s : v;
-      }
-    }
-    return v;
-  }
-  // numpy's leaf: 8 strided accumulators over the body of 8m sites, combined as
-  // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the tail added in order.  Accumulator c
-  // adds the sites st+c+8t, t = 0..m-1, sequentially from 0.0.  All closed forms below are
-  // bit-identical to that sequence (adding +0.0 to a non-negative partial sum is exact and
-  // a constant v added k times from 0.0 is seqsum(v, k)):
-  //  - constant envelope F over the body: every r_c = seqsum(F, m), and r summed by the
-  //    tree is 8*seqsum(F, m) (each level doubles exactly);
-  //  - one nonzero run s over a zero background (a hit boundary inside the leaf, ~97% of
-  //    the non-constant leaves): r_c = seqsum(s, k_c), where k_c = the sites of run in
-  //    lane c's stride spans at most 3 adjacent values;
-  //  - otherwise the envelope's runs are walked once in site order and each run's value
-  //    is added k_c times to every accumulator (interleaved, no per-accumulator search).
-  template <bool REG>
-  __device__ __forceinline__ void att(const Contig& C, int i, int& l, int& h, double& v) const {
-    if (REG) { l = lo[i]; h = hi[i]; v = sc[i]; } else get(C, kb + i, l, h, v);
-  }
-  template <bool REG>
-  __device__ __forceinline__ double body_sum(const Contig& C, int st, int m) const {
-    const int be = st + (m << 3);
-    const int na = REG ? kRegAtt : ke - kb;
-    double F = 0.0;
-#pragma unroll
-    for (int i = 0; i < na; ++i) {
-      int l, h; double v;
-      att<REG>(C, i, l, h, v);
-      if (l < h && l <= st && be <= h) F = v > F ? v : F;
-    }
-    int npos = 0, plo = 0, phi = 0;
-    double ps = 0.0;
-#pragma unroll
-    for (int i = 0; i < na; ++i) {
-      int l, h; double v;
-      att<REG>(C, i, l, h, v);
-      if (l < h && l < be && h > st && !(l <= st && be <= h) && v > F) {
-        ++npos; plo = l; phi = h; ps = v;
-      }
-    }
-    if (npos == 0) return F > 0.0 ? 8.0 * seqsum(F, m) : 0.0;
-    double r[8];
-    if (npos == 1 && !(F > 0.0)) {
-      int k[8], kmin = m;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        k[c] = below(st + c, phi, m) - below(st + c, plo, m);
-        kmin = min(kmin, k[c]);
-      }
-      const double s0 = seqsum(ps, kmin), s1 = s0 + ps, s2 = s1 + ps;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) r[c] = k[c] == kmin ? s0 : (k[c] == kmin + 1 ? s1 : s2);
-      return leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
-    }
-#pragma unroll
-    for (int c = 0; c < 8; ++c) r[c] = 0.0;
-    for (int x = st; x < be;) {
-      double v = 0.0;
-      int nx = be;
-#pragma unroll
-      for (int i = 0; i < na; ++i) {
-        int l, h; double s;
-        att<REG>(C, i, l, h, s);
-        if (l < h) {
-          if (l <= x && x < h) { v = s > v ? s : v; nx = min(nx, h); }
-          else if (l > x) nx = min(nx, l);
-        }
-      }
-      if (v > 0.0) {
-        int k[8], kmax = 0;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          k[c] = below(st + c, nx, m) - below(st + c, x, m);
-          kmax = max(kmax, k[c]);
-        }
-        for (int q = 0; q < kmax; ++q) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) r[c] = q < k[c] ? r[c] + v : r[c];
-        }
-      }
-      x = nx;
-    }
-    return leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
-  }
-  __device__ __forceinline__ double leaf(const Contig& C, int st, int ln) const {
-    const int m = ln >> 3, be = st + (m << 3);
-    double res = 0.0;
-    if (m > 0) res = reg ? body_sum<true>(C, st, m) : body_sum<false>(C, st, m);
-    for (int x = be; x < st + ln; ++x) res += value_at(C, x);
-    return res;
-  }
-};
-
-// Exact np.mean of one (clade, locus) site array (orgscorer.py:399-406) by one thread:
-// leaves in order, combined on a shift-register stack; 8192-element buffers added from
-// 0.0 (numpy NPY_BUFSIZE).  Used for loci too long for the lane-parallel path.
-__device__ __forceinline__ double segment_mean(const Contig& C, int g, int kb, int ke) {
-  const int n = C.loc_len[g];
-  const int4* lv = C.leaves + C.leaf_off[g];
-  const int nl = C.leaf_off[g + 1] - C.leaf_off[g];
-  const int full_bufs = n / kNpyBuf;
-  SegAtt at;
-  at.load(C, kb, ke);
-  SumStack stk;
-  double total = 0.0;
-  for (int j = 0; j < nl; ++j) {
-    const int4 e = lv[j];
-    stk.push(at.leaf(C, e.x, e.y));
-    for (int a = 0; a < e.z; ++a) stk.add_top();
-    if (j == nl - 1 || (((j + 1) & 63) == 0 && ((j + 1) >> 6) <= full_bufs)) {
-      total += stk.s0;
-      stk.s0 = 0.0;
-    }
-  }
-  return total / (double)n;
-}
-
-// Lane-parallel site means: a group of gs lanes (8/16/32/64) takes one segment whose locus
-// has <= gs leaves in a single numpy buffer; lane i computes leaf i, then the pairwise
-// tree is combined bottom-up with lane shuffles following the locus' schedule (lane i
-// adds lane j's partial sum when i starts an internal node whose right child starts at
-// j), so every addition is numpy's (left + right).  `list` holds the class's segments.
-template <int NW>
-__device__ __forceinline__ void site_means_grouped(const Contig& C, const int* list, int count, int gs) {
-  const int lane = lane_id(), w = wave_id();
-  const int per_round = 64 / gs, gi = lane / gs, li = lane % gs;
-  for (int base = w * per_round; base < count; base += NW * per_round) {
-    const int idx = base + gi;
-    const bool has = idx < count;
-    const int s = has ? list[idx] : 0;
-    const int kb = has ? C.seg_start[s] : 0, ke = has ? C.seg_start[s + 1] : 0;
-    const int g = has ? (int)((C.keys[kb] >> 24) & 0xFFFF) : 0;
-    const int nl = has ? C.leaf_off[g + 1] - C.leaf_off[g] : 0;
-    double v = 0.0;
-    if (has && li < nl) {
-      SegAtt at;
-      at.load(C, kb, ke);
-      const int4 e = C.leaves[C.leaf_off[g] + li];
-      v = at.leaf(C, e.x, e.y);
-    }
-    const int steps = has ? C.loc_steps[g] : 0;
-    int maxsteps = steps;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) maxsteps = max(maxsteps, __shfl_xor(maxsteps, off, 64));
-    const int8_t* sch = C.sched + (has ? C.sched_off[g] : 0);
-    for (int d = maxsteps - 1; d >= 0; --d) {
-      const int src = (has && d < steps) ? (int)sch[d * gs + li] : -1;
-      const double o = __shfl(v, src >= 0 ? gi * gs + src : lane, 64);
-      if (src >= 0) v = v + o;
-    }
-    if (has && li == 0) C.S[(int64_t)C.seg_cl[s] * C.G + g] = v / (double)C.loc_len[g];
-  }
-}
-
-// --- two-clade option evaluation (orgscorer.py:511-545, 678-744), one thread ---------
-struct OptEval {
-  int ok, swapped, dir, same, c1p, c2p;
-};
-
-__device__ __forceinline__ uint8_t two_char(const KArgs& K, const Contig& C, int pa, int pb,
-                                            bool unk, int g) {
-  const DevParams& P = K.p;
-  if (C.ign[g]) return '~';
-  double s1 = C.S[(int64_t)pa * C.G + g], s2 = C.S[(int64_t)pb * C.G + g];
-  double mn = s2 < s1 ? s2 : s1;
-  if (mn >= P.k_amb && !unk) return '*';
-  if (s1 >= P.k2) return 'A';
-  if (s2 >= P.k2) return 'B';
-  return '!';
-}
-
-__device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
-                            const uint8_t* best, uint8_t* out) {
-  const DevParams& P = K.p;
-  const int G = C.G;
-  const bool unk = C.cl_id[pa] == K.unknown || C.cl_id[pb] == K.unknown;
-  OptEval e;
-  e.swapped = 0;
-  for (int g = 0; g < G; ++g) {  // "^[^A]*B" -> swap (orgscorer.py:537-540)
-    uint8_t c = two_char(K, C, pa, pb, unk, g);
-    if (c == 'A') break;
-    if (c == 'B') { e.swapped = 1; break; }
-  }
-  auto fin = [&](int g) -> uint8_t {
-    uint8_t c = two_char(K, C, pa, pb, unk, g);
-    if (e.swapped) c = (c == 'A') ? 'B' : (c == 'B' ? 'A' : c);
-    return c;
-  };
-  int state = 0, nA = 0, nB = 0;
-  bool dir_ok = true;
-  int64_t tot = 0, amb = 0;
-  e.same = 1;
-  for (int g = 0; g < G; ++g) {
-    uint8_t c = fin(g);
-    if (out) out[g] = c;
-    if (best && best[g] != c) e.same = 0;
-    const int len = C.loc_len[g];
-    if (c == 'A') { ++nA; tot += len; }
-    else if (c == 'B') { ++nB; tot += len; }
-    else if (c == '*') { tot += len; amb += len; }
-    if (c != '~') {  // "^A+B+A+$" on synteny without '~' (orgscorer.py:542)
-      if (state == 0) { if (c == 'A') state = 1; else dir_ok = false; }
-      else if (state == 1) { if (c == 'B') state = 2; else if (c != 'A') dir_ok = false; }
-      else if (state == 2) { if (c == 'A') state = 3; else if (c != 'B') dir_ok = false; }
-      else { if (c != 'A') dir_ok = false; }
-    }
-  }
-  e.dir = (dir_ok && state == 3) ? 1 : 0;
-  e.c1p = e.swapped ? pb : pa;
-  e.c2p = e.swapped ? pa : pb;
-  e.ok = 1;
-  // check_ambiguous_fraction (:693-702): total > 0 whenever crit >= k2 on >= 1 locus
-  if ((double)amb / (double)tot > P.amb_frac) e.ok = 0;
-  // check_clade_genes (:704-708)
-  if (P.clade_genes >= 0 && min(nA, nB) < P.clade_genes) e.ok = 0;
-  const int X = C.cl_id[e.c1p], Y = C.cl_id[e.c2p];
-  // check_clade_leaves (:710-715); recip = clade2 when the direction is known
-  if (P.clade_leaves >= 0) {
-    int64_t lc = e.dir ? K.leaves[Y] : min(K.leaves[X], K.leaves[Y]);
-    if (lc < P.clade_leaves) e.ok = 0;
-  }
-  // check_sister_penalty (:717-744): fail iff a checked locus has a present sister clade
-  // (other than the pair) scoring >= threshold there
-  if (P.sister_on && e.ok) {
-    const int px = K.parent[X], py = K.parent[Y];
-    for (int g = 0; g < G && e.ok; ++g) {
-      uint8_t c = fin(g);
-      int need;
-      if (c == 'B') need = px;
-      else if (c == 'A' && !e.dir) need = py;
-      else continue;
-      for (int q = 0; q < Pcount; ++q) {
-        const int s = C.cl_id[q];
-        if (K.sibp[s] != need) continue;
-        if (s == X || s == Y) continue;
-        if (C.S[(int64_t)q * G + g] >= P.sister_thr) { e.ok = 0; break; }
-      }
-    }
-  }
-  return e;
-}
-
-__device__ __forceinline__ double pair_rank(const Contig& C, int pa, int pb, int Gu) {
-  const double* ra = C.S + (int64_t)pa * C.G;
-  const double* rb = C.S + (int64_t)pb * C.G;
-  return np_sum(Gu, [&](int u) {
-           double a = ra[C.um[u]], b = rb[C.um[u]];
-           return a < b ? b : a;
-         }) / (double)Gu;
-}
-
-__device__ __forceinline__ double pair_crit(const Contig& C, int pa, int pb, int Gu) {
-  const double* ra = C.S + (int64_t)pa * C.G;
-  const double* rb = C.S + (int64_t)pb * C.G;
-  double m = 0.0;
-  for (int u = 0; u < Gu; ++u) {
-    double a = ra[C.um[u]], b = rb[C.um[u]];
-    double x = a < b ? b : a;
-    m = (u == 0 || x < m) ? x : m;
-  }
-  return m;
-}
 
 // --------------------------------------------------------------------------
 // the contig workgroup
@@ -710,7 +19,7 @@ __device__ __forceinline__ double pair_crit(const Contig& C, int pa, int pb, int
 template <int NT, bool BIG>
 __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abase, int64_t acap, Ctl& ctl) {
   constexpr int NW = NT / 64;
-  const int tid = threadIdx.x, w = wave_id();
+  const int tid = threadIdx.x;
   const DevParams& P = K.p;
   const int nsys = K.n_sys;
   Contig C;
@@ -760,7 +69,7 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
     // lane-group size for the parallel site means (0: serial path)
     const int gs = (n > kNpyBuf || nl > kGroupMax) ? 0 : nl <= 8 ? 8 : nl <= 16 ? 16 : nl <= 32 ? 32 : 64;
     C.loc_grp[g] = gs;
-    C.sched_off[g + 1] = kMaxDepth * gs;
+    C.sched_off[g + 1] = gs;
   }
   __syncthreads();
   if (tid == 0) {
@@ -777,7 +86,7 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
   STAMP(0);
   const int NL = ctl.cnt, NSCH = ctl.cnt2;
   C.leaves = ar.take<int4>(NL);
-  C.sched = ar.take<int8_t>(NSCH);
+  C.sched = ar.take<uint64_t>(NSCH);
 
   // ---- attach hits to loci: count (orgscorer.py:359-369, :559-564; utils.py:487-500) ---
   auto attaches = [&](int qlo, int qhi, int hs, int g) -> bool {
@@ -817,18 +126,18 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
     return;
   }
   // leaf tables and combine schedules
-  for (int i = tid; i < NSCH; i += NT) C.sched[i] = -1;
+  for (int i = tid; i < NSCH; i += NT) C.sched[i] = ~0ull;
   __syncthreads();
   for (int g = tid; g < G; g += NT) {
     int k = C.leaf_off[g];
     const int n = C.loc_len[g], gs = C.loc_grp[g];
-    int8_t* sch = gs ? C.sched + C.sched_off[g] : nullptr;
+    int8_t* sch = gs ? reinterpret_cast<int8_t*>(C.sched + C.sched_off[g]) : nullptr;
     for (int o = 0; o < n; o += kNpyBuf)
       k += gen_leaves(o, min(kNpyBuf, n - o), C.leaves + k, sch, gs);
     int steps = 0;
     for (int d = 0; d < kMaxDepth && sch; ++d)
       for (int i = 0; i < gs; ++i)
-        if (sch[d * gs + i] >= 0) steps = d + 1;
+        if (sch[i * 8 + d] >= 0) steps = d + 1;
     C.loc_steps[g] = steps;
   }
   // ---- attach: fill, with the python-slice site range (orgscorer.py:371-382) ---------
@@ -994,12 +303,8 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
       return;
     }
     for (int i = tid; i < Pn * G; i += NT) C.S[i] = 0.0;
-    for (int g = tid; g < G; g += NT) C.maxes[g] = 0;
-    if (tid == 0) ctl.root_present = 0;
     __syncthreads();
     STAMP(7);
-    for (int p = tid; p < Pn; p += NT)
-      if (C.cl_id[p] == K.root) ctl.root_present = 1;
     // ---- site-score means (orgscorer.py:399-406) -------------------------------------
     // segments grouped by their locus' lane-group class (8/16/32/64 lanes; 4 = serial)
     if (tid < 5) ctl.cls_cnt[tid] = 0;
@@ -1025,8 +330,14 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
       if (cls >= 0) C.sorder[ctl.cls_off[cls] + atomicAdd(&ctl.cls_cnt[cls], 1)] = s;
     }
     __syncthreads();
-    for (int q = 0; q < 4; ++q)
+    STAMP(22);
+    for (int q = 0; q < 4; ++q) {
       site_means_grouped<NW>(C, C.sorder + ctl.cls_off[q], ctl.cls_cnt[q], 8 << q);
+      STAT(27 + q, ctl.cls_cnt[q]);
+      STAMP_SYNC();
+      STAMP(23 + q);
+    }
+    STAT(31, ctl.cls_cnt[4]);
     for (int i = tid; i < ctl.cls_cnt[4]; i += NT) {
       const int s = C.sorder[ctl.cls_off[4] + i];
       const int kb = C.seg_start[s], ke = C.seg_start[s + 1];
@@ -1035,241 +346,11 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
     }
     __syncthreads();
     STAMP(8);
-    // ---- per-locus max over known clades, weak loci (:407-427) ----------------------
-    for (int i = tid; i < Pn * G; i += NT) {
-      if (C.cl_id[i / G] == K.unknown) continue;
-      const double v = C.S[i];
-      if (v > 0.0) atomicMax((unsigned long long*)&C.maxes[i % G], dbits(v));
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int Gu = 0;
-      for (int g = 0; g < G; ++g) {
-        const double m = __longlong_as_double((long long)C.maxes[g]);
-        int ig = 0;
-        if (P.weak == 0) ig = !(m >= P.kmin);
-        else if (P.weak == 2) C.S[(int64_t)ctl.p_unk * G + g] = 1.0 - m;
-        C.ign[g] = ig;
-        if (!ig) C.um[Gu++] = g;
-      }
-      ctl.Gu = Gu;
-      ctl.all_ignored = (Gu == 0);
-    }
-    __syncthreads();
-    STAMP(9);
-    const int Gu = ctl.Gu;
-    if (first) {
-      first = false;
-      if (ctl.all_ignored) return;   // skipped contig (orgscorer.py:959) -> unclassified
-    }
-    if (Gu == 0) {                   // np.min of an empty array upstream
-      if (tid == 0) ctl.status = WF_E_EMPTYMASK;
-      __syncthreads();
-      break;
-    }
-
-    // ================= explain_one (orgscorer.py:585-597) ============================
     {
-      // Contig.score (:447-461) for one clade: (min, np.mean) of its masked row
-      auto score_one = [&](int p, double& crit, double& rank) {
-        const double* row = C.S + (int64_t)p * G;
-        crit = row[C.um[0]];
-        for (int u = 1; u < Gu; ++u) { const double v = row[C.um[u]]; crit = v < crit ? v : crit; }
-        rank = np_sum(Gu, [&](int u) { return row[C.um[u]]; }) / (double)Gu;
-      };
-      double br = -__builtin_inf();
-      long long bk = -1;
-      for (int p = tid; p < Pn; p += NT) {
-        double crit, rank;
-        score_one(p, crit, rank);
-        if (crit >= P.k1 && better(rank, p, br, bk)) { br = rank; bk = p; }
-      }
-      block_argmax<NT>(br, bk, ctl);
-      STAMP(10);
-      if (bk >= 0) {
-        // meld_one (:621-631): options within --range of the best
-        const int bp = (int)bk;
-        if (tid == 0) ctl.cnt = 0;
-        __syncthreads();
-        if (P.dis1 == 1) {
-          for (int p = tid; p < Pn; p += NT) {
-            double crit, rank;
-            score_one(p, crit, rank);
-            if (crit >= P.k1 && (br - rank) <= P.range) {
-              const int slot = atomicAdd(&ctl.cnt, 1);
-              C.mem1[slot] = C.cl_id[p];
-            }
-          }
-        }
-        __syncthreads();
-        const int m = ctl.cnt;
-        if (P.dis1 == 1 && m == 0) {   // negative --range: get_lca() of nothing raises upstream
-          if (tid == 0) K.status[c] = WF_E_BADINPUT;
-          return;
-        }
-        const int lca = (P.dis1 == 1) ? block_lca(K, C.mem1, m, ctl) : C.cl_id[bp];
-        for (int i = tid; i < m; i += NT) K.meld[C.mbase + i] = C.mem1[i];
-        for (int g = tid; g < G; g += NT) {  // set_synteny_one (:495-509) of the best
-          const double s = C.S[(int64_t)bp * G + g];
-          K.syn[C.l0 + g] = C.ign[g] ? '~' : (s >= P.k1 ? 'A' : '!');
-        }
-        STAMP(11);
-        if (tid == 0) {
-          double crit, rank;
-          score_one(bp, crit, rank);
-          K.call[c] = WF_CALL_NO_LGT;
-          K.crit[c] = crit;
-          K.rank[c] = br;
-          K.c1[c] = lca;
-          K.c2[c] = -1;
-          K.nm1[c] = m;
-          K.iters[c] = (int16_t)iteration;
-          K.pair_evals[c] = pair_evals;
-        }
-        return;
-      }
+      const int dec = decide_level<NT>(K, C, ctl, c, Pn, iteration, first, pair_evals);
+      if (dec == kDecDone) return;
+      if (dec == kDecStop) break;
     }
-
-    // ================= explain_two (orgscorer.py:599-619) ============================
-    {
-      // potential clades: max over ALL loci >= k2 (:603-605)
-      int flag_local = 0;
-      const int per = (Pn + NT - 1) / NT;
-      const int pb0 = min(Pn, tid * per), pe0 = min(Pn, pb0 + per);
-      auto potential = [&](int p) -> bool {
-        const double* row = C.S + (int64_t)p * G;
-        double mx = row[0];
-        for (int g = 1; g < G; ++g) mx = row[g] > mx ? row[g] : mx;
-        return mx >= P.k2;
-      };
-      for (int p = pb0; p < pe0; ++p) flag_local += potential(p) ? 1 : 0;
-      int Pp;
-      int pos = block_scan<NT>(flag_local, &Pp, ctl);
-      for (int p = pb0; p < pe0; ++p)
-        if (potential(p)) C.pot[pos++] = p;
-      pair_evals += (int64_t)Pp * (Pp - 1) / 2;
-      const bool use_mask = Gu <= 64;
-      const uint64_t full = (Gu >= 64) ? ~0ull : ((1ull << Gu) - 1ull);
-      __syncthreads();
-      if (use_mask) {
-        for (int i = tid; i < Pp; i += NT) {
-          const double* row = C.S + (int64_t)C.pot[i] * G;
-          uint64_t m = 0;
-          for (int u = 0; u < Gu; ++u)
-            if (row[C.um[u]] >= P.k2) m |= 1ull << u;
-          C.mask[i] = m;
-        }
-      }
-      __syncthreads();
-      // pass 1: best pair over all pairs clade1 < clade2 (name order == index order)
-      double br = -__builtin_inf();
-      long long bk = -1;
-      auto candidate = [&](int i, int j) -> bool {
-        if (use_mask) return (C.mask[i] | C.mask[j]) == full;
-        return pair_crit(C, C.pot[i], C.pot[j], Gu) >= P.k2;
-      };
-      for (int i = w; i < Pp; i += NW) {
-        for (int j = i + 1 + lane_id(); j < Pp; j += 64) {
-          if (!candidate(i, j)) continue;
-          const double r = pair_rank(C, C.pot[i], C.pot[j], Gu);
-          const long long key = (long long)i * Pp + j;
-          if (better(r, key, br, bk)) { br = r; bk = key; }
-        }
-      }
-      block_argmax<NT>(br, bk, ctl);
-      bool have_ok = false;
-      if (bk >= 0) {
-        const int bi = (int)(bk / Pp), bj = (int)(bk % Pp);
-        for (int i = tid; i < (Pn + 31) / 32; i += NT) { C.bm1[i] = 0; C.bm2[i] = 0; }
-        if (tid == 0) {
-          OptEval e = eval_two(K, C, Pn, C.pot[bi], C.pot[bj], nullptr, C.best_syn);
-          ctl.best_ok = e.ok; ctl.best_dir = e.dir;
-          ctl.best_c1p = e.c1p; ctl.best_c2p = e.c2p;
-          ctl.best_crit = pair_crit(C, C.pot[bi], C.pot[bj], Gu);
-          ctl.n_in = 0; ctl.all_ok = 1; ctl.all_same = 1;
-        }
-        __syncthreads();
-        // pass 2: options within --range of the best get the LGT filters (:636-639)
-        for (int i = w; i < Pp; i += NW) {
-          for (int j = i + 1 + lane_id(); j < Pp; j += 64) {
-            if (!candidate(i, j)) continue;
-            const double r = pair_rank(C, C.pot[i], C.pot[j], Gu);
-            if (!((br - r) <= P.range)) continue;
-            OptEval e = eval_two(K, C, Pn, C.pot[i], C.pot[j], C.best_syn, nullptr);
-            atomicAdd(&ctl.n_in, 1);
-            if (!e.ok) atomicAnd(&ctl.all_ok, 0);
-            if (!e.same) atomicAnd(&ctl.all_same, 0);
-            atomicOr(&C.bm1[e.c1p >> 5], 1u << (e.c1p & 31));
-            atomicOr(&C.bm2[e.c2p >> 5], 1u << (e.c2p & 31));
-          }
-        }
-        __syncthreads();
-        // meld_two (:640-669)
-        if (tid == 0) {
-          int kind;   // 0 none, 1 best as is, 2 meld, 3 unchecked best, 4 upstream crash
-          if (ctl.n_in == 0) kind = (P.dis2 == 0) ? 3 : (P.dis2 == 1 ? 0 : 4);  // --range < 0
-          else if (ctl.n_in == 1 || P.dis2 == 0) kind = 1;
-          else if (P.dis2 == 1) kind = 0;
-          else kind = (ctl.all_ok && ctl.all_same) ? 2 : 0;
-          ctl.res_kind = kind;
-          ctl.cnt = 0;
-          ctl.cnt2 = 0;
-        }
-        __syncthreads();
-        const int kind = ctl.res_kind;
-        if (kind == 4) {
-          if (tid == 0) K.status[c] = WF_E_BADINPUT;
-          return;
-        }
-        int lca1 = -1, lca2v = -1, m1 = 0, m2 = 0;
-        if (kind == 2) {
-          for (int p = tid; p < Pn; p += NT) {
-            if (C.bm1[p >> 5] & (1u << (p & 31))) C.mem1[atomicAdd(&ctl.cnt, 1)] = C.cl_id[p];
-            if (C.bm2[p >> 5] & (1u << (p & 31))) C.mem2[atomicAdd(&ctl.cnt2, 1)] = C.cl_id[p];
-          }
-          __syncthreads();
-          m1 = ctl.cnt;
-          m2 = ctl.cnt2;
-          __syncthreads();
-          lca1 = block_lca(K, C.mem1, m1, ctl);
-          lca2v = block_lca(K, C.mem2, m2, ctl);
-          bool keep = true;
-          if (!P.allow_lca) {
-            const int nl = lca2(K, lca1, lca2v);
-            keep = !(nl == lca1 || nl == lca2v);
-          }
-          have_ok = keep;   // melded options are all OK
-        } else if (kind == 1) {
-          have_ok = ctl.best_ok != 0;
-        } else if (kind == 3) {
-          have_ok = true;
-        }
-        if (have_ok) {
-          for (int g = tid; g < G; g += NT) K.syn[C.l0 + g] = C.best_syn[g];
-          if (kind == 2) {
-            for (int i = tid; i < m1; i += NT) K.meld[C.mbase + i] = C.mem1[i];
-            for (int i = tid; i < m2; i += NT) K.meld[C.mbase + m1 + i] = C.mem2[i];
-          }
-          if (tid == 0) {
-            K.call[c] = WF_CALL_LGT;
-            K.crit[c] = ctl.best_crit;
-            K.rank[c] = br;
-            K.dir[c] = (int8_t)ctl.best_dir;
-            K.c1[c] = (kind == 2) ? lca1 : C.cl_id[ctl.best_c1p];
-            K.c2[c] = (kind == 2) ? lca2v : C.cl_id[ctl.best_c2p];
-            K.nm1[c] = (kind == 2) ? m1 : 0;
-            K.nm2[c] = (kind == 2) ? m2 : 0;
-            K.iters[c] = (int16_t)iteration;
-            K.pair_evals[c] = pair_evals;
-          }
-          return;
-        }
-      }
-    }
-
-    STAMP(12);
-    // ================= roll-up (orgscorer.py:571-581) ================================
-    if (Pn == 0 || ctl.root_present) break;
     for (int a = tid; a < A; a += NT) C.acl[a] = K.parent[C.acl[a]];
     ++iteration;
     if (iteration > kMaxIter) {

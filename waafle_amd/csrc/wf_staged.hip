@@ -1,0 +1,685 @@
+// Staged form of the contig-scoring path (gfx950 / MI355X).  Instead of one workgroup
+// carrying a contig through every phase (wf_kernels.hip), each phase is a flat kernel over
+// all contigs' items, so every phase fills the chip at its own natural granularity:
+//
+//   hits        k_hit_contig, k_att_count     thread per hit: attached loci (orgscorer.py:359-369)
+//               device exclusive scan          -> attachment offsets (contiguous per contig)
+//               k_att_fill                     thread per hit: site ranges (:371-382)
+//   loci        k_annot                        thread per locus: annotation winners (:383-392)
+//   per level   k_keys_*                       (contig rank, clade, locus) keys
+//               device radix sort              -> segments = equal keys (:394-406)
+//               k_seg_flags + scan + k_segs    segment boundaries
+//               k_seg_mean                     thread per segment: exact numpy mean
+//               k_decide / k_decide_big        workgroup per contig: maxes, weak loci,
+//                                              explain_one/two, melds, LGT filters
+//                                              (decide_level, shared with the fused form);
+//                                              raised contigs re-keyed to parents (:431-445)
+//
+// The numpy pairwise-sum leaf tables depend only on the length of a buffer (<= 8192), so
+// they are generated once per context into a device table (k_lut_*), with the same
+// generator the fused kernels use.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#undef WF_STAMPS
+#include "wf_device.h"
+
+namespace wf {
+
+namespace {
+
+__device__ __forceinline__ int upper_index(const int64_t* off, int n, int64_t x) {
+  // largest c in [0, n) with off[c] <= x  (off is non-decreasing, off[0] = 0)
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= x) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int lower_bound_i32(const int32_t* a, int n, int x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ bool attaches(const DevParams& P, int qlo, int qhi, int hs, int l1,
+                                         int len, int lst) {
+  if (P.stranded && hs != lst) return false;
+  const int l2 = l1 + len - 1;
+  if (l1 > qhi || qlo > l2) return 0.0 >= P.min_overlap;   // calc_overlap -> int 0
+  const int ov = min(qhi, l2) - max(qlo, l1) + 1;
+  const int den = min(qhi - qlo + 1, l2 - l1 + 1);
+  return (double)ov / (double)den >= P.min_overlap;
+}
+
+// ---- numpy leaf tables by buffer length ------------------------------------------------
+__global__ void k_lut_count(int32_t* cnt) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n > kNpyBuf) return;
+  cnt[n] = n == 0 ? 0 : gen_leaves(0, n, nullptr);
+}
+__global__ void k_lut_fill(const int32_t* off, int4* lut) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < 1 || n > kNpyBuf) return;
+  gen_leaves(0, n, lut + off[n]);
+}
+
+// ---- contigs, hits, attachments ----------------------------------------------------------
+__global__ void k_init(const KArgs* __restrict__ kp) {
+  const KArgs& K = *kp;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= K.n_contigs) return;
+  K.call[c] = WF_CALL_UNCLASSIFIED;
+  K.crit[c] = 0.0; K.rank[c] = 0.0; K.c1[c] = -1; K.c2[c] = -1; K.dir[c] = 0;
+  K.iters[c] = 0; K.nm1[c] = 0; K.nm2[c] = 0; K.pair_evals[c] = 0; K.status[c] = 0;
+  K.need[c] = 0;
+}
+
+__global__ void k_hit_contig(const SArgs* __restrict__ sp, int32_t* hit_contig) {
+  const SArgs& S = *sp;
+  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= S.n_hits_i) return;
+  hit_contig[h] = upper_index(S.k.hit_off, S.k.n_contigs, h);
+}
+
+__global__ void k_att_count(const SArgs* __restrict__ sp, int64_t* cnt) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h > S.n_hits_i) return;
+  if (h == S.n_hits_i) { cnt[h] = 0; return; }
+  int n = 0;
+  if (K.scov[h] >= K.p.min_scov) {
+    const int c = S.hit_contig[h];
+    const int qlo = K.qlo[h], qhi = K.qhi[h], hs = K.hstrand[h];
+    for (int64_t l = K.loc_off[c]; l < K.loc_off[c + 1]; ++l) {
+      const int s = K.lstart[l], e = K.lend[l];
+      const int lo = min(s, e), len = max(s, e) - lo + 1;
+      n += attaches(K.p, qlo, qhi, hs, lo, len, K.lstrand[l]) ? 1 : 0;
+    }
+  }
+  cnt[h] = n;
+}
+
+__global__ void k_att_fill(const SArgs* __restrict__ sp) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= S.n_hits_i) return;
+  if (!(K.scov[h] >= K.p.min_scov)) return;
+  const int c = S.hit_contig[h];
+  const int qlo = K.qlo[h], qhi = K.qhi[h], hs = K.hstrand[h];
+  int clade = K.taxon[h];
+  for (int j = 0; j < K.p.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
+  int64_t o = S.att_off[h];
+  const int64_t l0 = K.loc_off[c];
+  for (int64_t l = l0; l < K.loc_off[c + 1]; ++l) {
+    const int s = K.lstart[l], e = K.lend[l];
+    const int lo = min(s, e), len = max(s, e) - lo + 1;
+    if (!attaches(K.p, qlo, qhi, hs, lo, len, K.lstrand[l])) continue;
+    const int h1 = max(0, qlo - lo);
+    const int h2 = min(len - 1, qhi - lo);
+    const int start = min(h1, len);
+    int stop = h2 + 1;                         // site[h1:h2+1], python slice rules
+    if (stop < 0) { stop += len; if (stop < 0) stop = 0; }
+    S.att_lo[o] = start;
+    S.att_hi[o] = stop;                        // empty when stop <= start
+    S.att_loc[o] = (int)(l - l0);
+    S.att_clade[o] = clade;
+    S.att_hit[o] = (int)h;
+    S.att_sc[o] = K.score[h];
+    ++o;
+  }
+}
+
+// Annotation transfer (orgscorer.py:383-392): per (locus, system) the last hit in file
+// order whose score equals the running maximum >= threshold.
+__global__ void k_annot(const SArgs* __restrict__ sp, int64_t n_loci) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= n_loci || K.n_sys == 0) return;
+  const int c = upper_index(K.loc_off, K.n_contigs, l);
+  const int g = (int)(l - K.loc_off[c]);
+  const int64_t a0 = S.att_off[K.hit_off[c]], a1 = S.att_off[K.hit_off[c + 1]];
+  for (int b = 0; b < K.n_sys; ++b) {
+    double best = -1.0;
+    int idx = -1;
+    for (int64_t a = a0; a < a1; ++a) {
+      if (S.att_loc[a] != g) continue;
+      const double s = S.att_sc[a];
+      if (!((K.sysmask[S.att_hit[a]] >> b) & 1u) || !(s >= K.p.annot_ref)) continue;
+      if (s > best || (s == best && S.att_hit[a] > idx)) { best = s; idx = S.att_hit[a]; }
+    }
+    K.annot[l * K.n_sys + b] = idx;
+  }
+}
+
+// ---- one roll-up level -------------------------------------------------------------------
+__device__ __forceinline__ uint64_t make_key(const SArgs& S, int crank, int a) {
+  return ((uint64_t)crank << (S.key_tb + S.key_lb)) | ((uint64_t)(uint32_t)S.att_clade[a] << S.key_lb) |
+         (uint64_t)S.att_loc[a];
+}
+
+__global__ void k_keys_all(const SArgs* __restrict__ sp, int64_t n_att, uint64_t* keys, int32_t* vals) {
+  const SArgs& S = *sp;
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n_att) return;
+  keys[a] = make_key(S, S.hit_contig[S.att_hit[a]], (int)a);
+  vals[a] = (int)a;
+}
+
+__global__ void k_keys_active(const SArgs* __restrict__ sp, int n_act, uint64_t* keys, int32_t* vals) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const int c = S.act[cr];
+    const int64_t a0 = S.att_off[K.hit_off[c]], a1 = S.att_off[K.hit_off[c + 1]];
+    const int64_t base = S.act_base[cr];
+    for (int64_t i = threadIdx.x; i < a1 - a0; i += blockDim.x) {
+      keys[base + i] = make_key(S, cr, (int)(a0 + i));
+      vals[base + i] = (int)(a0 + i);
+    }
+  }
+}
+
+__global__ void k_seg_flags(const uint64_t* keys, int64_t n, int32_t* flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+}
+
+__global__ void k_segs(const SArgs* __restrict__ sp, int64_t n) {
+  const SArgs& S = *sp;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (S.flags[i]) {
+    const int s = S.seg_id[i] - 1;
+    S.seg_start[s] = (int)i;
+    S.seg_crank[s] = (int)(S.keys[i] >> (S.key_tb + S.key_lb));
+  }
+  if (i == n - 1) S.seg_start[S.seg_id[i]] = (int)n;
+}
+
+// Exact np.mean of one (clade, locus) site array from its attachments and the leaf table
+// of each 8192-element numpy buffer (same arithmetic as the fused serial path).
+__global__ void k_seg_mean(const SArgs* __restrict__ sp, int64_t n) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !S.flags[i]) return;
+  const int s = S.seg_id[i] - 1;
+  const int kb = (int)i, ke = S.seg_start[s + 1];
+  const uint64_t key = S.keys[i];
+  const int crank = (int)(key >> (S.key_tb + S.key_lb));
+  const int g = (int)(key & ((1ull << S.key_lb) - 1));
+  const int c = S.act ? S.act[crank] : crank;
+  const int64_t l = K.loc_off[c] + g;
+  const int ls = K.lstart[l], le = K.lend[l];
+  const int len = max(ls, le) - min(ls, le) + 1;
+  const ValSrc src{S.vals, S.att_lo, S.att_hi, S.att_sc};
+  SegAttT<ValSrc> at;
+  at.load(src, kb, ke);
+  double total = 0.0;
+  for (int o = 0; o < len; o += kNpyBuf) {
+    const int m = min(kNpyBuf, len - o);
+    const int4* lv = S.lut + S.lut_off[m];
+    const int nl = S.lut_off[m + 1] - S.lut_off[m];
+    SumStack stk;
+    for (int j = 0; j < nl; ++j) {
+      const int4 e = lv[j];
+      stk.push(at.leaf(src, o + e.x, e.y));
+      for (int q = 0; q < e.z; ++q) stk.add_top();
+    }
+    total += stk.s0;
+  }
+  S.seg_mean[s] = total / (double)len;
+}
+
+// Decision workgroup for one contig at one level.  Builds the gene-score matrix of the
+// level (rows = clades in id order, the virtual "Unknown" row of --weak-loci
+// assign-unknown included) from the contig's segments, then runs decide_level.
+// Returns false when the arena is too small (caller hands the contig to the HBM tier).
+template <int NT>
+__device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* abase, int64_t acap,
+                              Ctl& ctl, int64_t n_keys) {
+  const KArgs& K = S.k;
+  const DevParams& P = K.p;
+  const int tid = threadIdx.x;
+  const int64_t h0 = K.hit_off[c];
+  const int H = (int)(K.hit_off[c + 1] - h0);
+  Contig C;
+  C.l0 = K.loc_off[c];
+  C.G = (int)(K.loc_off[c + 1] - C.l0);
+  C.h0 = h0;
+  C.H = H;
+  C.mbase = 2 * h0 + 2 * (int64_t)c;
+  const int G = C.G;
+  if (H == 0 || G == 0) return true;            // never evaluated (orgscorer.py:959)
+  if (tid == 0) {
+    const int nseg = n_keys > 0 ? S.seg_id[n_keys - 1] : 0;
+    ctl.cnt = lower_bound_i32(S.seg_crank, nseg, cr);
+    ctl.cnt2 = lower_bound_i32(S.seg_crank, nseg, cr + 1);
+    ctl.status = 0;
+    ctl.p_unk = -1;
+  }
+  __syncthreads();
+  const int so = ctl.cnt, se = ctl.cnt2, ns = se - so;
+  const int Pmax = ns + 1;
+  Arena ar{abase, acap, 0};
+  C.cl_id = ar.take<int>(Pmax);
+  C.S = ar.take<double>((int64_t)Pmax * G);
+  C.maxes = ar.take<uint64_t>(G);
+  C.ign = ar.take<int>(G);
+  C.um = ar.take<int>(G);
+  C.pot = ar.take<int>(Pmax);
+  C.mask = ar.take<uint64_t>(Pmax);
+  C.mem1 = ar.take<int>(Pmax);
+  C.mem2 = ar.take<int>(Pmax);
+  C.bm1 = ar.take<unsigned>((Pmax + 31) / 32);
+  C.bm2 = ar.take<unsigned>((Pmax + 31) / 32);
+  C.best_syn = ar.take<uint8_t>(G);
+  C.loc_len = ar.take<int>(G);                  // ambiguous fraction weights (orgscorer.py:693-702)
+  int* seg_ci = ar.take<int>(ns + 1);
+  if (!ar.fits()) {
+    if (tid == 0) K.need[c] = ar.used + 4096;
+    __syncthreads();
+    return false;
+  }
+  for (int g = tid; g < G; g += NT) {
+    const int ls = K.lstart[C.l0 + g], le = K.lend[C.l0 + g];
+    C.loc_len[g] = max(ls, le) - min(ls, le) + 1;
+  }
+  const uint64_t cmask = (1ull << S.key_tb) - 1;
+  auto clade_of = [&](int s) { return (int)((S.keys[S.seg_start[s]] >> S.key_lb) & cmask); };
+  // clade list = distinct clades of the segments (sorted by id = name order)
+  const int per = (ns + NT - 1) / NT;
+  const int b = min(ns, tid * per), e = min(ns, b + per);
+  int nc = 0;
+  for (int t = b; t < e; ++t)
+    if (t == 0 || clade_of(so + t) != clade_of(so + t - 1)) ++nc;
+  int Pn;
+  int ci = block_scan<NT>(nc, &Pn, ctl) - 1;
+  for (int t = b; t < e; ++t) {
+    const int cl = clade_of(so + t);
+    if (t == 0 || cl != clade_of(so + t - 1)) {
+      ++ci;
+      C.cl_id[ci] = cl;
+      if (cl == K.unknown) ctl.p_unk = ci;
+    }
+    seg_ci[t] = ci;
+  }
+  __syncthreads();
+  if (P.weak == 2 && ctl.p_unk < 0) {            // virtual "Unknown" row (orgscorer.py:416-418)
+    if (tid == 0) {
+      int pos = 0;
+      while (pos < Pn && C.cl_id[pos] < K.unknown) ++pos;
+      for (int q = Pn; q > pos; --q) C.cl_id[q] = C.cl_id[q - 1];
+      C.cl_id[pos] = K.unknown;
+      ctl.p_unk = pos;
+    }
+    __syncthreads();
+    const int pos = ctl.p_unk;
+    for (int t = tid; t < ns; t += NT)
+      if (seg_ci[t] >= pos) seg_ci[t] += 1;
+    ++Pn;
+  }
+  for (int i = tid; i < Pn * G; i += NT) C.S[i] = 0.0;
+  __syncthreads();
+  for (int t = tid; t < ns; t += NT) {
+    const int g = (int)(S.keys[S.seg_start[so + t]] & ((1ull << S.key_lb) - 1));
+    C.S[(int64_t)seg_ci[t] * G + g] = S.seg_mean[so + t];
+  }
+  __syncthreads();
+  const int iteration = level + 1;
+  bool first = level == 0;
+  int64_t pair_evals = level == 0 ? 0 : K.pair_evals[c];
+  const int dec = decide_level<NT>(K, C, ctl, c, Pn, iteration, first, pair_evals);
+  if (dec == kDecDone) return true;
+  if (dec == kDecRaise && iteration + 1 <= kMaxIter) {
+    // roll up (orgscorer.py:431-445): this contig's attachments move to the parent clade
+    const int64_t a0 = S.att_off[h0], a1 = S.att_off[h0 + H];
+    if (tid == 0) {
+      const int slot = (int)atomicAdd(&S.counters[0], 1ull);
+      S.act_next[slot] = c;
+      S.act_base_next[slot] = (int64_t)atomicAdd(&S.counters[1], (unsigned long long)(a1 - a0));
+      K.pair_evals[c] = pair_evals;
+    }
+    for (int64_t a = a0 + tid; a < a1; a += NT) S.att_clade[a] = K.parent[S.att_clade[a]];
+    return true;
+  }
+  if (tid == 0) {                                // unclassified after evaluation
+    const int it = dec == kDecRaise ? iteration + 1 : iteration;
+    K.iters[c] = (int16_t)min(it, 32767);
+    K.pair_evals[c] = pair_evals;
+    K.status[c] = dec == kDecRaise ? WF_E_RUNAWAY : ctl.status;
+  }
+  return true;
+}
+
+constexpr int kDecNT = 128;
+
+__global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs* __restrict__ sp, int n_act,
+                                                       int level, int64_t n_keys) {
+  const SArgs& S = *sp;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ Ctl ctl;
+  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const int c = S.act ? S.act[cr] : cr;
+    const bool ok = decide_contig<kDecNT>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
+    if (!ok && threadIdx.x == 0) {
+      const int slot = (int)atomicAdd(&S.counters[2], 1ull);
+      S.big_list[2 * slot] = cr;
+      S.big_list[2 * slot + 1] = c;
+      atomicMax(&S.counters[3], (unsigned long long)S.k.need[c]);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs* __restrict__ sp, int level,
+                                                          int64_t n_keys, int count) {
+  const SArgs& S = *sp;
+  __shared__ Ctl ctl;
+  char* base = S.k.big_ws + (int64_t)blockIdx.x * S.k.slot_bytes;
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int cr = S.big_list[2 * i], c = S.big_list[2 * i + 1];
+    const bool ok = decide_contig<kBlock>(S, c, cr, level, base, S.k.slot_bytes, ctl, n_keys);
+    if (!ok && threadIdx.x == 0) S.k.status[c] = WF_E_NOMEM;
+    __syncthreads();
+  }
+}
+
+int bits_for(int64_t v) {   // bits to hold values 0..v
+  int b = 1;
+  while (b < 62 && (int64_t(1) << b) <= v) ++b;
+  return b;
+}
+
+hipStream_t g_sync_stream = nullptr;   // stream drained before any buffer is reallocated
+
+struct Buf {
+  void* p = nullptr;
+  size_t n = 0;
+  ~Buf() { if (p) (void)hipFree(p); }
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n) return hipSuccess;
+    if (p) {
+      // queued kernels may still use the old allocation: drain the stream first
+      if (g_sync_stream) {
+        hipError_t e = hipStreamSynchronize(g_sync_stream);
+        if (e != hipSuccess) return e;
+      }
+      (void)hipFree(p);
+      p = nullptr;
+      n = 0;
+    }
+    size_t want = std::max<size_t>(bytes + bytes / 4, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) n = want;
+    return e;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace
+
+constexpr int kRing = 64;
+
+struct StagedState {
+  int device = 0;
+  int cus = 256;
+  Buf lut_off, lut, sargs, kargs_big, cnt, att_off, hit_contig, counters, pinned_dummy;
+  Buf att_lo, att_hi, att_loc, att_clade, att_hit, att_sc;
+  Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
+  Buf act0, act1, base0, base1, big_list, big_ws, tmp;
+  bool lut_ready = false;
+  int64_t dec_lds = 48 * 1024;
+  unsigned long long* host_counters = nullptr;   // pinned
+  SArgs* ring = nullptr;                          // pinned argument snapshots
+  ~StagedState() {
+    if (host_counters) (void)hipHostFree(host_counters);
+    if (ring) (void)hipHostFree(ring);
+  }
+};
+
+StagedState* staged_create(int device) {
+  StagedState* st = new StagedState();
+  st->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) st->cus = prop.multiProcessorCount;
+  if (hipHostMalloc(reinterpret_cast<void**>(&st->host_counters), 8 * sizeof(unsigned long long)) != hipSuccess)
+    st->host_counters = nullptr;
+  return st;
+}
+
+void staged_destroy(StagedState* st) { delete st; }
+
+void staged_set_lds(StagedState* st, int64_t bytes) { st->dec_lds = bytes; }
+
+#define ST_TRY(x)                                                                        \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess) { *err = std::string(#x) + ": " + hipGetErrorString(e_); return -2; } \
+  } while (0)
+
+static int build_lut(StagedState* st, hipStream_t s, std::string* err) {
+  if (st->lut_ready) return 0;
+  ST_TRY(st->lut_off.ensure((kNpyBuf + 2) * sizeof(int32_t)));
+  Buf counts;
+  ST_TRY(counts.ensure((kNpyBuf + 2) * sizeof(int32_t)));
+  hipLaunchKernelGGL(k_lut_count, dim3((kNpyBuf + 256) / 256), dim3(256), 0, s, counts.as<int32_t>());
+  ST_TRY(hipGetLastError());
+  std::vector<int32_t> h(kNpyBuf + 2, 0);
+  ST_TRY(hipMemcpyAsync(h.data(), counts.p, (kNpyBuf + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipStreamSynchronize(s));
+  std::vector<int32_t> off(kNpyBuf + 2, 0);
+  for (int n = 0; n <= kNpyBuf; ++n) off[n + 1] = off[n] + h[n];
+  ST_TRY(st->lut.ensure((size_t)off[kNpyBuf + 1] * sizeof(int4)));
+  ST_TRY(hipMemcpyAsync(st->lut_off.p, off.data(), (kNpyBuf + 2) * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  hipLaunchKernelGGL(k_lut_fill, dim3((kNpyBuf + 256) / 256), dim3(256), 0, s, st->lut_off.as<int32_t>(),
+                     st->lut.as<int4>());
+  ST_TRY(hipGetLastError());
+  ST_TRY(hipStreamSynchronize(s));
+  st->lut_ready = true;
+  return 0;
+}
+
+static inline unsigned grid_for(int64_t n, int block = 256) {
+  return (unsigned)std::max<int64_t>(1, (n + block - 1) / block);
+}
+
+// Runs the whole path for one batch on stream `s` (synchronising on it between levels).
+// `k` carries device pointers for batch, taxonomy, params and results.
+int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipStream_t s,
+                 std::string* err) {
+  const int N = k.n_contigs;
+  if (N <= 0) return 0;
+  g_sync_stream = s;
+  int rc = build_lut(st, s, err);
+  if (rc) return rc;
+  // host copy of the offsets we need: total hits / loci
+  int64_t tail[2];
+  ST_TRY(hipMemcpyAsync(&tail[0], k.hit_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipMemcpyAsync(&tail[1], k.loc_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipStreamSynchronize(s));
+  const int64_t NH = tail[0], NL = tail[1];
+  if (NH >= (int64_t(1) << 31) - 1) { *err = "too many hits for one batch (split it)"; return -1; }
+
+  SArgs sa{};
+  sa.k = k;
+  sa.n_hits_i = (int)NH;
+  sa.key_lb = bits_for(std::max(max_loci, 1));
+  sa.key_tb = bits_for(std::max(n_tax, 1));
+  sa.lut_off = st->lut_off.as<int32_t>();
+  sa.lut = st->lut.as<int4>();
+  sa.dec_lds_bytes = st->dec_lds;
+  // argument snapshots: every upload gets its own pinned host slot and device slot, so no
+  // copy is overwritten before the stream consumed it (the previous call ended synchronised)
+  ST_TRY(st->sargs.ensure(kRing * sizeof(SArgs)));
+  if (!st->ring) {
+    ST_TRY(hipHostMalloc(reinterpret_cast<void**>(&st->ring), kRing * sizeof(SArgs)));
+  }
+  int ring_i = 0;
+  SArgs* dsa = st->sargs.as<SArgs>();
+  auto upload = [&]() -> hipError_t {
+    if (ring_i == kRing) {                 // wrap: wait until every snapshot was consumed
+      hipError_t e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return e;
+      ring_i = 0;
+    }
+    st->ring[ring_i] = sa;
+    dsa = st->sargs.as<SArgs>() + ring_i;
+    return hipMemcpyAsync(dsa, st->ring + ring_i++, sizeof(SArgs), hipMemcpyHostToDevice, s);
+  };
+  ST_TRY(st->counters.ensure(8 * sizeof(unsigned long long)));
+  sa.counters = st->counters.as<unsigned long long>();
+
+  // contigs, hits -> attachments
+  ST_TRY(st->hit_contig.ensure((size_t)std::max<int64_t>(NH, 1) * sizeof(int32_t)));
+  ST_TRY(st->cnt.ensure((size_t)(NH + 1) * sizeof(int64_t)));
+  ST_TRY(st->att_off.ensure((size_t)(NH + 1) * sizeof(int64_t)));
+  sa.hit_contig = st->hit_contig.as<int32_t>();
+  sa.att_off = st->att_off.as<int64_t>();
+  ST_TRY(upload());
+  hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, &dsa->k);
+  hipLaunchKernelGGL(k_hit_contig, dim3(grid_for(NH)), dim3(256), 0, s, dsa, st->hit_contig.as<int32_t>());
+  hipLaunchKernelGGL(k_att_count, dim3(grid_for(NH + 1)), dim3(256), 0, s, dsa, st->cnt.as<int64_t>());
+  ST_TRY(hipGetLastError());
+  size_t tmp_bytes = 0;
+  ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, st->cnt.as<int64_t>(),
+                                          st->att_off.as<int64_t>(), (int)(NH + 1), s));
+  ST_TRY(st->tmp.ensure(tmp_bytes));
+  tmp_bytes = st->tmp.n;
+  ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, tmp_bytes, st->cnt.as<int64_t>(),
+                                          st->att_off.as<int64_t>(), (int)(NH + 1), s));
+  int64_t A = 0;
+  ST_TRY(hipMemcpyAsync(&A, st->att_off.as<int64_t>() + NH, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipStreamSynchronize(s));
+  if (A >= (int64_t(1) << 31) - 1) { *err = "too many hit-locus attachments for one batch"; return -1; }
+  const size_t A1 = (size_t)std::max<int64_t>(A, 1);
+  ST_TRY(st->att_lo.ensure(A1 * 4)); ST_TRY(st->att_hi.ensure(A1 * 4));
+  ST_TRY(st->att_loc.ensure(A1 * 4)); ST_TRY(st->att_clade.ensure(A1 * 4));
+  ST_TRY(st->att_hit.ensure(A1 * 4)); ST_TRY(st->att_sc.ensure(A1 * 8));
+  ST_TRY(st->keys0.ensure(A1 * 8)); ST_TRY(st->keys1.ensure(A1 * 8));
+  ST_TRY(st->vals0.ensure(A1 * 4)); ST_TRY(st->vals1.ensure(A1 * 4));
+  ST_TRY(st->flags.ensure(A1 * 4)); ST_TRY(st->seg_id.ensure(A1 * 4));
+  ST_TRY(st->seg_start.ensure((A1 + 1) * 4)); ST_TRY(st->seg_crank.ensure(A1 * 4));
+  ST_TRY(st->seg_mean.ensure(A1 * 8));
+  ST_TRY(st->act0.ensure((size_t)N * 4)); ST_TRY(st->act1.ensure((size_t)N * 4));
+  ST_TRY(st->base0.ensure((size_t)N * 8)); ST_TRY(st->base1.ensure((size_t)N * 8));
+  ST_TRY(st->big_list.ensure((size_t)N * 8));
+  sa.att_lo = st->att_lo.as<int32_t>(); sa.att_hi = st->att_hi.as<int32_t>();
+  sa.att_loc = st->att_loc.as<int32_t>(); sa.att_clade = st->att_clade.as<int32_t>();
+  sa.att_hit = st->att_hit.as<int32_t>(); sa.att_sc = st->att_sc.as<double>();
+  sa.flags = st->flags.as<int32_t>(); sa.seg_id = st->seg_id.as<int32_t>();
+  sa.seg_start = st->seg_start.as<int32_t>(); sa.seg_crank = st->seg_crank.as<int32_t>();
+  sa.seg_mean = st->seg_mean.as<double>();
+  sa.big_list = st->big_list.as<int32_t>();
+  {
+    // temp storage for every primitive of this call, sized once (no reallocation between
+    // enqueued kernels)
+    size_t t1 = 0, t2 = 0;
+    hipcub::DoubleBuffer<uint64_t> kb0(st->keys0.as<uint64_t>(), st->keys1.as<uint64_t>());
+    hipcub::DoubleBuffer<int32_t> vb0(st->vals0.as<int32_t>(), st->vals1.as<int32_t>());
+    ST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kb0, vb0, (int)A1, 0, 64, s));
+    ST_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t2, st->flags.as<int32_t>(),
+                                            st->seg_id.as<int32_t>(), (int)A1, s));
+    ST_TRY(st->tmp.ensure(std::max(t1, t2)));
+  }
+  ST_TRY(upload());
+  hipLaunchKernelGGL(k_att_fill, dim3(grid_for(NH)), dim3(256), 0, s, dsa);
+  if (k.n_sys > 0 && NL > 0)
+    hipLaunchKernelGGL(k_annot, dim3(grid_for(NL)), dim3(256), 0, s, dsa, NL);
+  else if (NL > 0)
+    ;  // no annotation systems: nothing to write
+  ST_TRY(hipGetLastError());
+
+  // roll-up levels
+  Buf* act[2] = {&st->act0, &st->act1};
+  Buf* base[2] = {&st->base0, &st->base1};
+  int n_act = N;
+  int64_t n_keys = A;
+  for (int level = 0; n_act > 0; ++level) {
+    const int cur = level & 1;
+    sa.act = level == 0 ? nullptr : act[cur]->as<int32_t>();
+    sa.act_base = level == 0 ? nullptr : base[cur]->as<int64_t>();
+    sa.act_next = act[cur ^ 1]->as<int32_t>();
+    sa.act_base_next = base[cur ^ 1]->as<int64_t>();
+    const int cb = bits_for(n_act);
+    const int end_bit = cb + sa.key_tb + sa.key_lb;
+    if (end_bit > 64) { *err = "sort key wider than 64 bits"; return -1; }
+    hipcub::DoubleBuffer<uint64_t> kbuf(st->keys0.as<uint64_t>(), st->keys1.as<uint64_t>());
+    hipcub::DoubleBuffer<int32_t> vbuf(st->vals0.as<int32_t>(), st->vals1.as<int32_t>());
+    sa.keys = nullptr;
+    sa.vals = nullptr;
+    ST_TRY(upload());
+    if (n_keys > 0) {
+      if (level == 0)
+        hipLaunchKernelGGL(k_keys_all, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys,
+                           kbuf.Current(), vbuf.Current());
+      else
+        hipLaunchKernelGGL(k_keys_active, dim3(std::min(n_act, st->cus * 8)), dim3(256), 0, s, dsa,
+                           n_act, kbuf.Current(), vbuf.Current());
+      ST_TRY(hipGetLastError());
+      size_t need = 0;
+      ST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, need, kbuf, vbuf, (int)n_keys, 0, end_bit, s));
+      ST_TRY(st->tmp.ensure(need));
+      need = st->tmp.n;
+      ST_TRY(hipcub::DeviceRadixSort::SortPairs(st->tmp.p, need, kbuf, vbuf, (int)n_keys, 0, end_bit, s));
+    }
+    sa.keys = kbuf.Current();
+    sa.vals = vbuf.Current();
+    ST_TRY(upload());
+    ST_TRY(hipMemsetAsync(st->counters.p, 0, 8 * sizeof(unsigned long long), s));
+    if (n_keys > 0) {
+      hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa.keys, n_keys, sa.flags);
+      size_t need = 0;
+      ST_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, need, sa.flags, sa.seg_id, (int)n_keys, s));
+      ST_TRY(st->tmp.ensure(need));
+      need = st->tmp.n;
+      ST_TRY(hipcub::DeviceScan::InclusiveSum(st->tmp.p, need, sa.flags, sa.seg_id, (int)n_keys, s));
+      hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
+      hipLaunchKernelGGL(k_seg_mean, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
+      ST_TRY(hipGetLastError());
+    }
+    if (st->dec_lds > 64 * 1024) {
+      static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide),
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   160 * 1024 - 1024);
+      ST_TRY(attr);
+    }
+    const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
+    hipLaunchKernelGGL(k_decide, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
+    ST_TRY(hipGetLastError());
+    ST_TRY(hipMemcpyAsync(st->host_counters, st->counters.p, 4 * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, s));
+    ST_TRY(hipStreamSynchronize(s));
+    const int n_big = (int)st->host_counters[2];
+    if (n_big > 0) {
+      const int64_t slot = ((int64_t)st->host_counters[3] + 255) & ~int64_t(255);
+      const int slots = std::min(n_big, st->cus * 2);
+      ST_TRY(st->big_ws.ensure((size_t)slot * slots));
+      sa.k.big_ws = st->big_ws.as<char>();
+      sa.k.slot_bytes = slot;
+      ST_TRY(upload());
+      hipLaunchKernelGGL(k_decide_big, dim3(slots), dim3(kBlock), 0, s, dsa, level, n_keys, n_big);
+      ST_TRY(hipGetLastError());
+      ST_TRY(hipMemcpyAsync(st->host_counters, st->counters.p, 4 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, s));
+      ST_TRY(hipStreamSynchronize(s));
+    }
+    n_act = (int)st->host_counters[0];
+    n_keys = (int64_t)st->host_counters[1];
+  }
+  return 0;
+}
+
+}  // namespace wf

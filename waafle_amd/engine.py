@@ -19,6 +19,7 @@ DIS_ONE = {"report-best": 0, "meld": 1}
 DIS_TWO = {"report-best": 0, "jump": 1, "meld": 2}
 LEVEL = {"off": 0, "lenient": 1, "strict": 2}
 WEAK = {"ignore": 0, "penalize": 1, "assign-unknown": 2}
+MODES = {"staged": L.MODE_STAGED, "fused": L.MODE_FUSED}
 
 
 def params_struct(p):
@@ -103,7 +104,7 @@ def taxonomy_struct(t):
 class GpuScorer:
     """One libwaafle_hip context on one device."""
 
-    def __init__(self, device=0, lds_bytes=None, threads=None, tier2_lds_bytes=None):
+    def __init__(self, device=0, lds_bytes=None, threads=None, tier2_lds_bytes=None, mode=None):
         self.lib = L.load()
         h = C.c_void_p()
         rc = self.lib.wf_init(int(device), C.byref(h))
@@ -111,6 +112,8 @@ class GpuScorer:
             raise L.WaafleHipError(rc, "wf_init(device={}) failed".format(device))
         self.h = h
         self.device = device
+        if mode is not None:
+            self._check(self.lib.wf_set_mode(self.h, MODES[mode] if isinstance(mode, str) else int(mode)))
         if lds_bytes:
             self._check(self.lib.wf_set_lds_bytes(self.h, int(lds_bytes)))
         if threads:

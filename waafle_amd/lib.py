@@ -12,6 +12,7 @@ LIB_PATH = os.path.join(HERE, "libwaafle_hip.so")
 WF_OK, WF_E_BADINPUT, WF_E_HIP, WF_E_RUNAWAY, WF_E_NOMEM, WF_E_STATE, WF_E_EMPTYMASK = \
     0, -1, -2, -3, -4, -5, -6
 CALL_UNCLASSIFIED, CALL_NO_LGT, CALL_LGT = 0, 1, 2
+MODE_STAGED, MODE_FUSED = 0, 1
 
 _P = C.c_void_p
 
@@ -64,6 +65,7 @@ SIGNATURES = {
     "wf_set_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
     "wf_set_workgroup": (C.c_int, [C.c_void_p, C.c_int]),
     "wf_set_tier2_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
+    "wf_set_mode": (C.c_int, [C.c_void_p, C.c_int]),
     "wf_set_taxonomy": (C.c_int, [C.c_void_p, C.POINTER(WfTaxonomy)]),
     "wf_score": (C.c_int, [C.c_void_p, C.POINTER(WfBatch), C.POINTER(WfParams),
                            C.POINTER(WfResult)]),
