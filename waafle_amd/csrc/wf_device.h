@@ -429,12 +429,27 @@ struct KeySrc {
   const int *alo, *ahi;
   const double* asc;
   __device__ __forceinline__ int idx(int t) const { return (int)(keys[t] & 0xFFFFFFull); }
+  __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
+    l = alo[a]; h = ahi[a]; v = asc[a];
+  }
+};
+struct SortedSrc {                       // attachments gathered into sorted order
+  const int2* lohi;
+  const double* sc;
+  __device__ __forceinline__ int idx(int t) const { return t; }
+  __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
+    const int2 x = lohi[a];
+    l = x.x; h = x.y; v = sc[a];
+  }
 };
 struct ValSrc {
   const int* vals;
   const int *alo, *ahi;
   const double* asc;
   __device__ __forceinline__ int idx(int t) const { return vals[t]; }
+  __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
+    l = alo[a]; h = ahi[a]; v = asc[a];
+  }
 };
 
 template <class Src>
@@ -450,15 +465,16 @@ struct SegAttT {
 #pragma unroll
     for (int i = 0; i < kRegAtt; ++i) {
       const bool use = reg && kb + i < ke;
-      const int a = use ? C.idx(kb + i) : 0;
-      lo[i] = use ? C.alo[a] : 0;
-      hi[i] = use ? C.ahi[a] : 0;          // lo == hi: never covers
-      sc[i] = use ? C.asc[a] : 0.0;
+      int l = 0, h = 0;
+      double v = 0.0;
+      if (use) C.att(C.idx(kb + i), l, h, v);
+      lo[i] = l;
+      hi[i] = h;                           // lo == hi: never covers
+      sc[i] = v;
     }
   }
   __device__ __forceinline__ void get(const Src& C, int t, int& l, int& h, double& v) const {
-    const int a = C.idx(t);
-    l = C.alo[a]; h = C.ahi[a]; v = C.asc[a];
+    C.att(C.idx(t), l, h, v);
   }
   __device__ __forceinline__ double value_at(const Src& C, int x) const {
     double v = 0.0;

@@ -64,6 +64,16 @@ struct SArgs {
   int32_t* act_next; int64_t* act_base_next;      // raised contigs (next level)
   unsigned long long* counters;  // [0] next active, [1] next attachments, [2] big count
   int32_t* big_list;             // contigs whose decision state needs an HBM slot
+  int32_t* seg_nleaf;            // [segments + 1] numpy leaves per segment
+  int32_t* leaf_off;             // [segments + 1] exclusive scan of seg_nleaf
+  int32_t* leaf_seg;             // [leaves] segment of each leaf
+  int4* seg_rec;                 // [segments] (first sorted attachment, count, locus length, leaves)
+  int2* seg_cg;                  // [segments] (clade, locus)
+  int32_t* crank_first;          // [active + 1] first segment of each active contig
+  int2* satt_lohi;               // [attachments] site range, in sorted (segment) order
+  double* satt_sc;               // [attachments] score, in sorted order
+  double* leaf_val;              // [leaves] exact leaf sums
+  uint64_t* annot_best;          // [n_loci * n_sys] best annotation score bits
   const int32_t* lut_off;        // [kNpyBuf + 2] numpy leaf table offsets by length
   const int4* lut;               // (start, length, parent adds) per leaf
   int64_t dec_lds_bytes;         // LDS arena of the decision workgroup

@@ -50,6 +50,10 @@ __device__ __forceinline__ int lower_bound_i32(const int32_t* a, int n, int x) {
   return lo;
 }
 
+__device__ __forceinline__ int seg_count(const SArgs& S, int64_t n_keys) {
+  return n_keys > 0 ? S.seg_id[n_keys - 1] : 0;
+}
+
 __device__ __forceinline__ bool attaches(const DevParams& P, int qlo, int qhi, int hs, int l1,
                                          int len, int lst) {
   if (P.stranded && hs != lst) return false;
@@ -90,23 +94,32 @@ __global__ void k_hit_contig(const SArgs* __restrict__ sp, int32_t* hit_contig) 
   hit_contig[h] = upper_index(S.k.hit_off, S.k.n_contigs, h);
 }
 
-__global__ void k_att_count(const SArgs* __restrict__ sp, int64_t* cnt) {
+// Attachments per hit (cnt) and an upper bound of the numpy leaves their segments can
+// have (leaves: a segment has at most the leaves of its locus, and no more segments than
+// attachments).
+__global__ void k_att_count(const SArgs* __restrict__ sp, int64_t* cnt, int64_t* leaves) {
   const SArgs& S = *sp;
   const KArgs& K = S.k;
   const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (h > S.n_hits_i) return;
-  if (h == S.n_hits_i) { cnt[h] = 0; return; }
+  if (h == S.n_hits_i) { cnt[h] = 0; leaves[h] = 0; return; }
   int n = 0;
+  int64_t nl = 0;
   if (K.scov[h] >= K.p.min_scov) {
     const int c = S.hit_contig[h];
     const int qlo = K.qlo[h], qhi = K.qhi[h], hs = K.hstrand[h];
     for (int64_t l = K.loc_off[c]; l < K.loc_off[c + 1]; ++l) {
       const int s = K.lstart[l], e = K.lend[l];
       const int lo = min(s, e), len = max(s, e) - lo + 1;
-      n += attaches(K.p, qlo, qhi, hs, lo, len, K.lstrand[l]) ? 1 : 0;
+      if (attaches(K.p, qlo, qhi, hs, lo, len, K.lstrand[l])) {
+        ++n;
+        nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+              (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+      }
     }
   }
   cnt[h] = n;
+  leaves[h] = nl;
 }
 
 __global__ void k_att_fill(const SArgs* __restrict__ sp) {
@@ -141,25 +154,24 @@ __global__ void k_att_fill(const SArgs* __restrict__ sp) {
 }
 
 // Annotation transfer (orgscorer.py:383-392): per (locus, system) the last hit in file
-// order whose score equals the running maximum >= threshold.
-__global__ void k_annot(const SArgs* __restrict__ sp, int64_t n_loci) {
+// order whose score equals the running maximum >= threshold, i.e. the largest hit index
+// among the hits with the maximal qualifying score.  Two passes over attachments: max
+// score bits (scores are >= 0), then max hit index at that score.
+__global__ void k_annot(const SArgs* __restrict__ sp, int64_t n_att, int pass) {
   const SArgs& S = *sp;
   const KArgs& K = S.k;
-  const int64_t l = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= n_loci || K.n_sys == 0) return;
-  const int c = upper_index(K.loc_off, K.n_contigs, l);
-  const int g = (int)(l - K.loc_off[c]);
-  const int64_t a0 = S.att_off[K.hit_off[c]], a1 = S.att_off[K.hit_off[c + 1]];
+  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (a >= n_att) return;
+  const int h = S.att_hit[a];
+  const uint32_t m = K.sysmask[h];
+  const double sc = S.att_sc[a];
+  if (m == 0 || !(sc >= K.p.annot_ref)) return;
+  const int64_t l = K.loc_off[S.hit_contig[h]] + S.att_loc[a];
   for (int b = 0; b < K.n_sys; ++b) {
-    double best = -1.0;
-    int idx = -1;
-    for (int64_t a = a0; a < a1; ++a) {
-      if (S.att_loc[a] != g) continue;
-      const double s = S.att_sc[a];
-      if (!((K.sysmask[S.att_hit[a]] >> b) & 1u) || !(s >= K.p.annot_ref)) continue;
-      if (s > best || (s == best && S.att_hit[a] > idx)) { best = s; idx = S.att_hit[a]; }
-    }
-    K.annot[l * K.n_sys + b] = idx;
+    if (!((m >> b) & 1u)) continue;
+    const int64_t slot = l * K.n_sys + b;
+    if (pass == 0) atomicMax(reinterpret_cast<unsigned long long*>(&S.annot_best[slot]), dbits(sc));
+    else if (S.annot_best[slot] == dbits(sc)) atomicMax(&K.annot[slot], h);
   }
 }
 
@@ -208,35 +220,159 @@ __global__ void k_segs(const SArgs* __restrict__ sp, int64_t n) {
   if (i == n - 1) S.seg_start[S.seg_id[i]] = (int)n;
 }
 
-// Exact np.mean of one (clade, locus) site array from its attachments and the leaf table
-// of each 8192-element numpy buffer (same arithmetic as the fused serial path).
-__global__ void k_seg_mean(const SArgs* __restrict__ sp, int64_t n) {
+// crank_first[cr] = first segment of active contig cr (segments are sorted by rank; ranks
+// without segments get the next rank's start), crank_first[n_act] = segment count.
+__global__ void k_crank_first(const SArgs* __restrict__ sp, int64_t n_keys, int n_act) {
   const SArgs& S = *sp;
-  const KArgs& K = S.k;
+  const int ns = seg_count(S, n_keys);
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > ns) return;
+  const int c0 = s == 0 ? -1 : S.seg_crank[s - 1];
+  const int c1 = s == ns ? n_act : S.seg_crank[s];
+  for (int cr = c0 + 1; cr <= c1; ++cr) S.crank_first[cr] = s;
+}
+
+// Attachments copied into sorted order, so each segment's are contiguous.
+__global__ void k_gather(const SArgs* __restrict__ sp, int64_t n) {
+  const SArgs& S = *sp;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n || !S.flags[i]) return;
-  const int s = S.seg_id[i] - 1;
-  const int kb = (int)i, ke = S.seg_start[s + 1];
-  const uint64_t key = S.keys[i];
+  if (i >= n) return;
+  const int a = S.vals[i];
+  S.satt_lohi[i] = make_int2(S.att_lo[a], S.att_hi[a]);
+  S.satt_sc[i] = S.att_sc[a];
+}
+
+// ---- exact segment means, leaf-parallel ------------------------------------------------
+// A segment's site array (length n) is summed by numpy as 8192-element buffers added in
+// order from 0.0, each buffer by the pairwise tree whose leaves the LUT lists.  Leaves are
+// evaluated independently (one thread each, closed forms; the rare multi-run leaf by eight
+// cooperating lanes), then one thread per segment combines its leaf values in tree order.
+struct SegInfo {
+  int kb, ke, c, g, len;
+};
+
+__device__ __forceinline__ SegInfo seg_info(const SArgs& S, int s) {
+  const KArgs& K = S.k;
+  SegInfo i;
+  i.kb = S.seg_start[s];
+  i.ke = S.seg_start[s + 1];
+  const uint64_t key = S.keys[i.kb];
   const int crank = (int)(key >> (S.key_tb + S.key_lb));
-  const int g = (int)(key & ((1ull << S.key_lb) - 1));
-  const int c = S.act ? S.act[crank] : crank;
-  const int64_t l = K.loc_off[c] + g;
+  i.g = (int)(key & ((1ull << S.key_lb) - 1));
+  i.c = S.act ? S.act[crank] : crank;
+  const int64_t l = K.loc_off[i.c] + i.g;
   const int ls = K.lstart[l], le = K.lend[l];
-  const int len = max(ls, le) - min(ls, le) + 1;
-  const ValSrc src{S.vals, S.att_lo, S.att_hi, S.att_sc};
-  SegAttT<ValSrc> at;
-  at.load(src, kb, ke);
+  i.len = max(ls, le) - min(ls, le) + 1;
+  return i;
+}
+
+__device__ __forceinline__ int lut_count(const SArgs& S, int m) { return S.lut_off[m + 1] - S.lut_off[m]; }
+
+// Per segment: its leaf count (for the leaf offsets scan) and a self-contained record, so
+// the leaf kernels resolve a segment with one load.
+__global__ void k_seg_rec(const SArgs* __restrict__ sp, int64_t n_keys) {
+  const SArgs& S = *sp;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > n_keys) return;
+  int nl = 0;
+  if (s < seg_count(S, n_keys)) {
+    const SegInfo si = seg_info(S, (int)s);
+    nl = (si.len / kNpyBuf) * lut_count(S, kNpyBuf) + lut_count(S, si.len % kNpyBuf);
+    S.seg_rec[s] = make_int4(si.kb, si.ke - si.kb, si.len, nl);
+    S.seg_cg[s] = make_int2((int)((S.keys[si.kb] >> S.key_lb) & ((1ull << S.key_tb) - 1)), si.g);
+  }
+  S.seg_nleaf[s] = nl;
+}
+
+// leaf j of a segment: (start within the locus, length)
+__device__ __forceinline__ int2 leaf_span(const SArgs& S, int len, int j) {
+  const int full = len / kNpyBuf, per = lut_count(S, kNpyBuf);
+  int chunk, m, jj;
+  if (j < full * per) { chunk = j / per; jj = j - chunk * per; m = kNpyBuf; }
+  else { chunk = full; jj = j - full * per; m = len - full * kNpyBuf; }
+  const int4 e = S.lut[S.lut_off[m] + jj];
+  return make_int2(chunk * kNpyBuf + e.x, e.y);
+}
+
+__global__ void k_leaf_expand(const SArgs* __restrict__ sp, int64_t n_keys) {
+  const SArgs& S = *sp;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= seg_count(S, n_keys)) return;
+  const int o = S.leaf_off[s], n = S.seg_nleaf[s];
+  for (int j = 0; j < n; ++j) S.leaf_seg[o + j] = (int)s;
+}
+
+// One lane per leaf.  Leaves without a closed form (multi-run envelopes, ~3% of the
+// partial leaves) are finished cooperatively by the wave right away: lane octet j takes
+// the j-th of them, lane c of the octet its stride accumulator c, and the eight sums are
+// combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) with xor shuffles (float addition is
+// commutative, so the result is exact).  Wave-uniform loop: every lane runs the same trips.
+__global__ void k_leaf(const SArgs* __restrict__ sp, int64_t n_keys) {
+  const SArgs& S = *sp;
+  const int ns = seg_count(S, n_keys);
+  const int TL = S.leaf_off[ns];
+  const SortedSrc src{S.satt_lohi, S.satt_sc};
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (int base = wave * 64; base < TL; base += nwaves * 64) {
+    const int i = base + lane;
+    const bool has = i < TL;
+    int4 r = make_int4(0, 0, 0, 0);
+    int st = 0, ln = 0;
+    double v = 0.0;
+    bool runs = false;
+    SegAttT<SortedSrc> at;
+    if (has) {
+      const int s = S.leaf_seg[i];
+      r = S.seg_rec[s];
+      const int2 span = leaf_span(S, r.z, i - S.leaf_off[s]);
+      st = span.x; ln = span.y;
+      at.load(src, r.x, r.x + r.y);
+      runs = !at.leaf_fast(src, st, ln, v);
+    }
+    uint64_t pend = __ballot(runs);
+    while (pend) {
+      const int oct = lane >> 3, c = lane & 7;
+      uint64_t m = pend;
+      for (int k = 0; k < oct && m; ++k) m &= m - 1;
+      const int src_lane = m ? __builtin_ctzll(m) : lane;
+      const int okb = __shfl(r.x, src_lane, 64), ona = __shfl(r.y, src_lane, 64);
+      const int ost = __shfl(st, src_lane, 64), oln = __shfl(ln, src_lane, 64);
+      double acc = 0.0;
+      if (m) {
+        SegAttT<SortedSrc> a2;
+        a2.load(src, okb, okb + ona);
+        acc = a2.stride_sum(src, ost, oln >> 3, c);
+      }
+      acc = acc + __shfl_xor(acc, 1, 64);
+      acc = acc + __shfl_xor(acc, 2, 64);
+      acc = acc + __shfl_xor(acc, 4, 64);
+      const int j = __popcll(pend & ((1ull << lane) - 1ull));
+      const double body = __shfl(acc, (j & 7) * 8, 64);
+      if (runs && j < 8) { v = at.add_tail(src, st, ln, body); runs = false; }
+      for (int k = 0; k < 8 && pend; ++k) pend &= pend - 1;
+    }
+    if (has) S.leaf_val[i] = v;
+  }
+}
+
+__global__ void k_seg_combine(const SArgs* __restrict__ sp, int64_t n_keys) {
+  const SArgs& S = *sp;
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= seg_count(S, n_keys)) return;
+  const int len = S.seg_rec[s].z;
+  const double* lv = S.leaf_val + S.leaf_off[s];
   double total = 0.0;
+  int j = 0;
   for (int o = 0; o < len; o += kNpyBuf) {
     const int m = min(kNpyBuf, len - o);
-    const int4* lv = S.lut + S.lut_off[m];
-    const int nl = S.lut_off[m + 1] - S.lut_off[m];
+    const int4* lt = S.lut + S.lut_off[m];
+    const int nl = lut_count(S, m);
     SumStack stk;
-    for (int j = 0; j < nl; ++j) {
-      const int4 e = lv[j];
-      stk.push(at.leaf(src, o + e.x, e.y));
-      for (int q = 0; q < e.z; ++q) stk.add_top();
+    for (int q = 0; q < nl; ++q, ++j) {
+      stk.push(lv[j]);
+      for (int a = 0; a < lt[q].z; ++a) stk.add_top();
     }
     total += stk.s0;
   }
@@ -264,14 +400,13 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   const int G = C.G;
   if (H == 0 || G == 0) return true;            // never evaluated (orgscorer.py:959)
   if (tid == 0) {
-    const int nseg = n_keys > 0 ? S.seg_id[n_keys - 1] : 0;
-    ctl.cnt = lower_bound_i32(S.seg_crank, nseg, cr);
-    ctl.cnt2 = lower_bound_i32(S.seg_crank, nseg, cr + 1);
     ctl.status = 0;
     ctl.p_unk = -1;
   }
+  const int so = n_keys > 0 ? S.crank_first[cr] : 0;
+  const int se = n_keys > 0 ? S.crank_first[cr + 1] : 0;
+  const int ns = se - so;
   __syncthreads();
-  const int so = ctl.cnt, se = ctl.cnt2, ns = se - so;
   const int Pmax = ns + 1;
   Arena ar{abase, acap, 0};
   C.cl_id = ar.take<int>(Pmax);
@@ -298,7 +433,8 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
     C.loc_len[g] = max(ls, le) - min(ls, le) + 1;
   }
   const uint64_t cmask = (1ull << S.key_tb) - 1;
-  auto clade_of = [&](int s) { return (int)((S.keys[S.seg_start[s]] >> S.key_lb) & cmask); };
+  (void)cmask;
+  auto clade_of = [&](int s) { return S.seg_cg[s].x; };
   // clade list = distinct clades of the segments (sorted by id = name order)
   const int per = (ns + NT - 1) / NT;
   const int b = min(ns, tid * per), e = min(ns, b + per);
@@ -334,8 +470,7 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   for (int i = tid; i < Pn * G; i += NT) C.S[i] = 0.0;
   __syncthreads();
   for (int t = tid; t < ns; t += NT) {
-    const int g = (int)(S.keys[S.seg_start[so + t]] & ((1ull << S.key_lb) - 1));
-    C.S[(int64_t)seg_ci[t] * G + g] = S.seg_mean[so + t];
+    C.S[(int64_t)seg_ci[t] * G + S.seg_cg[so + t].y] = S.seg_mean[so + t];
   }
   __syncthreads();
   const int iteration = level + 1;
@@ -364,7 +499,7 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   return true;
 }
 
-constexpr int kDecNT = 128;
+constexpr int kDecNT = 64;   // one wave per contig decision: no cross-wave barriers
 
 __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs* __restrict__ sp, int n_act,
                                                        int level, int64_t n_keys) {
@@ -439,9 +574,11 @@ struct StagedState {
   Buf lut_off, lut, sargs, kargs_big, cnt, att_off, hit_contig, counters, pinned_dummy;
   Buf att_lo, att_hi, att_loc, att_clade, att_hit, att_sc;
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
+  Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
+  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc;
   Buf act0, act1, base0, base1, big_list, big_ws, tmp;
   bool lut_ready = false;
-  int64_t dec_lds = 48 * 1024;
+  int64_t dec_lds = 24 * 1024;
   unsigned long long* host_counters = nullptr;   // pinned
   SArgs* ring = nullptr;                          // pinned argument snapshots
   ~StagedState() {
@@ -503,14 +640,14 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   const int N = k.n_contigs;
   if (N <= 0) return 0;
   g_sync_stream = s;
+  if (!st->host_counters) { *err = "pinned host allocation failed"; return -2; }
   int rc = build_lut(st, s, err);
   if (rc) return rc;
-  // host copy of the offsets we need: total hits / loci
-  int64_t tail[2];
-  ST_TRY(hipMemcpyAsync(&tail[0], k.hit_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  ST_TRY(hipMemcpyAsync(&tail[1], k.loc_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  int64_t* hc = reinterpret_cast<int64_t*>(st->host_counters);   // pinned
+  ST_TRY(hipMemcpyAsync(&hc[0], k.hit_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipMemcpyAsync(&hc[1], k.loc_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   ST_TRY(hipStreamSynchronize(s));
-  const int64_t NH = tail[0], NL = tail[1];
+  const int64_t NH = hc[0], NL = hc[1];
   if (NH >= (int64_t(1) << 31) - 1) { *err = "too many hits for one batch (split it)"; return -1; }
 
   SArgs sa{};
@@ -545,26 +682,40 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   // contigs, hits -> attachments
   ST_TRY(st->hit_contig.ensure((size_t)std::max<int64_t>(NH, 1) * sizeof(int32_t)));
   ST_TRY(st->cnt.ensure((size_t)(NH + 1) * sizeof(int64_t)));
+  ST_TRY(st->cnt_leaves.ensure((size_t)(NH + 1) * sizeof(int64_t)));
   ST_TRY(st->att_off.ensure((size_t)(NH + 1) * sizeof(int64_t)));
+  ST_TRY(st->red.ensure(sizeof(int64_t)));
   sa.hit_contig = st->hit_contig.as<int32_t>();
   sa.att_off = st->att_off.as<int64_t>();
   ST_TRY(upload());
   hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, &dsa->k);
   hipLaunchKernelGGL(k_hit_contig, dim3(grid_for(NH)), dim3(256), 0, s, dsa, st->hit_contig.as<int32_t>());
-  hipLaunchKernelGGL(k_att_count, dim3(grid_for(NH + 1)), dim3(256), 0, s, dsa, st->cnt.as<int64_t>());
+  hipLaunchKernelGGL(k_att_count, dim3(grid_for(NH + 1)), dim3(256), 0, s, dsa, st->cnt.as<int64_t>(),
+                     st->cnt_leaves.as<int64_t>());
   ST_TRY(hipGetLastError());
-  size_t tmp_bytes = 0;
-  ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, st->cnt.as<int64_t>(),
-                                          st->att_off.as<int64_t>(), (int)(NH + 1), s));
-  ST_TRY(st->tmp.ensure(tmp_bytes));
-  tmp_bytes = st->tmp.n;
-  ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, tmp_bytes, st->cnt.as<int64_t>(),
-                                          st->att_off.as<int64_t>(), (int)(NH + 1), s));
-  int64_t A = 0;
-  ST_TRY(hipMemcpyAsync(&A, st->att_off.as<int64_t>() + NH, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  {
+    size_t t1 = 0, t2 = 0;
+    ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, st->cnt.as<int64_t>(),
+                                            st->att_off.as<int64_t>(), (int)(NH + 1), s));
+    ST_TRY(hipcub::DeviceReduce::Sum(nullptr, t2, st->cnt_leaves.as<int64_t>(),
+                                     st->red.as<int64_t>(), (int)(NH + 1), s));
+    ST_TRY(st->tmp.ensure(std::max(t1, t2)));
+    size_t tb = st->tmp.n;
+    ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, tb, st->cnt.as<int64_t>(),
+                                            st->att_off.as<int64_t>(), (int)(NH + 1), s));
+    tb = st->tmp.n;
+    ST_TRY(hipcub::DeviceReduce::Sum(st->tmp.p, tb, st->cnt_leaves.as<int64_t>(),
+                                     st->red.as<int64_t>(), (int)(NH + 1), s));
+  }
+  ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + NH, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   ST_TRY(hipStreamSynchronize(s));
-  if (A >= (int64_t(1) << 31) - 1) { *err = "too many hit-locus attachments for one batch"; return -1; }
-  const size_t A1 = (size_t)std::max<int64_t>(A, 1);
+  const int64_t A = hc[2], TLB = hc[3];
+  if (A >= (int64_t(1) << 31) - 1 || TLB >= (int64_t(1) << 31) - 1) {
+    *err = "too many hit-locus attachments for one batch (split it)";
+    return -1;
+  }
+  const size_t A1 = (size_t)std::max<int64_t>(A, 1), T1 = (size_t)std::max<int64_t>(TLB, 1);
   ST_TRY(st->att_lo.ensure(A1 * 4)); ST_TRY(st->att_hi.ensure(A1 * 4));
   ST_TRY(st->att_loc.ensure(A1 * 4)); ST_TRY(st->att_clade.ensure(A1 * 4));
   ST_TRY(st->att_hit.ensure(A1 * 4)); ST_TRY(st->att_sc.ensure(A1 * 8));
@@ -573,38 +724,59 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->flags.ensure(A1 * 4)); ST_TRY(st->seg_id.ensure(A1 * 4));
   ST_TRY(st->seg_start.ensure((A1 + 1) * 4)); ST_TRY(st->seg_crank.ensure(A1 * 4));
   ST_TRY(st->seg_mean.ensure(A1 * 8));
+  ST_TRY(st->seg_nleaf.ensure((A1 + 1) * 4)); ST_TRY(st->leaf_off.ensure((A1 + 1) * 4));
+  ST_TRY(st->leaf_seg.ensure(T1 * 4)); ST_TRY(st->leaf_val.ensure(T1 * 8));
+  ST_TRY(st->seg_rec.ensure(A1 * 16)); ST_TRY(st->seg_cg.ensure(A1 * 8));
+  ST_TRY(st->crank_first.ensure(((size_t)N + 1) * 4));
+  ST_TRY(st->satt_lohi.ensure(A1 * 8)); ST_TRY(st->satt_sc.ensure(A1 * 8));
   ST_TRY(st->act0.ensure((size_t)N * 4)); ST_TRY(st->act1.ensure((size_t)N * 4));
   ST_TRY(st->base0.ensure((size_t)N * 8)); ST_TRY(st->base1.ensure((size_t)N * 8));
   ST_TRY(st->big_list.ensure((size_t)N * 8));
+  const int64_t n_annot = NL * k.n_sys;
+  if (n_annot > 0) ST_TRY(st->annot_best.ensure((size_t)n_annot * 8));
+  {
+    // temp storage for every primitive of this call, sized once (no reallocation between
+    // enqueued kernels)
+    size_t t1 = 0, t2 = 0, t3 = 0;
+    hipcub::DoubleBuffer<uint64_t> kb0(st->keys0.as<uint64_t>(), st->keys1.as<uint64_t>());
+    hipcub::DoubleBuffer<int32_t> vb0(st->vals0.as<int32_t>(), st->vals1.as<int32_t>());
+    ST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kb0, vb0, (int)A1, 0, 64, s));
+    ST_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t2, st->flags.as<int32_t>(),
+                                            st->seg_id.as<int32_t>(), (int)A1, s));
+    ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, st->seg_nleaf.as<int32_t>(),
+                                            st->leaf_off.as<int32_t>(), (int)A1 + 1, s));
+    ST_TRY(st->tmp.ensure(std::max(t1, std::max(t2, t3))));
+  }
   sa.att_lo = st->att_lo.as<int32_t>(); sa.att_hi = st->att_hi.as<int32_t>();
   sa.att_loc = st->att_loc.as<int32_t>(); sa.att_clade = st->att_clade.as<int32_t>();
   sa.att_hit = st->att_hit.as<int32_t>(); sa.att_sc = st->att_sc.as<double>();
   sa.flags = st->flags.as<int32_t>(); sa.seg_id = st->seg_id.as<int32_t>();
   sa.seg_start = st->seg_start.as<int32_t>(); sa.seg_crank = st->seg_crank.as<int32_t>();
   sa.seg_mean = st->seg_mean.as<double>();
+  sa.seg_nleaf = st->seg_nleaf.as<int32_t>(); sa.leaf_off = st->leaf_off.as<int32_t>();
+  sa.leaf_seg = st->leaf_seg.as<int32_t>(); sa.leaf_val = st->leaf_val.as<double>();
+  sa.seg_rec = st->seg_rec.as<int4>();
+  sa.seg_cg = st->seg_cg.as<int2>();
+  sa.crank_first = st->crank_first.as<int32_t>();
+  sa.satt_lohi = st->satt_lohi.as<int2>(); sa.satt_sc = st->satt_sc.as<double>();
+  sa.annot_best = st->annot_best.as<uint64_t>();
   sa.big_list = st->big_list.as<int32_t>();
-  {
-    // temp storage for every primitive of this call, sized once (no reallocation between
-    // enqueued kernels)
-    size_t t1 = 0, t2 = 0;
-    hipcub::DoubleBuffer<uint64_t> kb0(st->keys0.as<uint64_t>(), st->keys1.as<uint64_t>());
-    hipcub::DoubleBuffer<int32_t> vb0(st->vals0.as<int32_t>(), st->vals1.as<int32_t>());
-    ST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, kb0, vb0, (int)A1, 0, 64, s));
-    ST_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t2, st->flags.as<int32_t>(),
-                                            st->seg_id.as<int32_t>(), (int)A1, s));
-    ST_TRY(st->tmp.ensure(std::max(t1, t2)));
-  }
   ST_TRY(upload());
   hipLaunchKernelGGL(k_att_fill, dim3(grid_for(NH)), dim3(256), 0, s, dsa);
-  if (k.n_sys > 0 && NL > 0)
-    hipLaunchKernelGGL(k_annot, dim3(grid_for(NL)), dim3(256), 0, s, dsa, NL);
-  else if (NL > 0)
-    ;  // no annotation systems: nothing to write
+  if (n_annot > 0) {
+    ST_TRY(hipMemsetAsync(st->annot_best.p, 0, (size_t)n_annot * 8, s));
+    ST_TRY(hipMemsetAsync(k.annot, 0xFF, (size_t)n_annot * 4, s));     // -1: no winner
+    if (A > 0) {
+      hipLaunchKernelGGL(k_annot, dim3(grid_for(A)), dim3(256), 0, s, dsa, A, 0);
+      hipLaunchKernelGGL(k_annot, dim3(grid_for(A)), dim3(256), 0, s, dsa, A, 1);
+    }
+  }
   ST_TRY(hipGetLastError());
 
   // roll-up levels
   Buf* act[2] = {&st->act0, &st->act1};
   Buf* base[2] = {&st->base0, &st->base1};
+  const unsigned persistent = (unsigned)st->cus * 8;
   int n_act = N;
   int64_t n_keys = A;
   for (int level = 0; n_act > 0; ++level) {
@@ -621,6 +793,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     sa.keys = nullptr;
     sa.vals = nullptr;
     ST_TRY(upload());
+    ST_TRY(hipMemsetAsync(st->counters.p, 0, 8 * sizeof(unsigned long long), s));
     if (n_keys > 0) {
       if (level == 0)
         hipLaunchKernelGGL(k_keys_all, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys,
@@ -629,26 +802,29 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
         hipLaunchKernelGGL(k_keys_active, dim3(std::min(n_act, st->cus * 8)), dim3(256), 0, s, dsa,
                            n_act, kbuf.Current(), vbuf.Current());
       ST_TRY(hipGetLastError());
-      size_t need = 0;
-      ST_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, need, kbuf, vbuf, (int)n_keys, 0, end_bit, s));
-      ST_TRY(st->tmp.ensure(need));
-      need = st->tmp.n;
+      size_t need = st->tmp.n;
       ST_TRY(hipcub::DeviceRadixSort::SortPairs(st->tmp.p, need, kbuf, vbuf, (int)n_keys, 0, end_bit, s));
-    }
-    sa.keys = kbuf.Current();
-    sa.vals = vbuf.Current();
-    ST_TRY(upload());
-    ST_TRY(hipMemsetAsync(st->counters.p, 0, 8 * sizeof(unsigned long long), s));
-    if (n_keys > 0) {
+      sa.keys = kbuf.Current();
+      sa.vals = vbuf.Current();
+      ST_TRY(upload());
       hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa.keys, n_keys, sa.flags);
-      size_t need = 0;
-      ST_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, need, sa.flags, sa.seg_id, (int)n_keys, s));
-      ST_TRY(st->tmp.ensure(need));
       need = st->tmp.n;
       ST_TRY(hipcub::DeviceScan::InclusiveSum(st->tmp.p, need, sa.flags, sa.seg_id, (int)n_keys, s));
       hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
-      hipLaunchKernelGGL(k_seg_mean, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
+      hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
+      hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys, n_act);
+      hipLaunchKernelGGL(k_seg_rec, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys);
+      need = st->tmp.n;
+      ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_nleaf, sa.leaf_off,
+                                              (int)n_keys + 1, s));
+      hipLaunchKernelGGL(k_leaf_expand, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
+      hipLaunchKernelGGL(k_leaf, dim3(persistent), dim3(256), 0, s, dsa, n_keys);
+      hipLaunchKernelGGL(k_seg_combine, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
       ST_TRY(hipGetLastError());
+    } else {
+      sa.keys = kbuf.Current();
+      sa.vals = vbuf.Current();
+      ST_TRY(upload());
     }
     if (st->dec_lds > 64 * 1024) {
       static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide),
