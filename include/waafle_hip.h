@@ -39,10 +39,10 @@ enum wf_status {
 enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
 
 /* Execution form of wf_score (same results either way):
- *  WF_MODE_STAGED: one flat kernel per phase over all contigs (hits, attachments,
+ *  WF_MODE_STAGED (default): one flat kernel per phase over all contigs (hits, attachments,
  *    a device radix sort per roll-up level, segments, per-contig decisions); synchronises
  *    on the context stream between roll-up levels.
- *  WF_MODE_FUSED (default): one workgroup carries a contig through every phase (LDS tiers + an HBM
+ *  WF_MODE_FUSED: one workgroup carries a contig through every phase (LDS tiers + an HBM
  *    workspace tier); fully asynchronous when the batch is device resident. */
 enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_FUSED = 1 };
 

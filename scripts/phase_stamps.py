@@ -15,7 +15,7 @@ from waafle_amd import build, cli, engine, lib as L, synth  # noqa: E402
 
 NAMES = {0: "loci+leaf counts", 1: "attach count+scan", 2: "leaf tables+attach fill",
          3: "annotations+jump", 4: "keys build", 5: "bitonic sort", 6: "segments/clades scan",
-         7: "S alloc/zero", 8: "site: serial segments", 9: "maxes+weak loci", 10: "explain_one",
+         7: "S alloc/zero (staged: decide setup)", 8: "site: serial segments", 9: "maxes+weak loci", 10: "explain_one",
          11: "meld_one+write", 12: "two: pass 2 + meld", 20: "contigs (count)", 21: "levels (count)",
          22: "site: classify segments", 23: "site: 8-lane groups", 24: "site: 16-lane groups",
          25: "site: 32-lane groups", 26: "site: 64-lane groups", 16: "two: potential scan",
@@ -33,24 +33,28 @@ def main():
     ap.add_argument("--contigs", type=int, default=None)
     ap.add_argument("--lds-bytes", type=int, default=None)
     ap.add_argument("--threads", type=int, default=None)
+    ap.add_argument("--mode", default="fused", choices=["fused", "staged"])
     a = ap.parse_args()
     path = build.build(stamps=True, verbose=False)
     L._lib = None
     so = L.load(path)
-    so.wf_stamps_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    sfx = "_staged" if a.mode == "staged" else ""
+    read = getattr(so, "wf_stamps_read" + sfx)
+    reset = getattr(so, "wf_stamps_reset" + sfx)
+    read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     spec = dict(synth.CONFIGS[a.config])
     if a.contigs:
         spec["n"] = a.contigs
     data = synth.generate(seed=int(a.config[-1]), **spec)
     batch, tax = synth.to_batch(data, with_codes=False)
     params = cli.param_dict(cli.parse_flags([]))
-    s = engine.GpuScorer(0, a.lds_bytes, a.threads)
+    s = engine.GpuScorer(0, a.lds_bytes, a.threads, mode=a.mode)
     s.set_taxonomy(tax)
     s.score(batch, params)            # warm-up
-    so.wf_stamps_reset()
+    reset()
     s.score(batch, params)
     buf = (C.c_ulonglong * 32)()
-    so.wf_stamps_read(buf, 32)
+    read(buf, 32)
     n = batch.n_contigs
     total = sum(buf[i] for i in PHASES)
     print("contigs={} (stamps: s_memtime cycles per contig, thread 0)".format(

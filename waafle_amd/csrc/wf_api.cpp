@@ -48,7 +48,7 @@ struct wf_ctx {
   std::vector<std::pair<int, int>> ev_lds, ev_big;  // indices into ev_pool
   int64_t launches = 0, overflow_contigs = 0;
   // path: WF_MODE_STAGED (flat kernels per phase) or WF_MODE_FUSED (workgroup per contig)
-  int mode = WF_MODE_FUSED;
+  int mode = WF_MODE_STAGED;
   bool lds_set = false;            // wf_set_lds_bytes called: also the staged decision arena
   wf::StagedState* staged = nullptr;
 };

@@ -383,6 +383,8 @@ struct Contig {
   uint64_t* mask;
   unsigned *bm1, *bm2;
   uint8_t* best_syn;
+  char* xws = nullptr;                    // optional scratch for mask classes (explain_two)
+  int64_t xcap = 0;
 };
 
 // Shift-register stack of partial sums for numpy's pairwise tree.  Static indexing keeps
@@ -751,6 +753,126 @@ __device__ __forceinline__ void for_each_candidate_t(const uint64_t* mask, int P
   }
 }
 
+// Mask classes for large potential sets: potential clades with the same "score >= k2" mask
+// are interchangeable for the crit >= k2 test, so the test runs once per pair of classes
+// (U^2 / 2 instead of Pp^2 / 2), and only members of passing class pairs are enumerated --
+// exactly the same candidate pairs, in a different order (pass 1 picks by (rank, pair
+// index), pass 2 only aggregates, so the order does not matter).
+constexpr int kClsMin = 512;            // use classes from this many potential clades on
+constexpr int kClsMaxU = 2048;          // ... unless the masks are this diverse
+constexpr int kClsMaxPairs = 4096;      // ... or this many class pairs pass
+
+__device__ __forceinline__ int64_t cls_bytes(int pmax) {
+  int n2 = 1;
+  while (n2 < pmax) n2 <<= 1;
+  return (int64_t)n2 * 8 + (int64_t)(pmax + 1) * 4 + kClsMaxPairs * 8 + (kClsMaxPairs + 1) * 8 + 64;
+}
+
+struct MaskClasses {
+  int U, npairs, ib;
+  uint64_t* keys;      // (mask << ib | potential index), sorted: classes are runs
+  int* cstart;         // [U + 1]
+  int2* pairs;         // passing class pairs (a <= b)
+  long long* pref;     // [npairs + 1] candidate-count prefix
+};
+
+// Builds the classes (block-wide).  Returns false when they would not pay off or fit.
+template <int NT>
+__device__ bool build_mask_classes(const Contig& C, Ctl& ctl, int Pp, int Gu, uint64_t full,
+                                   MaskClasses& M) {
+  const int tid = threadIdx.x;
+  int ib = 1;
+  while ((1 << ib) < Pp) ++ib;
+  if (!C.xws || Pp < kClsMin || Gu + ib > 64 || cls_bytes(Pp) > C.xcap) return false;
+  int n2 = 1;
+  while (n2 < Pp) n2 <<= 1;
+  Arena ar{C.xws, C.xcap, 0};
+  M.ib = ib;
+  M.keys = ar.take<uint64_t>(n2);
+  M.cstart = ar.take<int>(Pp + 1);
+  M.pairs = ar.take<int2>(kClsMaxPairs);
+  M.pref = ar.take<long long>(kClsMaxPairs + 1);
+  for (int t = tid; t < n2; t += NT)
+    M.keys[t] = t < Pp ? ((C.mask[t] << ib) | (uint64_t)t) : ~0ull;
+  __syncthreads();
+  bitonic_sort<NT>(M.keys, n2);
+  const int per = (Pp + NT - 1) / NT;
+  const int b = min(Pp, tid * per), e = min(Pp, b + per);
+  int nc = 0;
+  for (int t = b; t < e; ++t)
+    if (t == 0 || (M.keys[t] >> ib) != (M.keys[t - 1] >> ib)) ++nc;
+  int U;
+  int ci = block_scan<NT>(nc, &U, ctl);
+  for (int t = b; t < e; ++t)
+    if (t == 0 || (M.keys[t] >> ib) != (M.keys[t - 1] >> ib)) M.cstart[ci++] = t;
+  if (tid == 0) { M.cstart[U] = Pp; ctl.cnt = 0; }
+  __syncthreads();
+  M.U = U;
+  if (U > kClsMaxU) return false;
+  for (int t = tid; t < U * U; t += NT) {
+    const int a = t / U, bb = t % U;
+    if (a > bb) continue;
+    const uint64_t ma = M.keys[M.cstart[a]] >> ib, mb = M.keys[M.cstart[bb]] >> ib;
+    if ((ma | mb) != full) continue;
+    if (a == bb && M.cstart[a + 1] - M.cstart[a] < 2) continue;
+    const int slot = atomicAdd(&ctl.cnt, 1);
+    if (slot < kClsMaxPairs) M.pairs[slot] = make_int2(a, bb);
+  }
+  __syncthreads();
+  const int np = ctl.cnt;
+  __syncthreads();
+  if (np > kClsMaxPairs) return false;
+  if (tid == 0) {
+    long long acc = 0;
+    for (int q = 0; q < np; ++q) {
+      M.pref[q] = acc;
+      const int2 ab = M.pairs[q];
+      const long long na = M.cstart[ab.x + 1] - M.cstart[ab.x];
+      const long long nb = M.cstart[ab.y + 1] - M.cstart[ab.y];
+      acc += ab.x == ab.y ? na * (na - 1) / 2 : na * nb;
+    }
+    M.pref[np] = acc;
+  }
+  __syncthreads();
+  M.npairs = np;
+  return true;
+}
+
+// f(i, j) for every candidate pair i < j of the classes (threads stride the candidates).
+template <int NT, class F>
+__device__ __forceinline__ void for_each_candidate_cls(const MaskClasses& M, F f) {
+  const long long T = M.npairs > 0 ? M.pref[M.npairs] : 0;
+  const uint64_t imask = (1ull << M.ib) - 1;
+  for (long long x = threadIdx.x; x < T; x += NT) {
+    int lo = 0, hi = M.npairs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (M.pref[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    const int2 ab = M.pairs[lo];
+    const long long y = x - M.pref[lo];
+    const int a0 = M.cstart[ab.x], na = M.cstart[ab.x + 1] - a0;
+    int u, v;
+    if (ab.x == ab.y) {
+      // y-th (p, q), p < q, in row-major order: row p starts at p*(2na-p-1)/2
+      int plo = 0, phi = na - 2;
+      while (plo < phi) {
+        const int mid = (plo + phi + 1) >> 1;
+        if ((long long)mid * (2 * na - mid - 1) / 2 <= y) plo = mid; else phi = mid - 1;
+      }
+      const long long rs = (long long)plo * (2 * na - plo - 1) / 2;
+      u = a0 + plo;
+      v = a0 + plo + 1 + (int)(y - rs);
+    } else {
+      const int b0 = M.cstart[ab.y], nb = M.cstart[ab.y + 1] - b0;
+      u = a0 + (int)(y / nb);
+      v = b0 + (int)(y % nb);
+    }
+    const int i = (int)(M.keys[u] & imask), j = (int)(M.keys[v] & imask);
+    f(min(i, j), max(i, j));
+  }
+}
+
 template <int NW, class Slow, class F>
 __device__ __forceinline__ void for_each_candidate(const uint64_t* mask, bool use_mask, int Pp,
                                                    uint64_t full, Slow slow, F f) {
@@ -873,16 +995,16 @@ __device__ __forceinline__ double pair_crit(const Contig& C, int pa, int pb, int
 // "Unknown" when it is present.  Writes the contig's result when an explanation is found.
 // Returns kDecDone (contig finished), kDecStop (no explanation possible: unclassified, with
 // ctl.status possibly set) or kDecRaise (roll up one taxonomy level and try again).
-constexpr int kDecDone = 0, kDecStop = 1, kDecRaise = 2;
+constexpr int kDecDone = 0, kDecStop = 1, kDecRaise = 2, kDecNext = 3;
 
+// Maxes over known clades and weak loci (orgscorer.py:407-429); sets ctl.Gu / C.um /
+// C.ign / ctl.root_present.  kDecNext: go on to explain_one.
 template <int NT>
-__device__ __forceinline__ int decide_level(const KArgs& K, const Contig& C, Ctl& ctl, int c, int Pn,
-                                            int iteration, bool& first, int64_t& pair_evals) {
-  constexpr int NW = NT / 64;
-  const int tid = threadIdx.x, w = wave_id();
+__device__ __forceinline__ int decide_prologue(const KArgs& K, const Contig& C, Ctl& ctl, int Pn,
+                                               bool& first) {
+  const int tid = threadIdx.x;
   const DevParams& P = K.p;
   const int G = C.G;
-  (void)w;
   for (int g = tid; g < G; g += NT) C.maxes[g] = 0;
   if (tid == 0) ctl.root_present = 0;
   __syncthreads();
@@ -921,6 +1043,20 @@ __device__ __forceinline__ int decide_level(const KArgs& K, const Contig& C, Ctl
     return kDecStop;
   }
 
+  return kDecNext;
+}
+
+// explain_one + meld_one (orgscorer.py:585-597, 621-631).  kDecDone when a one-clade
+// explanation was written, kDecNext otherwise.
+template <int NT>
+__device__ __forceinline__ int decide_one(const KArgs& K, const Contig& C, Ctl& ctl, int c, int Pn,
+                                          int iteration, int64_t pair_evals) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, w = wave_id();
+  const DevParams& P = K.p;
+  const int G = C.G;
+  const int Gu = ctl.Gu;
+  (void)w; (void)NW;
   // ================= explain_one (orgscorer.py:585-597) ============================
   {
     // Contig.score (:447-461) for one clade: (min, np.mean) of its masked row
@@ -983,6 +1119,20 @@ __device__ __forceinline__ int decide_level(const KArgs& K, const Contig& C, Ctl
     }
   }
 
+  return kDecNext;
+}
+
+// explain_two + LGT filters + meld_two (orgscorer.py:599-619, 633-744), then the roll-up
+// decision: kDecDone (written), kDecStop (unclassified) or kDecRaise.
+template <int NT>
+__device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& ctl, int c, int Pn,
+                                          int iteration, int64_t& pair_evals) {
+  constexpr int NW = NT / 64;
+  const int tid = threadIdx.x, w = wave_id();
+  const DevParams& P = K.p;
+  const int G = C.G;
+  const int Gu = ctl.Gu;
+  (void)w; (void)NW;
   // ================= explain_two (orgscorer.py:599-619) ============================
   {
     // potential clades: max over ALL loci >= k2 (:603-605)
@@ -1029,7 +1179,10 @@ __device__ __forceinline__ int decide_level(const KArgs& K, const Contig& C, Ctl
       const long long key = (long long)i * Pp + j;
       if (better(r, key, br, bk)) { br = r; bk = key; }
     };
-    for_each_candidate<NW>(C.mask, use_mask, Pp, full, candidate, consider);
+    MaskClasses mcls;
+    const bool use_cls = use_mask && build_mask_classes<NT>(C, ctl, Pp, Gu, full, mcls);
+    if (use_cls) for_each_candidate_cls<NT>(mcls, consider);
+    else for_each_candidate<NW>(C.mask, use_mask, Pp, full, candidate, consider);
     block_argmax<NT>(br, bk, ctl);
     STAMP(18);
     bool have_ok = false;
@@ -1055,7 +1208,8 @@ __device__ __forceinline__ int decide_level(const KArgs& K, const Contig& C, Ctl
         atomicOr(&C.bm1[e.c1p >> 5], 1u << (e.c1p & 31));
         atomicOr(&C.bm2[e.c2p >> 5], 1u << (e.c2p & 31));
       };
-      for_each_candidate<NW>(C.mask, use_mask, Pp, full, candidate, within);
+      if (use_cls) for_each_candidate_cls<NT>(mcls, within);
+      else for_each_candidate<NW>(C.mask, use_mask, Pp, full, candidate, within);
       __syncthreads();
       // meld_two (:640-669)
       if (tid == 0) {
@@ -1123,6 +1277,16 @@ __device__ __forceinline__ int decide_level(const KArgs& K, const Contig& C, Ctl
   STAMP(12);
   __syncthreads();
   return (Pn == 0 || ctl.root_present) ? kDecStop : kDecRaise;
+}
+
+template <int NT>
+__device__ __forceinline__ int decide_level(const KArgs& K, const Contig& C, Ctl& ctl, int c, int Pn,
+                                            int iteration, bool& first, int64_t& pair_evals) {
+  int d = decide_prologue<NT>(K, C, ctl, Pn, first);
+  if (d != kDecNext) return d;
+  d = decide_one<NT>(K, C, ctl, c, Pn, iteration, pair_evals);
+  if (d != kDecNext) return d;
+  return decide_two<NT>(K, C, ctl, c, Pn, iteration, pair_evals);
 }
 
 }  // namespace

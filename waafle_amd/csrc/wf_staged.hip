@@ -24,7 +24,6 @@
 #include <string>
 #include <vector>
 
-#undef WF_STAMPS
 #include "wf_device.h"
 
 namespace wf {
@@ -383,7 +382,9 @@ __global__ void k_seg_combine(const SArgs* __restrict__ sp, int64_t n_keys) {
 // level (rows = clades in id order, the virtual "Unknown" row of --weak-loci
 // assign-unknown included) from the contig's segments, then runs decide_level.
 // Returns false when the arena is too small (caller hands the contig to the HBM tier).
-template <int NT>
+// PHASE 0: the whole level (HBM-slot tier); 1: prologue + explain_one, contigs without a
+// one-clade explanation are queued for phase 2; 2: prologue + explain_two + roll-up.
+template <int NT, int PHASE>
 __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* abase, int64_t acap,
                               Ctl& ctl, int64_t n_keys) {
   const KArgs& K = S.k;
@@ -399,6 +400,7 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   C.mbase = 2 * h0 + 2 * (int64_t)c;
   const int G = C.G;
   if (H == 0 || G == 0) return true;            // never evaluated (orgscorer.py:959)
+  STAMP_INIT();
   if (tid == 0) {
     ctl.status = 0;
     ctl.p_unk = -1;
@@ -423,6 +425,10 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   C.best_syn = ar.take<uint8_t>(G);
   C.loc_len = ar.take<int>(G);                  // ambiguous fraction weights (orgscorer.py:693-702)
   int* seg_ci = ar.take<int>(ns + 1);
+  if (Pmax >= kClsMin) {                         // mask classes for a large explain_two
+    C.xcap = cls_bytes(Pmax);
+    C.xws = ar.take<char>(C.xcap);
+  }
   if (!ar.fits()) {
     if (tid == 0) K.need[c] = ar.used + 4096;
     __syncthreads();
@@ -473,10 +479,29 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
     C.S[(int64_t)seg_ci[t] * G + S.seg_cg[so + t].y] = S.seg_mean[so + t];
   }
   __syncthreads();
+  STAMP(7);
   const int iteration = level + 1;
   bool first = level == 0;
   int64_t pair_evals = level == 0 ? 0 : K.pair_evals[c];
-  const int dec = decide_level<NT>(K, C, ctl, c, Pn, iteration, first, pair_evals);
+  int dec;
+  if (PHASE == 0) {
+    dec = decide_level<NT>(K, C, ctl, c, Pn, iteration, first, pair_evals);
+  } else {
+    dec = decide_prologue<NT>(K, C, ctl, Pn, first);
+    if (PHASE == 1 && dec == kDecNext) {
+      dec = decide_one<NT>(K, C, ctl, c, Pn, iteration, pair_evals);
+      if (dec == kDecNext) {
+        if (tid == 0) {
+          const int slot = (int)atomicAdd(&S.counters[5], 1ull);
+          S.two_list[2 * slot] = cr;
+          S.two_list[2 * slot + 1] = c;
+        }
+        return true;
+      }
+    } else if (PHASE == 2 && dec == kDecNext) {
+      dec = decide_two<NT>(K, C, ctl, c, Pn, iteration, pair_evals);
+    }
+  }
   if (dec == kDecDone) return true;
   if (dec == kDecRaise && iteration + 1 <= kMaxIter) {
     // roll up (orgscorer.py:431-445): this contig's attachments move to the parent clade
@@ -501,14 +526,17 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
 
 constexpr int kDecNT = 64;   // one wave per contig decision: no cross-wave barriers
 
+template <int PHASE>
 __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs* __restrict__ sp, int n_act,
                                                        int level, int64_t n_keys) {
   const SArgs& S = *sp;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
-  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
-    const int c = S.act ? S.act[cr] : cr;
-    const bool ok = decide_contig<kDecNT>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
+  const int count = PHASE == 1 ? n_act : (int)S.counters[5];
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int cr = PHASE == 1 ? i : S.two_list[2 * i];
+    const int c = PHASE == 1 ? (S.act ? S.act[cr] : cr) : S.two_list[2 * i + 1];
+    const bool ok = decide_contig<kDecNT, PHASE>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
     if (!ok && threadIdx.x == 0) {
       const int slot = (int)atomicAdd(&S.counters[2], 1ull);
       S.big_list[2 * slot] = cr;
@@ -526,7 +554,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs* __restric
   char* base = S.k.big_ws + (int64_t)blockIdx.x * S.k.slot_bytes;
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const int cr = S.big_list[2 * i], c = S.big_list[2 * i + 1];
-    const bool ok = decide_contig<kBlock>(S, c, cr, level, base, S.k.slot_bytes, ctl, n_keys);
+    const bool ok = decide_contig<kBlock, 0>(S, c, cr, level, base, S.k.slot_bytes, ctl, n_keys);
     if (!ok && threadIdx.x == 0) S.k.status[c] = WF_E_NOMEM;
     __syncthreads();
   }
@@ -576,7 +604,7 @@ struct StagedState {
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
   Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc;
-  Buf act0, act1, base0, base1, big_list, big_ws, tmp;
+  Buf act0, act1, base0, base1, big_list, two_list, big_ws, tmp;
   bool lut_ready = false;
   int64_t dec_lds = 24 * 1024;
   unsigned long long* host_counters = nullptr;   // pinned
@@ -732,6 +760,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->act0.ensure((size_t)N * 4)); ST_TRY(st->act1.ensure((size_t)N * 4));
   ST_TRY(st->base0.ensure((size_t)N * 8)); ST_TRY(st->base1.ensure((size_t)N * 8));
   ST_TRY(st->big_list.ensure((size_t)N * 8));
+  ST_TRY(st->two_list.ensure((size_t)N * 8));
   const int64_t n_annot = NL * k.n_sys;
   if (n_annot > 0) ST_TRY(st->annot_best.ensure((size_t)n_annot * 8));
   {
@@ -761,6 +790,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   sa.satt_lohi = st->satt_lohi.as<int2>(); sa.satt_sc = st->satt_sc.as<double>();
   sa.annot_best = st->annot_best.as<uint64_t>();
   sa.big_list = st->big_list.as<int32_t>();
+  sa.two_list = st->two_list.as<int32_t>();
   ST_TRY(upload());
   hipLaunchKernelGGL(k_att_fill, dim3(grid_for(NH)), dim3(256), 0, s, dsa);
   if (n_annot > 0) {
@@ -827,13 +857,21 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       ST_TRY(upload());
     }
     if (st->dec_lds > 64 * 1024) {
-      static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide),
-                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                   160 * 1024 - 1024);
-      ST_TRY(attr);
+      static hipError_t attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<1>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    160 * 1024 - 1024);
+      static hipError_t attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<2>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    160 * 1024 - 1024);
+      ST_TRY(attr1);
+      ST_TRY(attr2);
     }
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
-    hipLaunchKernelGGL(k_decide, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
+    hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
+    // explain_two for the contigs phase 1 left open (count on the device: a grid of
+    // rank-independent size, idle blocks exit at once)
+    hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * 4)), dim3(kDecNT),
+                       (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
     ST_TRY(hipGetLastError());
     ST_TRY(hipMemcpyAsync(st->host_counters, st->counters.p, 4 * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, s));
@@ -858,4 +896,15 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   return 0;
 }
 
+#ifdef WF_STAMPS
+extern "C" int wf_stamps_read_staged(unsigned long long* out, int n) {
+  if (n > 32) n = 32;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess
+             ? 0 : -2;
+}
+extern "C" int wf_stamps_reset_staged(void) {
+  unsigned long long z[32] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) == hipSuccess ? 0 : -2;
+}
+#endif
 }  // namespace wf
