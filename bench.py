@@ -196,13 +196,20 @@ def main():
     value = world * N / (elapsed / args.steps)
     k_ms = tm.lds_kernel_ms / max(1, tm.launches)
     big_ms = tm.big_kernel_ms / max(1, tm.launches)
+    if args.mode == "staged":
+        # the staged form has no single kernel that consumes the path's input: the unit is
+        # one whole wf_score pass (HIP events around all of its kernels, on its stream)
+        kname, kernel_ms = "wf_score pass (staged: all kernels)", {"wf_score_pass": k_ms}
+    else:
+        kname, kernel_ms = "k_contig_lds", {"k_contig_lds": k_ms, "k_contig_big": big_ms}
     b_alg = algorithmic_bytes(batch)
     achieved = b_alg / (k_ms * 1e-3) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         with open(args.traffic_json) as fh:
             tj = json.load(fh)
-        if tj.get("config") == args.config and tj.get("contigs") == N:
+        if (tj.get("config") == args.config and tj.get("contigs") == N
+                and tj.get("mode", "fused") == args.mode):
             traffic = tj.get("hbm_bytes_per_launch")
     ops0 = site_ops_level0(batch)
     result = {
@@ -218,10 +225,11 @@ def main():
         "calls": {"lgt": int((calls == 2).sum()), "no_lgt": int((calls == 1).sum()),
                   "unclassified": int((calls == 0).sum()),
                   "rolled_up": int((iters > 1).sum())},
-        "kernel_ms": {"k_contig_lds": k_ms, "k_contig_big": big_ms},
+        "mode": args.mode,
+        "kernel_ms": kernel_ms,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_contig_lds", "algorithmic_bytes_per_launch": b_alg,
+                     "kernel": kname, "algorithmic_bytes_per_launch": b_alg,
                      "valu": {"site_adds_level0": ops0,
                               "achieved_ops_per_s": ops0 / (k_ms * 1e-3),
                               "peak_ops_per_s": VALU_F64_PEAK,
