@@ -385,6 +385,7 @@ struct Contig {
   uint8_t* best_syn;
   char* xws = nullptr;                    // optional scratch for mask classes (explain_two)
   int64_t xcap = 0;
+  int* sib_of = nullptr;                  // [Pn] listed parent of each clade (sister checks)
 };
 
 // Shift-register stack of partial sums for numpy's pairwise tree.  Static indexing keeps
@@ -958,8 +959,8 @@ __device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int
       else if (c == 'A' && !e.dir) need = py;
       else continue;
       for (int q = 0; q < Pcount; ++q) {
+        if (C.sib_of[q] != need) continue;
         const int s = C.cl_id[q];
-        if (K.sibp[s] != need) continue;
         if (s == X || s == Y) continue;
         if (C.S[(int64_t)q * G + g] >= P.sister_thr) { e.ok = 0; break; }
       }
@@ -1133,6 +1134,10 @@ __device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& 
   const int G = C.G;
   const int Gu = ctl.Gu;
   (void)w; (void)NW;
+  if (P.sister_on) {                     // sister checks read listed parents per clade
+    for (int q = tid; q < Pn; q += NT) C.sib_of[q] = K.sibp[C.cl_id[q]];
+    __syncthreads();
+  }
   // ================= explain_two (orgscorer.py:599-619) ============================
   {
     // potential clades: max over ALL loci >= k2 (:603-605)

@@ -71,6 +71,15 @@ struct SArgs {
   int4* seg_rec;                 // [segments] (first sorted attachment, count, locus length, leaves)
   int2* seg_cg;                  // [segments] (clade, locus)
   int32_t* crank_first;          // [active + 1] first segment of each active contig
+  // flat explain_one (weak loci ignore/penalize, <= 64 loci)
+  uint64_t* lmax;                // [n_loci] per-locus max score bits over known clades
+  int32_t* c_gu;                 // [active] unmasked loci (-1: contig needs no decision)
+  uint64_t* c_umask;             // [active] unmasked-locus bit mask
+  unsigned long long* c_best;    // [active] best one-clade rank bits + 1 (0: none)
+  int32_t* c_bestcl;             // [active] best clade id (ties: larger id)
+  int32_t* c_nopt;               // [active] options within --range
+  double* run_crit;              // [segments] crit of the clade run starting here
+  double* run_rank;              // [segments] rank of the clade run starting here
   int2* satt_lohi;               // [attachments] site range, in sorted (segment) order
   double* satt_sc;               // [attachments] score, in sorted order
   double* leaf_val;              // [leaves] exact leaf sums

@@ -286,7 +286,7 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
       // explain scratch: overlays the sort keys / segment tables when they fit (both are
       // dead once the gene-score matrix exists), else follows S
       Arena ex{abase, acap, persist_mark};
-      const int64_t need_ex = (int64_t)Pn * 20 + 8 * ((Pn + 31) / 32) + G + 6 * 16;
+      const int64_t need_ex = (int64_t)Pn * 24 + 8 * ((Pn + 31) / 32) + G + 7 * 16;
       if (persist_mark + need_ex > dead_end) ex.used = ar.used;
       C.pot = ex.take<int>(Pn);
       C.mask = ex.take<uint64_t>(Pn);
@@ -295,6 +295,7 @@ __device__ __forceinline__ void process_contig(const KArgs& K, int c, char* abas
       C.bm1 = ex.take<unsigned>((Pn + 31) / 32);
       C.bm2 = ex.take<unsigned>((Pn + 31) / 32);
       C.best_syn = ex.take<uint8_t>(G);
+      C.sib_of = ex.take<int>(Pn);
       if (ex.used > ar.used) ar.used = ex.used;
     }
     if (!ar.fits()) {

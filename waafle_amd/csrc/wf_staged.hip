@@ -21,6 +21,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -378,6 +379,183 @@ __global__ void k_seg_combine(const SArgs* __restrict__ sp, int64_t n_keys) {
   S.seg_mean[s] = total / (double)len;
 }
 
+// ---- flat explain_one (orgscorer.py:407-429, 585-597, 621-631) -------------------------
+// For --weak-loci ignore/penalize and <= 64 loci, the one-clade search needs no per-contig
+// workgroup: per-locus maxes are atomics over segments, each clade run (the clade's
+// segments, sorted by locus) scores itself, the best rank is an atomic max of its bits
+// (ranks are >= 0) and ties go to the larger clade id, like the sorted-order policy.
+__global__ void k_flat_maxes(const SArgs* __restrict__ sp, int64_t n_keys) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= seg_count(S, n_keys)) return;
+  const int2 cg = S.seg_cg[s];
+  if (cg.x == K.unknown) return;
+  const double v = S.seg_mean[s];
+  if (!(v > 0.0)) return;
+  const int cr = S.seg_crank[s];
+  const int c = S.act ? S.act[cr] : cr;
+  atomicMax(reinterpret_cast<unsigned long long*>(&S.lmax[K.loc_off[c] + cg.y]), dbits(v));
+}
+
+__global__ void k_flat_prep(const SArgs* __restrict__ sp, int n_act, int level) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int cr = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cr >= n_act) return;
+  const int c = S.act ? S.act[cr] : cr;
+  const int64_t l0 = K.loc_off[c];
+  const int G = (int)(K.loc_off[c + 1] - l0);
+  const int H = (int)(K.hit_off[c + 1] - K.hit_off[c]);
+  S.c_best[cr] = 0;
+  S.c_bestcl[cr] = -1;
+  S.c_nopt[cr] = 0;
+  if (H == 0 || G == 0) { S.c_gu[cr] = -1; return; }   // never evaluated (orgscorer.py:959)
+  uint64_t um = 0;
+  for (int g = 0; g < G; ++g) {
+    const double m = __longlong_as_double((long long)S.lmax[l0 + g]);
+    if (K.p.weak != 0 || m >= K.p.kmin) um |= 1ull << g;
+  }
+  const int Gu = __popcll(um);
+  S.c_umask[cr] = um;
+  if (Gu == 0) {
+    S.c_gu[cr] = -1;
+    if (level > 0) {                                     // np.min of an empty array upstream
+      K.iters[c] = (int16_t)min(level + 1, 32767);
+      K.status[c] = WF_E_EMPTYMASK;
+    }                                                    // level 0: skipped contig
+    return;
+  }
+  S.c_gu[cr] = Gu;
+}
+
+// numpy add.reduce of n <= 128 values produced in order by next() (pairwise_sum's leaf:
+// n < 8 sequential, else eight strided accumulators combined as a tree, then the tail)
+template <class F>
+__device__ __forceinline__ double np_sum_seq(int n, F next) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += next();
+    return r;
+  }
+  double r0 = next(), r1 = next(), r2 = next(), r3 = next();
+  double r4 = next(), r5 = next(), r6 = next(), r7 = next();
+  int i = 8;
+  const int m = n - (n & 7);
+  for (; i < m; i += 8) {
+    r0 += next(); r1 += next(); r2 += next(); r3 += next();
+    r4 += next(); r5 += next(); r6 += next(); r7 += next();
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += next();
+  return res;
+}
+
+__device__ __forceinline__ bool run_start(const SArgs& S, int s) {
+  return s == 0 || S.seg_crank[s] != S.seg_crank[s - 1] || S.seg_cg[s].x != S.seg_cg[s - 1].x;
+}
+
+// pass 0: crit/rank of each clade run (Contig.score, orgscorer.py:447-461), best rank;
+// pass 1: best clade (ties -> larger id) and the options within --range (meld members)
+__global__ void k_flat_runs(const SArgs* __restrict__ sp, int64_t n_keys, int pass) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ns = seg_count(S, n_keys);
+  if (s >= ns || !run_start(S, s)) return;
+  const int cr = S.seg_crank[s];
+  const int Gu = S.c_gu[cr];
+  if (Gu <= 0) return;
+  const int clade = S.seg_cg[s].x;
+  double crit, rank;
+  if (pass == 0) {
+    uint64_t um = S.c_umask[cr];
+    int t = s;
+    crit = 0.0;
+    bool firstv = true;
+    auto next = [&]() -> double {
+      const int g = __builtin_ctzll(um);
+      um &= um - 1;
+      while (t < ns && S.seg_crank[t] == cr && S.seg_cg[t].x == clade && S.seg_cg[t].y < g) ++t;
+      const double v = (t < ns && S.seg_crank[t] == cr && S.seg_cg[t].x == clade && S.seg_cg[t].y == g)
+                           ? S.seg_mean[t] : 0.0;
+      crit = (firstv || v < crit) ? v : crit;
+      firstv = false;
+      return v;
+    };
+    rank = np_sum_seq(Gu, next) / (double)Gu;
+    S.run_crit[s] = crit;
+    S.run_rank[s] = rank;
+    if (crit >= K.p.k1) atomicMax(&S.c_best[cr], dbits(rank) + 1ull);
+    return;
+  }
+  crit = S.run_crit[s];
+  rank = S.run_rank[s];
+  if (!(crit >= K.p.k1)) return;
+  const unsigned long long b = S.c_best[cr];
+  if (dbits(rank) + 1ull == b) atomicMax(&S.c_bestcl[cr], clade);
+  if (K.p.dis1 == 1) {
+    const double br = __longlong_as_double((long long)(b - 1ull));
+    if ((br - rank) <= K.p.range) {
+      const int c = S.act ? S.act[cr] : cr;
+      const int slot = atomicAdd(&S.c_nopt[cr], 1);
+      K.meld[2 * K.hit_off[c] + 2 * (int64_t)c + slot] = clade;
+    }
+  }
+}
+
+// One thread per contig: the result of a one-clade explanation, or hand-off to explain_two.
+__global__ void k_flat_finish(const SArgs* __restrict__ sp, int n_act, int level, int64_t n_keys) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int cr = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cr >= n_act || S.c_gu[cr] <= 0) return;
+  const int c = S.act ? S.act[cr] : cr;
+  const int best = S.c_bestcl[cr];
+  if (best < 0) {                                       // no one-clade option: explain_two
+    const int slot = (int)atomicAdd(&S.counters[5], 1ull);
+    S.two_list[2 * slot] = cr;
+    S.two_list[2 * slot + 1] = c;
+    return;
+  }
+  const int m = K.p.dis1 == 1 ? S.c_nopt[cr] : 0;
+  const int64_t mbase = 2 * K.hit_off[c] + 2 * (int64_t)c;
+  if (K.p.dis1 == 1 && m == 0) {                        // negative --range upstream crash
+    K.status[c] = WF_E_BADINPUT;
+    return;
+  }
+  int lca = best;
+  if (K.p.dis1 == 1) {
+    lca = -1;
+    for (int i = 0; i < m; ++i) lca = lca2(K, lca, K.meld[mbase + i]);
+  }
+  // the best clade's run: binary search by clade among this contig's segments
+  int lo = S.crank_first[cr], hi = S.crank_first[cr + 1];
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (S.seg_cg[mid].x < best) lo = mid + 1; else hi = mid;
+  }
+  const int rs = lo;
+  const int64_t l0 = K.loc_off[c];
+  const int G = (int)(K.loc_off[c + 1] - l0);
+  const uint64_t um = S.c_umask[cr];
+  int t = rs;
+  const int se = S.crank_first[cr + 1];
+  for (int g = 0; g < G; ++g) {                         // set_synteny_one (:495-509)
+    while (t < se && S.seg_cg[t].x == best && S.seg_cg[t].y < g) ++t;
+    const double v = (t < se && S.seg_cg[t].x == best && S.seg_cg[t].y == g) ? S.seg_mean[t] : 0.0;
+    K.syn[l0 + g] = !((um >> g) & 1ull) ? '~' : (v >= K.p.k1 ? 'A' : '!');
+  }
+  K.call[c] = WF_CALL_NO_LGT;
+  K.crit[c] = S.run_crit[rs];
+  K.rank[c] = S.run_rank[rs];
+  K.c1[c] = lca;
+  K.c2[c] = -1;
+  K.nm1[c] = m;
+  K.iters[c] = (int16_t)(level + 1);
+  K.pair_evals[c] = level == 0 ? 0 : K.pair_evals[c];
+}
+
 // Decision workgroup for one contig at one level.  Builds the gene-score matrix of the
 // level (rows = clades in id order, the virtual "Unknown" row of --weak-loci
 // assign-unknown included) from the contig's segments, then runs decide_level.
@@ -424,6 +602,7 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   C.bm2 = ar.take<unsigned>((Pmax + 31) / 32);
   C.best_syn = ar.take<uint8_t>(G);
   C.loc_len = ar.take<int>(G);                  // ambiguous fraction weights (orgscorer.py:693-702)
+  C.sib_of = ar.take<int>(Pmax);
   int* seg_ci = ar.take<int>(ns + 1);
   if (Pmax >= kClsMin) {                         // mask classes for a large explain_two
     C.xcap = cls_bytes(Pmax);
@@ -604,9 +783,11 @@ struct StagedState {
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
   Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc;
+  Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
   Buf act0, act1, base0, base1, big_list, two_list, big_ws, tmp;
   bool lut_ready = false;
-  int64_t dec_lds = 24 * 1024;
+  int64_t dec_lds = 24 * 1024;       // decision arena (grows with the data, see staged_score)
+  bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
   unsigned long long* host_counters = nullptr;   // pinned
   SArgs* ring = nullptr;                          // pinned argument snapshots
   ~StagedState() {
@@ -627,7 +808,10 @@ StagedState* staged_create(int device) {
 
 void staged_destroy(StagedState* st) { delete st; }
 
-void staged_set_lds(StagedState* st, int64_t bytes) { st->dec_lds = bytes; }
+void staged_set_lds(StagedState* st, int64_t bytes) {
+  st->dec_lds = bytes;
+  st->dec_lds_fixed = true;
+}
 
 #define ST_TRY(x)                                                                        \
   do {                                                                                   \
@@ -756,6 +940,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->leaf_seg.ensure(T1 * 4)); ST_TRY(st->leaf_val.ensure(T1 * 8));
   ST_TRY(st->seg_rec.ensure(A1 * 16)); ST_TRY(st->seg_cg.ensure(A1 * 8));
   ST_TRY(st->crank_first.ensure(((size_t)N + 1) * 4));
+  ST_TRY(st->lmax.ensure((size_t)std::max<int64_t>(NL, 1) * 8));
+  ST_TRY(st->c_gu.ensure((size_t)N * 4)); ST_TRY(st->c_umask.ensure((size_t)N * 8));
+  ST_TRY(st->c_best.ensure((size_t)N * 8)); ST_TRY(st->c_bestcl.ensure((size_t)N * 4));
+  ST_TRY(st->c_nopt.ensure((size_t)N * 4));
+  ST_TRY(st->run_crit.ensure(A1 * 8)); ST_TRY(st->run_rank.ensure(A1 * 8));
   ST_TRY(st->satt_lohi.ensure(A1 * 8)); ST_TRY(st->satt_sc.ensure(A1 * 8));
   ST_TRY(st->act0.ensure((size_t)N * 4)); ST_TRY(st->act1.ensure((size_t)N * 4));
   ST_TRY(st->base0.ensure((size_t)N * 8)); ST_TRY(st->base1.ensure((size_t)N * 8));
@@ -787,6 +976,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   sa.seg_rec = st->seg_rec.as<int4>();
   sa.seg_cg = st->seg_cg.as<int2>();
   sa.crank_first = st->crank_first.as<int32_t>();
+  sa.lmax = st->lmax.as<uint64_t>();
+  sa.c_gu = st->c_gu.as<int32_t>(); sa.c_umask = st->c_umask.as<uint64_t>();
+  sa.c_best = st->c_best.as<unsigned long long>(); sa.c_bestcl = st->c_bestcl.as<int32_t>();
+  sa.c_nopt = st->c_nopt.as<int32_t>();
+  sa.run_crit = st->run_crit.as<double>(); sa.run_rank = st->run_rank.as<double>();
   sa.satt_lohi = st->satt_lohi.as<int2>(); sa.satt_sc = st->satt_sc.as<double>();
   sa.annot_best = st->annot_best.as<uint64_t>();
   sa.big_list = st->big_list.as<int32_t>();
@@ -803,6 +997,13 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   }
   ST_TRY(hipGetLastError());
 
+  // flat explain_one applies to --weak-loci ignore/penalize and <= 64 loci per contig
+  // (WF_FLAT_ONE=0 forces the per-contig workgroup form; measurement aid)
+  // (WF_FLAT_ONE=1 selects it; by default explain_one runs in the per-contig workgroup,
+  // which measured faster on cfg2/cfg3 once its arena is sized to the data)
+  static const char* flat_env = getenv("WF_FLAT_ONE");
+  const bool flat_one = k.p.weak != 2 && max_loci <= 64 && flat_env && flat_env[0] == '1';
+  if (const char* dl = getenv("WF_DEC_LDS")) { st->dec_lds = atoll(dl); st->dec_lds_fixed = true; }
   // roll-up levels
   Buf* act[2] = {&st->act0, &st->act1};
   Buf* base[2] = {&st->base0, &st->base1};
@@ -867,7 +1068,17 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       ST_TRY(attr2);
     }
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
-    hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
+    if (flat_one) {
+      ST_TRY(hipMemsetAsync(sa.lmax, 0, (size_t)std::max<int64_t>(NL, 1) * 8, s));
+      hipLaunchKernelGGL(k_flat_maxes, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
+      hipLaunchKernelGGL(k_flat_prep, dim3(grid_for(n_act)), dim3(256), 0, s, dsa, n_act, level);
+      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys, 0);
+      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys, 1);
+      hipLaunchKernelGGL(k_flat_finish, dim3(grid_for(n_act)), dim3(256), 0, s, dsa, n_act, level, n_keys);
+    } else {
+      hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, dsa, n_act,
+                         level, n_keys);
+    }
     // explain_two for the contigs phase 1 left open (count on the device: a grid of
     // rank-independent size, idle blocks exit at once)
     hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * 4)), dim3(kDecNT),
@@ -890,6 +1101,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
                             hipMemcpyDeviceToHost, s));
       ST_TRY(hipStreamSynchronize(s));
     }
+    if (level == 0 && !st->dec_lds_fixed && n_big * 50 > n_act && st->dec_lds < 48 * 1024)
+      st->dec_lds += 8 * 1024;   // adaptive arena: grows while > 2% of contigs overflow
     n_act = (int)st->host_counters[0];
     n_keys = (int64_t)st->host_counters[1];
   }
