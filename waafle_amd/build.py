@@ -1,4 +1,5 @@
-"""Build libwaafle_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+"""Build libwaafle_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU), and the
+host-only native ingest library libwaafle_ingest.so (g++).
 
     python -m waafle_amd.build            # or __graft_entry__.build()
 """
@@ -37,6 +38,27 @@ def up_to_date(lib=LIB):
     return all(os.path.getmtime(d) <= t for d in DEPS)
 
 
+INGEST_LIB = os.path.join(HERE, "libwaafle_ingest.so")
+INGEST_SOURCES = [os.path.join(CSRC, "wf_ingest.cpp")]
+INGEST_DEPS = INGEST_SOURCES + [os.path.join(REPO, "include", "waafle_ingest.h")]
+
+
+def build_ingest(force=False, verbose=True):
+    """Host-only C++ (no HIP): the multi-threaded FASTA/BLAST/GFF parser."""
+    lib = INGEST_LIB
+    if not force and os.path.exists(lib) and all(
+            os.path.getmtime(d) <= os.path.getmtime(lib) for d in INGEST_DEPS):
+        return lib
+    cxx = os.environ.get("CXX", "g++")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-Wall", "-Wextra",
+           "-I" + os.path.join(REPO, "include")] + INGEST_SOURCES + ["-o", lib + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(lib + ".tmp", lib)
+    return lib
+
+
 def build(force=False, verbose=True, stamps=False, defines=(), out=None):
     """Build the product library (or, with stamps=True, the per-phase timing variant;
     `defines` + `out` build an experimental variant for sweeps)."""
@@ -60,5 +82,6 @@ if __name__ == "__main__":
                   out=os.path.join(HERE, "libwaafle_hip_{}.so".format(name)))
             sys.exit(0)
     build(force="--force" in sys.argv)
+    build_ingest(force="--force" in sys.argv)
     if "--stamps" in sys.argv:
         build(force="--force" in sys.argv, stamps=True)

@@ -76,8 +76,8 @@ int ensure(wf_ctx* ctx, DevBuf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.bytes >= bytes) return WF_OK;
   if (b.p) {
-    hipStreamSynchronize(ctx->stream);
-    hipFree(b.p);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
   }
@@ -94,7 +94,7 @@ int ensure(wf_ctx* ctx, DevBuf& b, size_t bytes) {
 }
 
 void release(DevBuf& b) {
-  if (b.p) hipFree(b.p);
+  if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.bytes = 0;
 }
@@ -217,8 +217,8 @@ int wf_init(int device, wf_ctx** out) {
 
 void wf_free(wf_ctx* ctx) {
   if (!ctx) return;
-  hipSetDevice(ctx->device);
-  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->ovf_list,
                     &ctx->ovf2_list, &ctx->kargs,
                     &ctx->ovf_count, &ctx->retry_list, &ctx->retry_count, &ctx->big_ws,
@@ -230,8 +230,8 @@ void wf_free(wf_ctx* ctx) {
                     &ctx->r_pairs, &ctx->r_status, &ctx->r_need};
   for (DevBuf* b : bufs) release(*b);
   if (ctx->staged) wf::staged_destroy(ctx->staged);
-  for (hipEvent_t ev : ctx->ev_pool) hipEventDestroy(ev);
-  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  for (hipEvent_t ev : ctx->ev_pool) (void)hipEventDestroy(ev);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
 
@@ -289,7 +289,7 @@ int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* t) {
     if (i == t->root ? t->depth[i] != 0 : t->depth[i] != t->depth[p] + 1)
       return fail(ctx, WF_E_BADINPUT, "depth inconsistent with parent at %d", i);
   }
-  hipSetDevice(ctx->device);
+  (void)hipSetDevice(ctx->device);
   const int32_t *dp, *dd, *ds;
   const int64_t* dl;
   int rc;
@@ -549,9 +549,9 @@ int wf_synchronize(wf_ctx* ctx) {
 
 int wf_timing_enable(wf_ctx* ctx, int on) {
   if (!ctx) return WF_E_BADINPUT;
-  hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
-  for (hipEvent_t ev : ctx->ev_pool) hipEventDestroy(ev);
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (hipEvent_t ev : ctx->ev_pool) (void)hipEventDestroy(ev);
   ctx->ev_pool.clear();
   ctx->ev_lds.clear();
   ctx->ev_big.clear();

@@ -315,46 +315,62 @@ __device__ double serial_block(int o, int l, F f) {
   return res;
 }
 
+// numpy's pairwise sum of one buffer (<= 8192 elements) by one thread: the leaves in
+// order (the walk of gen_leaves, frame stack in shift registers so nothing spills to
+// scratch), each folded onto a SumStack with its completed parent additions.
 template <class F>
 __device__ double serial_pairwise(int off0, int cl, F f) {
   if (cl <= kLeafMax) return serial_block(off0, cl, f);
-  int foff[16], flen[16], fst[16];
-  double facc[16];
+  int so[8], sl[8], ss[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { so[i] = 0; sl[i] = 0; ss[i] = 0; }
+  auto push = [&](int o, int l) {
+#pragma unroll
+    for (int i = 7; i > 0; --i) { so[i] = so[i - 1]; sl[i] = sl[i - 1]; ss[i] = ss[i - 1]; }
+    so[0] = o; sl[0] = l; ss[0] = 0;
+  };
+  auto pop = [&]() {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) { so[i] = so[i + 1]; sl[i] = sl[i + 1]; ss[i] = ss[i + 1]; }
+  };
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0, a4 = 0.0, a5 = 0.0, a6 = 0.0, a7 = 0.0;
   int sp = 1;
-  foff[0] = off0; flen[0] = cl; fst[0] = 0;
-  for (;;) {
-    int t = sp - 1;
-    if (flen[t] > kLeafMax && fst[t] == 0) {
-      int h = flen[t] / 2;
+  so[0] = off0; sl[0] = cl;
+  while (sp > 0) {
+    if (sl[0] > kLeafMax && ss[0] == 0) {
+      int h = sl[0] / 2;
       h -= h % 8;
-      fst[t] = 1;
-      foff[sp] = foff[t]; flen[sp] = h; fst[sp] = 0;
+      ss[0] = 1;
+      push(so[0], h);
       ++sp;
       continue;
     }
-    double val = serial_block(foff[t], flen[t], f);
+    const double v = serial_block(so[0], sl[0], f);
+    a7 = a6; a6 = a5; a5 = a4; a4 = a3; a3 = a2; a2 = a1; a1 = a0; a0 = v;
+    pop();
     --sp;
-    for (;;) {
-      if (sp == 0) return val;
-      int u = sp - 1;
-      if (fst[u] == 1) {
-        int h = flen[u] / 2;
+    while (sp > 0) {
+      if (ss[0] == 1) {
+        int h = sl[0] / 2;
         h -= h % 8;
-        facc[u] = val;
-        fst[u] = 2;
-        foff[sp] = foff[u] + h; flen[sp] = flen[u] - h; fst[sp] = 0;
+        ss[0] = 2;
+        push(so[0] + h, sl[0] - h);
         ++sp;
         break;
       }
-      val = facc[u] + val;
+      a0 = a1 + a0;                          // (left) + (right)
+      a1 = a2; a2 = a3; a3 = a4; a4 = a5; a5 = a6; a6 = a7;
+      pop();
       --sp;
     }
   }
+  return a0;
 }
 
-// np.add.reduce over f(0..n) (one thread).
+// np.add.reduce over f(0..n) (one thread): 8192-element buffers added from 0.0.
 template <class F>
-__device__ double np_sum(int n, F f) {
+__device__ __forceinline__ double np_sum(int n, F f) {
+  if (n <= kLeafMax) return 0.0 + serial_block(0, n, f);   // one leaf (n = 0: 0.0)
   double total = 0.0;
   for (int o = 0; o < n; o += kNpyBuf) total += serial_pairwise(o, min(kNpyBuf, n - o), f);
   return total;

@@ -9,7 +9,7 @@
 //   per level   k_keys_*                       (contig rank, clade, locus) keys
 //               device radix sort              -> segments = equal keys (:394-406)
 //               k_seg_flags + scan + k_segs    segment boundaries
-//               k_seg_mean                     thread per segment: exact numpy mean
+//               k_leaf + k_seg_combine         lane per numpy leaf, thread per segment: exact mean
 //               k_decide / k_decide_big        workgroup per contig: maxes, weak loci,
 //                                              explain_one/two, melds, LGT filters
 //                                              (decide_level, shared with the fused form);

@@ -265,9 +265,26 @@ def split_sseqids(sseqids):
 # ---------------------------------------------------------------------------
 
 def load_inputs(contigs_path, blastout_path, gff_path, taxonomy_path, min_gene_length,
-                warn=say):
-    """Parse all inputs -> (HostBatch, TaxonomyTables)."""
+                warn=say, native=None, threads=0):
+    """Parse all inputs -> (HostBatch, TaxonomyTables).
+
+    native (default: on unless WF_INGEST=python): parse with libwaafle_ingest.so
+    (multi-threaded C++); inputs it does not take in its plain form go to the Python
+    reader below, which gives the reference's result or error."""
     edges = read_edges(taxonomy_path)
+    if native is None:
+        native = os.environ.get("WF_INGEST", "native") != "python"
+    if native:
+        from . import ingest
+        try:
+            return ingest.parse(contigs_path, blastout_path, gff_path, edges, min_gene_length,
+                                threads=threads, warn=warn)
+        except ingest.Fallback:
+            pass
+    return _load_python(contigs_path, blastout_path, gff_path, edges, min_gene_length, warn)
+
+
+def _load_python(contigs_path, blastout_path, gff_path, edges, min_gene_length, warn):
     lengths = read_contig_lengths(contigs_path)
     names = list(lengths)
     index = {n: i for i, n in enumerate(names)}
