@@ -65,6 +65,8 @@ struct SArgs {
   unsigned long long* counters;  // [0] next active, [1] next attachments, [2] big count
   int32_t* big_list;             // contigs whose decision state needs an HBM slot
   int32_t* two_list;             // (rank, contig) pairs that need explain_two (counters[5])
+  int32_t* one_list;             // (rank, contig) pairs for the dense explain_one workgroup
+                                 // (counters[6]); null: every active contig goes there
   int32_t* seg_nleaf;            // [segments + 1] numpy leaves per segment
   int32_t* leaf_off;             // [segments + 1] exclusive scan of seg_nleaf
   int32_t* leaf_seg;             // [leaves] segment of each leaf

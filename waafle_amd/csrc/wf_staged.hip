@@ -556,6 +556,150 @@ __global__ void k_flat_finish(const SArgs* __restrict__ sp, int n_act, int level
   K.pair_evals[c] = level == 0 ? 0 : K.pair_evals[c];
 }
 
+// ---- explain_one, one wave per contig (orgscorer.py:407-429, 585-597, 621-631) ---------
+// The common case needs no gene-score matrix: the contig's segments (sorted by clade, then
+// locus) are staged in LDS, per-locus maxes are LDS atomics, and each clade run scores
+// itself (crit = min, rank = numpy-order mean over the unmasked loci, zeros where the clade
+// has no segment).  The best option is a wave argmax by (rank, larger clade id) -- the
+// sorted-order tie policy of decide_one -- and the winner's synteny is 'A' on every unmasked
+// locus ('~' elsewhere), since its crit >= k1.  Contigs with more segments than the stage
+// holds, more than 64 loci or --weak-loci assign-unknown (virtual "Unknown" row) go to the
+// dense workgroup (k_decide<1>); contigs without a one-clade option go to explain_two.
+constexpr int kOneCap = 384;
+
+__global__ __launch_bounds__(64) void k_one(const SArgs* __restrict__ sp, int n_act, int level,
+                                            int64_t n_keys) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const DevParams& P = K.p;
+  __shared__ int2 s_cg[kOneCap];
+  __shared__ double s_v[kOneCap];
+  __shared__ double s_rank[kOneCap];     // rank of the option whose clade run starts here, or -1
+  __shared__ int s_mem[kOneCap];
+  __shared__ unsigned long long s_max[64];
+  __shared__ int s_cnt;
+  const int lane = threadIdx.x;
+  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const int c = S.act ? S.act[cr] : cr;
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    const int64_t h0 = K.hit_off[c];
+    if (K.hit_off[c + 1] == h0 || G == 0) continue;       // never evaluated (orgscorer.py:959)
+    const int so = n_keys > 0 ? S.crank_first[cr] : 0;
+    const int ns = (n_keys > 0 ? S.crank_first[cr + 1] : 0) - so;
+    if (ns > kOneCap || G > 64 || P.weak == 2) {
+      if (lane == 0) {
+        const int slot = (int)atomicAdd(&S.counters[6], 1ull);
+        S.one_list[2 * slot] = cr;
+        S.one_list[2 * slot + 1] = c;
+      }
+      continue;
+    }
+    for (int t = lane; t < ns; t += 64) {
+      s_cg[t] = S.seg_cg[so + t];
+      s_v[t] = S.seg_mean[so + t];
+    }
+    s_max[lane] = 0;
+    __syncthreads();
+    // per-locus max over known clades (:407-411)
+    for (int t = lane; t < ns; t += 64) {
+      const int2 cg = s_cg[t];
+      const double v = s_v[t];
+      if (cg.x != K.unknown && v > 0.0) atomicMax(&s_max[cg.y], dbits(v));
+    }
+    __syncthreads();
+    // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
+    const double mx = __longlong_as_double((long long)s_max[lane]);
+    const uint64_t um = __ballot(lane < G && (P.weak != 0 || mx >= P.kmin));
+    const int Gu = __popcll(um);
+    if (Gu == 0) {
+      if (level > 0 && lane == 0) {                       // np.min of an empty array upstream
+        K.iters[c] = (int16_t)min(level + 1, 32767);
+        K.status[c] = WF_E_EMPTYMASK;
+      }                                                   // level 0: skipped contig (:959)
+      continue;
+    }
+    // Contig.score of every clade run (:447-461); options have crit >= k1 (:585-597)
+    double br = -__builtin_inf(), bcrit = 0.0;
+    long long bk = -1;
+    for (int t = lane; t < ns; t += 64) {
+      double rk = -1.0;
+      const int clade = s_cg[t].x;
+      if (t == 0 || s_cg[t - 1].x != clade) {
+        uint64_t m = um;
+        int q = t;
+        double crit = 0.0;
+        bool firstv = true;
+        auto next = [&]() -> double {
+          const int g = __builtin_ctzll(m);
+          m &= m - 1;
+          while (q < ns && s_cg[q].x == clade && s_cg[q].y < g) ++q;
+          const double v = (q < ns && s_cg[q].x == clade && s_cg[q].y == g) ? s_v[q] : 0.0;
+          crit = (firstv || v < crit) ? v : crit;
+          firstv = false;
+          return v;
+        };
+        const double rank = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+        if (crit >= P.k1) {
+          rk = rank;
+          if (better(rank, clade, br, bk)) { br = rank; bk = clade; bcrit = crit; }
+        }
+      }
+      s_rank[t] = rk;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double r2 = __shfl_xor(br, off, 64), c2 = __shfl_xor(bcrit, off, 64);
+      const long long k2 = __shfl_xor(bk, off, 64);
+      if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
+    }
+    if (bk < 0) {                                          // explain_two (:570)
+      if (lane == 0) {
+        const int slot = (int)atomicAdd(&S.counters[5], 1ull);
+        S.two_list[2 * slot] = cr;
+        S.two_list[2 * slot + 1] = c;
+      }
+      continue;
+    }
+    // meld_one (:621-631): options within --range of the best
+    if (lane == 0) s_cnt = 0;
+    __syncthreads();
+    if (P.dis1 == 1)
+      for (int t = lane; t < ns; t += 64) {
+        const double rk = s_rank[t];
+        if (rk >= 0.0 && (br - rk) <= P.range) s_mem[atomicAdd(&s_cnt, 1)] = s_cg[t].x;
+      }
+    __syncthreads();
+    const int nm = s_cnt;
+    if (P.dis1 == 1 && nm == 0) {                          // negative --range upstream crash
+      if (lane == 0) K.status[c] = WF_E_BADINPUT;
+      continue;
+    }
+    int lca = (int)bk;
+    if (P.dis1 == 1) {
+      int acc = -1;
+      for (int i = lane; i < nm; i += 64) acc = lca2(K, acc, s_mem[i]);
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) acc = lca2(K, acc, __shfl_xor(acc, off, 64));
+      lca = acc;
+    }
+    const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
+    for (int i = lane; i < nm; i += 64) K.meld[mbase + i] = s_mem[i];
+    if (lane < G) K.syn[l0 + lane] = ((um >> lane) & 1ull) ? 'A' : '~';   // set_synteny_one
+    if (lane == 0) {
+      K.call[c] = WF_CALL_NO_LGT;
+      K.crit[c] = bcrit;
+      K.rank[c] = br;
+      K.c1[c] = lca;
+      K.c2[c] = -1;
+      K.nm1[c] = nm;
+      K.iters[c] = (int16_t)(level + 1);
+      if (level == 0) K.pair_evals[c] = 0;
+    }
+    __syncthreads();                                       // LDS reuse by the next contig
+  }
+}
+
 // Decision workgroup for one contig at one level.  Builds the gene-score matrix of the
 // level (rows = clades in id order, the virtual "Unknown" row of --weak-loci
 // assign-unknown included) from the contig's segments, then runs decide_level.
@@ -711,10 +855,11 @@ __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs* __restrict__ 
   const SArgs& S = *sp;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
-  const int count = PHASE == 1 ? n_act : (int)S.counters[5];
+  const int32_t* list = PHASE == 1 ? S.one_list : S.two_list;
+  const int count = PHASE == 1 ? (list ? (int)S.counters[6] : n_act) : (int)S.counters[5];
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
-    const int cr = PHASE == 1 ? i : S.two_list[2 * i];
-    const int c = PHASE == 1 ? (S.act ? S.act[cr] : cr) : S.two_list[2 * i + 1];
+    const int cr = list ? list[2 * i] : i;
+    const int c = list ? list[2 * i + 1] : (S.act ? S.act[cr] : cr);
     const bool ok = decide_contig<kDecNT, PHASE>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
     if (!ok && threadIdx.x == 0) {
       const int slot = (int)atomicAdd(&S.counters[2], 1ull);
@@ -784,7 +929,7 @@ struct StagedState {
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
   Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc;
   Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
-  Buf act0, act1, base0, base1, big_list, two_list, big_ws, tmp;
+  Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp;
   bool lut_ready = false;
   int64_t dec_lds = 24 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
@@ -950,6 +1095,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->base0.ensure((size_t)N * 8)); ST_TRY(st->base1.ensure((size_t)N * 8));
   ST_TRY(st->big_list.ensure((size_t)N * 8));
   ST_TRY(st->two_list.ensure((size_t)N * 8));
+  ST_TRY(st->one_list.ensure((size_t)N * 8));
   const int64_t n_annot = NL * k.n_sys;
   if (n_annot > 0) ST_TRY(st->annot_best.ensure((size_t)n_annot * 8));
   {
@@ -1004,10 +1150,17 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   static const char* flat_env = getenv("WF_FLAT_ONE");
   const bool flat_one = k.p.weak != 2 && max_loci <= 64 && flat_env && flat_env[0] == '1';
   if (const char* dl = getenv("WF_DEC_LDS")) { st->dec_lds = atoll(dl); st->dec_lds_fixed = true; }
+  // explain_one by one wave per contig (k_one), the dense workgroup only for the contigs it
+  // hands over (WF_ONE_FAST=0: dense workgroup for every contig; measurement aid)
+  static const char* one_env = getenv("WF_ONE_FAST");
+  const bool one_fast = !flat_one && !(one_env && one_env[0] == '0');
+  sa.one_list = one_fast ? st->one_list.as<int32_t>() : nullptr;
   // roll-up levels
   Buf* act[2] = {&st->act0, &st->act1};
   Buf* base[2] = {&st->base0, &st->base1};
-  const unsigned persistent = (unsigned)st->cus * 8;
+  // k_leaf grid: blocks per CU (WF_LEAF_GRID overrides; measurement aid)
+  static const char* lg_env = getenv("WF_LEAF_GRID");
+  const unsigned persistent = (unsigned)st->cus * (lg_env ? (unsigned)atoi(lg_env) : 8u);
   int n_act = N;
   int64_t n_keys = A;
   for (int level = 0; n_act > 0; ++level) {
@@ -1075,6 +1228,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys, 0);
       hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys, 1);
       hipLaunchKernelGGL(k_flat_finish, dim3(grid_for(n_act)), dim3(256), 0, s, dsa, n_act, level, n_keys);
+    } else if (one_fast) {
+      hipLaunchKernelGGL(k_one, dim3(std::min<int64_t>(n_act, (int64_t)st->cus * 32)), dim3(64), 0, s, dsa,
+                         n_act, level, n_keys);
+      hipLaunchKernelGGL(k_decide<1>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * 4)), dim3(kDecNT),
+                         (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
     } else {
       hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, dsa, n_act,
                          level, n_keys);
