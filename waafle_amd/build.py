@@ -66,10 +66,25 @@ def build(force=False, verbose=True, stamps=False, defines=(), out=None):
     if not force and up_to_date(lib):
         return lib
     extra = (["-DWF_STAMPS"] if stamps else []) + ["-D" + d for d in defines]
-    cmd = [hipcc()] + FLAGS + extra + SOURCES + ["-o", lib + ".tmp"]
+    # one compile per source, in parallel, then a link step
+    cflags = [f for f in FLAGS if f != "-shared"]
+    objs, procs = [], []
+    for src in SOURCES:
+        obj = "{}.{}.o".format(lib, os.path.splitext(os.path.basename(src))[0])
+        cmd = [hipcc()] + cflags + extra + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append(subprocess.Popen(cmd))
+        objs.append(obj)
+    rcs = [p.wait() for p in procs]
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), "hipcc -c")
+    cmd = [hipcc()] + FLAGS + objs + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
+    for o in objs:
+        os.remove(o)
     os.replace(lib + ".tmp", lib)
     return lib
 

@@ -25,7 +25,8 @@ struct wf_ctx {
   std::string err;
   // taxonomy
   int32_t tax_n = 0, root = -1, unknown = -1;
-  DevBuf parent, depth, sibp, leaves;
+  DevBuf parent, depth, sibp, leaves, lin;
+  bool have_lin = false;
   // overflow work list + counter
   DevBuf ovf_list, ovf2_list, ovf_count;
   DevBuf retry_list, retry_count;
@@ -219,7 +220,7 @@ void wf_free(wf_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->ovf_list,
+  DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->lin, &ctx->ovf_list,
                     &ctx->ovf2_list, &ctx->kargs,
                     &ctx->ovf_count, &ctx->retry_list, &ctx->retry_count, &ctx->big_ws,
                     &ctx->b_hit_off, &ctx->b_qlo, &ctx->b_qhi, &ctx->b_taxon, &ctx->b_hstrand,
@@ -298,6 +299,26 @@ int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* t) {
       (rc = upload(ctx, ctx->sibp, t->sib_parent, t->n, &ds)) ||
       (rc = upload(ctx, ctx->leaves, t->leaf_count, t->n, &dl)))
     return rc;
+  // lineage rows (utils.py:392-399 as a table): LCA becomes one row compare instead of a
+  // parent walk of dependent loads
+  int32_t max_depth = 0;
+  for (int32_t i = 0; i < t->n; ++i) max_depth = std::max(max_depth, t->depth[i]);
+  ctx->have_lin = max_depth < wf::kLin;
+  if (ctx->have_lin) {
+    std::vector<int32_t> lin((size_t)t->n * wf::kLin, -1);
+    std::vector<int32_t> order(t->n);
+    for (int32_t i = 0; i < t->n; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int32_t a, int32_t b) { return t->depth[a] < t->depth[b]; });
+    for (int32_t i : order) {
+      int32_t* row = &lin[(size_t)i * wf::kLin];
+      if (i != t->root) std::copy_n(&lin[(size_t)t->parent[i] * wf::kLin], wf::kLin, row);
+      row[t->depth[i]] = i;
+    }
+    const int32_t* dlin;
+    if ((rc = upload(ctx, ctx->lin, lin.data(), (int64_t)lin.size(), &dlin))) return rc;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));   // `lin` is a pageable local
+  }
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   ctx->tax_n = t->n;
   ctx->root = t->root;
@@ -436,6 +457,7 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
   K.depth = static_cast<const int32_t*>(ctx->depth.p);
   K.sibp = static_cast<const int32_t*>(ctx->sibp.p);
   K.leaves = static_cast<const int64_t*>(ctx->leaves.p);
+  K.lin = ctx->have_lin ? static_cast<const int32_t*>(ctx->lin.p) : nullptr;
   K.p = derive_params(*p);
   const int64_t N = b->n_contigs, NH = b->n_hits, NL = b->n_loci;
   const int64_t n_meld = 2 * NH + 2 * N, n_annot = NL * b->n_systems;

@@ -198,6 +198,25 @@ __device__ __forceinline__ void bitonic_sort(T* keys, int n) {
 __device__ __forceinline__ int lca2(const KArgs& K, int a, int b) {
   if (a < 0) return b;
   if (b < 0) return a;
+  if (a == b) return a;
+  if (K.lin) {
+    // lineage rows agree on a prefix (root first); the LCA is the deepest common entry.
+    // Two independent 64-B row loads instead of a walk of dependent parent loads.
+    const int4* ra = reinterpret_cast<const int4*>(K.lin + (int64_t)a * kLin);
+    const int4* rb = reinterpret_cast<const int4*>(K.lin + (int64_t)b * kLin);
+    int4 x[kLin / 4], y[kLin / 4];
+#pragma unroll
+    for (int i = 0; i < kLin / 4; ++i) { x[i] = ra[i]; y[i] = rb[i]; }
+    int r = x[0].x;                                    // the root (depth 0)
+#pragma unroll
+    for (int i = 0; i < kLin / 4; ++i) {
+      if (x[i].x >= 0 && x[i].x == y[i].x) r = x[i].x;
+      if (x[i].y >= 0 && x[i].y == y[i].y) r = x[i].y;
+      if (x[i].z >= 0 && x[i].z == y[i].z) r = x[i].z;
+      if (x[i].w >= 0 && x[i].w == y[i].w) r = x[i].w;
+    }
+    return r;
+  }
   int da = K.depth[a], db = K.depth[b];
   while (da > db) { a = K.parent[a]; --da; }
   while (db > da) { b = K.parent[b]; --db; }
@@ -402,6 +421,8 @@ struct Contig {
   char* xws = nullptr;                    // optional scratch for mask classes (explain_two)
   int64_t xcap = 0;
   int* sib_of = nullptr;                  // [Pn] listed parent of each clade (sister checks)
+  uint64_t* hm = nullptr;                 // [Pn] loci where the clade scores >= the sister
+                                          // threshold (G <= 64; null: per-locus scan)
 };
 
 // Shift-register stack of partial sums for numpy's pairwise tree.  Static indexing keeps
@@ -612,17 +633,109 @@ struct SegAttT {
     out = add_tail(C, st, ln, body);
     return true;
   }
+  // All eight stride accumulators of the body [st, st+8m) in one pass over the envelope's
+  // runs: a run [x, nx) of value v adds v k_c times to accumulator c, where k_c (its sites
+  // of residue c) is kmin or kmin + 1.  Each accumulator still adds its own sites in site
+  // order, so the sums are those of stride_sum(); the runs are found once, not per c, and
+  // the eight independent chains interleave.
+  template <bool REG>
+  __device__ __forceinline__ double runs_body(const Src& C, int st, int m) const {
+    const int be = st + (m << 3), na = REG ? kRegAtt : ke - kb;
+    double r[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r[c] = 0.0;
+    for (int x = st; x < be;) {
+      double v = 0.0;
+      int nx = be;
+#pragma unroll
+      for (int i = 0; i < na; ++i) {
+        int l, h; double s;
+        att<REG>(C, i, l, h, s);
+        if (l < h) {
+          if (l <= x && x < h) { v = s > v ? s : v; nx = min(nx, h); }
+          else if (l > x) nx = min(nx, l);
+        }
+      }
+      if (v > 0.0) {
+        int k[8], kmin = m;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          k[c] = below(st + c, nx, m) - below(st + c, x, m);
+          kmin = min(kmin, k[c]);
+        }
+        for (int q = 0; q < kmin; ++q) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) r[c] += v;
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (k[c] > kmin) r[c] += v;
+      }
+      x = nx;
+    }
+    return leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+  }
   // Leaf value by one thread (serial path).
   __device__ __forceinline__ double leaf(const Src& C, int st, int ln) const {
     double v;
     if (leaf_fast(C, st, ln, v)) return v;
     const int m = ln >> 3;
-    double r[8];
+    const double body = reg ? runs_body<true>(C, st, m) : runs_body<false>(C, st, m);
+    return add_tail(C, st, ln, body);
+  }
+  // Whole leaf [st, st+ln) under one envelope value F (no higher attachment reaches into
+  // it): its value depends on (F, ln) only.  Register attachments only.
+  __device__ __forceinline__ bool leaf_const(int st, int ln, double& F) const {
+    const int le = st + ln;
+    F = 0.0;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) r[c] = stride_sum(C, st, m, c);
-    return add_tail(C, st, ln, leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]));
+    for (int i = 0; i < kRegAtt; ++i)
+      if (lo[i] < hi[i] && lo[i] <= st && le <= hi[i]) F = sc[i] > F ? sc[i] : F;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < kRegAtt; ++i)
+      if (lo[i] < hi[i] && lo[i] < le && hi[i] > st && !(lo[i] <= st && le <= hi[i]) && sc[i] > F)
+        ok = false;
+    return ok;
   }
 };
+
+// Value of a leaf of ln sites that all hold F (numpy's block: 8 accumulators over the
+// body, tree, then the tail in order).
+__device__ __forceinline__ double const_leaf_value(double F, int ln) {
+  if (!(F > 0.0)) return 0.0;
+  const int m = ln >> 3;
+  double res = m > 0 ? 8.0 * seqsum(F, m) : 0.0;
+  for (int x = m << 3; x < ln; ++x) res += F;
+  return res;
+}
+
+// Exact np.mean of one short segment (one buffer, register attachments) by one thread:
+// leaves from the length's table in tree order on a register stack.  Leaves under a single
+// envelope value reuse the last such leaf's value when (F, length) repeat -- the usual
+// case: a hit covering the locus makes every leaf constant, in <= 3 distinct lengths.
+template <class Src>
+__device__ __forceinline__ double seg_mean_thread(const SegAttT<Src>& at, const Src& src,
+                                                  const int4* lt, int nl, int len) {
+  SumStack stk;
+  double mF = -1.0, mv = 0.0;
+  int mln = -1;
+  int4 e = lt[0];
+  for (int q = 0; q < nl; ++q) {
+    const int4 cur = e;
+    if (q + 1 < nl) e = lt[q + 1];                 // next leaf's entry in flight
+    double F, v;
+    if (at.leaf_const(cur.x, cur.y, F)) {
+      if (F != mF || cur.y != mln) { mv = const_leaf_value(F, cur.y); mF = F; mln = cur.y; }
+      v = mv;
+    } else {
+      v = at.leaf(src, cur.x, cur.y);
+    }
+    stk.push(v);
+    for (int a = 0; a < cur.z; ++a) stk.add_top();
+  }
+  return (0.0 + stk.s0) / (double)len;
+}
 using SegAtt = SegAttT<KeySrc>;
 
 // Exact np.mean of one (clade, locus) site array (orgscorer.py:399-406) by one thread:
@@ -932,6 +1045,7 @@ __device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int
     return c;
   };
   int state = 0, nA = 0, nB = 0;
+  uint64_t mA = 0, mB = 0;       // loci with synteny A / B (sister masks, G <= 64)
   bool dir_ok = true;
   int64_t tot = 0, amb = 0;
   e.same = 1;
@@ -940,8 +1054,8 @@ __device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int
     if (out) out[g] = c;
     if (best && best[g] != c) e.same = 0;
     const int len = C.loc_len[g];
-    if (c == 'A') { ++nA; tot += len; }
-    else if (c == 'B') { ++nB; tot += len; }
+    if (c == 'A') { ++nA; tot += len; mA |= 1ull << (g & 63); }
+    else if (c == 'B') { ++nB; tot += len; mB |= 1ull << (g & 63); }
     else if (c == '*') { tot += len; amb += len; }
     if (c != '~') {  // "^A+B+A+$" on synteny without '~' (orgscorer.py:542)
       if (state == 0) { if (c == 'A') state = 1; else dir_ok = false; }
@@ -966,7 +1080,21 @@ __device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int
   }
   // check_sister_penalty (:717-744): fail iff a checked locus has a present sister clade
   // (other than the pair) scoring >= threshold there
-  if (P.sister_on && e.ok) {
+  if (P.sister_on && e.ok && C.hm) {
+    // per-clade threshold masks: one pass over the clades instead of one per locus
+    const int px = K.parent[X], py = K.parent[Y];
+    uint64_t fa = 0, fb = 0;
+    for (int q = 0; q < Pcount; ++q) {
+      const int sp = C.sib_of[q];
+      if (sp != px && sp != py) continue;
+      const int s = C.cl_id[q];
+      if (s == X || s == Y) continue;
+      const uint64_t h = C.hm[q];
+      if (sp == px) fb |= h;
+      if (sp == py) fa |= h;
+    }
+    if ((fb & mB) || (!e.dir && (fa & mA))) e.ok = 0;
+  } else if (P.sister_on && e.ok) {
     const int px = K.parent[X], py = K.parent[Y];
     for (int g = 0; g < G && e.ok; ++g) {
       uint8_t c = fin(g);
@@ -1151,7 +1279,16 @@ __device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& 
   const int Gu = ctl.Gu;
   (void)w; (void)NW;
   if (P.sister_on) {                     // sister checks read listed parents per clade
-    for (int q = tid; q < Pn; q += NT) C.sib_of[q] = K.sibp[C.cl_id[q]];
+    for (int q = tid; q < Pn; q += NT) {
+      C.sib_of[q] = K.sibp[C.cl_id[q]];
+      if (C.hm) {
+        const double* row = C.S + (int64_t)q * G;
+        uint64_t m = 0;
+        for (int g = 0; g < G; ++g)
+          if (row[g] >= P.sister_thr) m |= 1ull << g;
+        C.hm[q] = m;
+      }
+    }
     __syncthreads();
   }
   // ================= explain_two (orgscorer.py:599-619) ============================

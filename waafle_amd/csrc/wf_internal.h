@@ -15,6 +15,7 @@ constexpr int kNpyBuf = 8192;           // numpy reduction buffer (NPY_BUFSIZE)
 constexpr int kLeafSlots = 160;         // >= leaves of one 8192-element buffer
 constexpr int kMaxIter = 100;           // orgscorer.py:580
 constexpr int kPending = 1;             // status: handed to the overflow kernel
+constexpr int kLin = 16;                // lineage row: ancestors at depths 0..15 (64 B)
 
 // Parameters with the derived thresholds precomputed on the host
 // (orgscorer.py:338-346, :515-516, :720-721).
@@ -34,6 +35,8 @@ struct KArgs {
   const int64_t* loc_off; const int32_t* lstart; const int32_t* lend; const int8_t* lstrand;
   // taxonomy
   const int32_t* parent; const int32_t* depth; const int32_t* sibp; const int64_t* leaves;
+  const int32_t* lin;            // [names * kLin] ancestor at each depth (-1 below the name);
+                                 // null when the taxonomy is kLin or more levels deep
   int32_t root, unknown;
   DevParams p;
   // results
@@ -62,7 +65,7 @@ struct SArgs {
   int32_t* seg_start; int32_t* seg_crank; double* seg_mean;
   const int32_t* act;  const int64_t* act_base;   // active contigs of this level
   int32_t* act_next; int64_t* act_base_next;      // raised contigs (next level)
-  unsigned long long* counters;  // [0] next active, [1] next attachments, [2] big count
+  unsigned long long* counters;  // [0] next active << 40 | next attachments, [2] big count
   int32_t* big_list;             // contigs whose decision state needs an HBM slot
   int32_t* two_list;             // (rank, contig) pairs that need explain_two (counters[5])
   int32_t* one_list;             // (rank, contig) pairs for the dense explain_one workgroup
@@ -89,6 +92,7 @@ struct SArgs {
   const int32_t* lut_off;        // [kNpyBuf + 2] numpy leaf table offsets by length
   const int4* lut;               // (start, length, parent adds) per leaf
   int64_t dec_lds_bytes;         // LDS arena of the decision workgroup
+  int sort_cap;                  // per-contig LDS sort capacity (power of 2; 0: device radix sort)
 };
 
 struct StagedState;

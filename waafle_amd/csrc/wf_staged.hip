@@ -203,6 +203,69 @@ __global__ void k_keys_active(const SArgs* __restrict__ sp, int n_act, uint64_t*
   }
 }
 
+// Largest attachment count of one contig (sizes the per-contig sort; later levels only
+// hold subsets of the same contigs).
+__global__ void k_att_max(const SArgs* __restrict__ sp, unsigned long long* out) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= K.n_contigs) return;
+  const int64_t n = S.att_off[K.hit_off[c + 1]] - S.att_off[K.hit_off[c]];
+  if (n > 0) atomicMax(out, (unsigned long long)n);
+}
+
+// Segments only ever group attachments of one contig, and the contigs' key blocks already
+// sit in rank order (level 0: attachment order; later levels: act_base is handed out in
+// rank order), so sorting each contig's (key, attachment) pairs on its own -- in LDS, one
+// workgroup per contig -- gives the same sequence as one global radix sort of the level.
+// Ties keep attachment order (the pair is the sort key).  Keys are built here (no separate
+// key kernel).  Dynamic LDS: sort_cap x (8 + 4) bytes.
+constexpr int kSortNT = 256;
+constexpr int kSortMax = 4096;   // 48 KiB of LDS; larger contigs (cfg5 stress) sort faster with the radix sort
+
+__global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs* __restrict__ sp, int n_act,
+                                                          int level, uint64_t* keys, int32_t* vals) {
+  const SArgs& S = *sp;
+  const KArgs& K = S.k;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t* sk = reinterpret_cast<uint64_t*>(smem);
+  int32_t* sv = reinterpret_cast<int32_t*>(sk + S.sort_cap);
+  const int tid = threadIdx.x;
+  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const int c = S.act ? S.act[cr] : cr;
+    const int64_t a0 = S.att_off[K.hit_off[c]], a1 = S.att_off[K.hit_off[c + 1]];
+    const int n = (int)(a1 - a0);
+    if (n == 0) continue;
+    const int64_t base = level == 0 ? a0 : S.act_base[cr];
+    int n2 = 2;
+    while (n2 < n) n2 <<= 1;
+    for (int t = tid; t < n2; t += kSortNT) {
+      sk[t] = t < n ? make_key(S, cr, (int)(a0 + t)) : ~0ull;
+      sv[t] = t < n ? (int)(a0 + t) : 0x7fffffff;
+    }
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < (n2 >> 1); i += kSortNT) {
+          const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));   // i with a 0 inserted at bit j
+          const int hi = lo | j;
+          const bool up = (lo & k) == 0;
+          const uint64_t ka = sk[lo], kb = sk[hi];
+          const int32_t va = sv[lo], vb = sv[hi];
+          const bool gt = ka > kb || (ka == kb && va > vb);
+          if (gt == up) { sk[lo] = kb; sk[hi] = ka; sv[lo] = vb; sv[hi] = va; }
+        }
+        __syncthreads();
+      }
+    }
+    for (int t = tid; t < n; t += kSortNT) {
+      keys[base + t] = sk[t];
+      vals[base + t] = sv[t];
+    }
+    __syncthreads();
+  }
+}
+
 __global__ void k_seg_flags(const uint64_t* keys, int64_t n, int32_t* flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
@@ -270,6 +333,15 @@ __device__ __forceinline__ int lut_count(const SArgs& S, int m) { return S.lut_o
 
 // Per segment: its leaf count (for the leaf offsets scan) and a self-contained record, so
 // the leaf kernels resolve a segment with one load.
+//
+// Short segments (one buffer, <= kRegAtt attachments, <= kThreadLeaves leaves: every
+// segment of a <= 2.9 kb locus at the species level) are finished right here by their own
+// thread: leaves in tree order on a register stack, exactly like k_leaf + k_seg_combine,
+// without the leaf list, the leaf values or the leaf -> segment map ever touching HBM.
+// Their leaf count is reported as 0, so the leaf kernels skip them.
+constexpr int kThreadLeaves = 32;
+
+template <bool THREAD_MEAN>
 __global__ void k_seg_rec(const SArgs* __restrict__ sp, int64_t n_keys) {
   const SArgs& S = *sp;
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -278,8 +350,16 @@ __global__ void k_seg_rec(const SArgs* __restrict__ sp, int64_t n_keys) {
   if (s < seg_count(S, n_keys)) {
     const SegInfo si = seg_info(S, (int)s);
     nl = (si.len / kNpyBuf) * lut_count(S, kNpyBuf) + lut_count(S, si.len % kNpyBuf);
-    S.seg_rec[s] = make_int4(si.kb, si.ke - si.kb, si.len, nl);
     S.seg_cg[s] = make_int2((int)((S.keys[si.kb] >> S.key_lb) & ((1ull << S.key_tb) - 1)), si.g);
+    if (THREAD_MEAN && si.len < kNpyBuf && si.ke - si.kb <= kRegAtt && nl <= kThreadLeaves) {
+      const SortedSrc src{S.satt_lohi, S.satt_sc};
+      SegAttT<SortedSrc> at;
+      at.load(src, si.kb, si.ke);
+      S.seg_mean[s] = seg_mean_thread(at, src, S.lut + S.lut_off[si.len], nl, si.len);
+      nl = 0;
+    } else {
+      S.seg_rec[s] = make_int4(si.kb, si.ke - si.kb, si.len, nl);
+    }
   }
   S.seg_nleaf[s] = nl;
 }
@@ -360,7 +440,7 @@ __global__ void k_leaf(const SArgs* __restrict__ sp, int64_t n_keys) {
 __global__ void k_seg_combine(const SArgs* __restrict__ sp, int64_t n_keys) {
   const SArgs& S = *sp;
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= seg_count(S, n_keys)) return;
+  if (s >= seg_count(S, n_keys) || S.seg_nleaf[s] == 0) return;   // 0: mean done in k_seg_rec
   const int len = S.seg_rec[s].z;
   const double* lv = S.leaf_val + S.leaf_off[s];
   double total = 0.0;
@@ -747,6 +827,7 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   C.best_syn = ar.take<uint8_t>(G);
   C.loc_len = ar.take<int>(G);                  // ambiguous fraction weights (orgscorer.py:693-702)
   C.sib_of = ar.take<int>(Pmax);
+  if (P.sister_on && G <= 64) C.hm = ar.take<uint64_t>(Pmax);
   int* seg_ci = ar.take<int>(ns + 1);
   if (Pmax >= kClsMin) {                         // mask classes for a large explain_two
     C.xcap = cls_bytes(Pmax);
@@ -830,9 +911,13 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
     // roll up (orgscorer.py:431-445): this contig's attachments move to the parent clade
     const int64_t a0 = S.att_off[h0], a1 = S.att_off[h0 + H];
     if (tid == 0) {
-      const int slot = (int)atomicAdd(&S.counters[0], 1ull);
+      // slot (high 24 bits) and attachment base (low 40) from ONE atomic, so the bases of
+      // the next level ascend with the rank (the per-contig sort relies on it)
+      const unsigned long long old =
+          atomicAdd(&S.counters[0], (1ull << 40) | (unsigned long long)(a1 - a0));
+      const int slot = (int)(old >> 40);
       S.act_next[slot] = c;
-      S.act_base_next[slot] = (int64_t)atomicAdd(&S.counters[1], (unsigned long long)(a1 - a0));
+      S.act_base_next[slot] = (int64_t)(old & ((1ull << 40) - 1));
       K.pair_evals[c] = pair_evals;
     }
     for (int64_t a = a0 + tid; a < a1; a += NT) S.att_clade[a] = K.parent[S.att_clade[a]];
@@ -1041,7 +1126,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->cnt.ensure((size_t)(NH + 1) * sizeof(int64_t)));
   ST_TRY(st->cnt_leaves.ensure((size_t)(NH + 1) * sizeof(int64_t)));
   ST_TRY(st->att_off.ensure((size_t)(NH + 1) * sizeof(int64_t)));
-  ST_TRY(st->red.ensure(sizeof(int64_t)));
+  ST_TRY(st->red.ensure(2 * sizeof(int64_t)));
   sa.hit_contig = st->hit_contig.as<int32_t>();
   sa.att_off = st->att_off.as<int64_t>();
   ST_TRY(upload());
@@ -1064,10 +1149,21 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     ST_TRY(hipcub::DeviceReduce::Sum(st->tmp.p, tb, st->cnt_leaves.as<int64_t>(),
                                      st->red.as<int64_t>(), (int)(NH + 1), s));
   }
+  ST_TRY(hipMemsetAsync(st->red.as<int64_t>() + 1, 0, sizeof(int64_t), s));
+  hipLaunchKernelGGL(k_att_max, dim3(grid_for(N)), dim3(256), 0, s, dsa,
+                     reinterpret_cast<unsigned long long*>(st->red.as<int64_t>() + 1));
   ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + NH, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   ST_TRY(hipStreamSynchronize(s));
-  const int64_t A = hc[2], TLB = hc[3];
+  const int64_t A = hc[2], TLB = hc[3], max_att = hc[4];
+  // per-contig LDS sort when every contig's attachments fit one workgroup's LDS
+  // (WF_LDS_SORT=0: device radix sort of the whole level; measurement aid)
+  static const char* ls_env = getenv("WF_LDS_SORT");
+  sa.sort_cap = 0;
+  if (!(ls_env && ls_env[0] == '0') && max_att <= kSortMax) {
+    sa.sort_cap = 2;
+    while (sa.sort_cap < max_att) sa.sort_cap <<= 1;
+  }
   if (A >= (int64_t(1) << 31) - 1 || TLB >= (int64_t(1) << 31) - 1) {
     *err = "too many hit-locus attachments for one batch (split it)";
     return -1;
@@ -1155,6 +1251,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   static const char* one_env = getenv("WF_ONE_FAST");
   const bool one_fast = !flat_one && !(one_env && one_env[0] == '0');
   sa.one_list = one_fast ? st->one_list.as<int32_t>() : nullptr;
+  // short segments' means by one thread each in k_seg_rec (WF_THREAD_MEAN=0: every segment
+  // through the leaf kernels; measurement aid)
+  static const char* tm_env = getenv("WF_THREAD_MEAN");
+  const bool thread_mean = !(tm_env && tm_env[0] == '0');
   // roll-up levels
   Buf* act[2] = {&st->act0, &st->act1};
   Buf* base[2] = {&st->base0, &st->base1};
@@ -1179,15 +1279,29 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     ST_TRY(upload());
     ST_TRY(hipMemsetAsync(st->counters.p, 0, 8 * sizeof(unsigned long long), s));
     if (n_keys > 0) {
-      if (level == 0)
-        hipLaunchKernelGGL(k_keys_all, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys,
-                           kbuf.Current(), vbuf.Current());
-      else
-        hipLaunchKernelGGL(k_keys_active, dim3(std::min(n_act, st->cus * 8)), dim3(256), 0, s, dsa,
-                           n_act, kbuf.Current(), vbuf.Current());
-      ST_TRY(hipGetLastError());
       size_t need = st->tmp.n;
-      ST_TRY(hipcub::DeviceRadixSort::SortPairs(st->tmp.p, need, kbuf, vbuf, (int)n_keys, 0, end_bit, s));
+      if (sa.sort_cap > 0) {
+        const size_t lds = (size_t)sa.sort_cap * 12;
+        if (lds > 64 * 1024) {
+          static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(kSortMax * 12));
+          ST_TRY(attr);
+        }
+        const int per_cu = std::max(1, (int)((160 * 1024) / lds));
+        hipLaunchKernelGGL(k_sort_contig, dim3(std::min(n_act, st->cus * per_cu)), dim3(kSortNT), lds, s,
+                           dsa, n_act, level, kbuf.Current(), vbuf.Current());
+      } else {
+        if (level == 0)
+          hipLaunchKernelGGL(k_keys_all, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys,
+                             kbuf.Current(), vbuf.Current());
+        else
+          hipLaunchKernelGGL(k_keys_active, dim3(std::min(n_act, st->cus * 8)), dim3(256), 0, s, dsa,
+                             n_act, kbuf.Current(), vbuf.Current());
+        ST_TRY(hipGetLastError());
+        ST_TRY(hipcub::DeviceRadixSort::SortPairs(st->tmp.p, need, kbuf, vbuf, (int)n_keys, 0, end_bit, s));
+      }
+      ST_TRY(hipGetLastError());
       sa.keys = kbuf.Current();
       sa.vals = vbuf.Current();
       ST_TRY(upload());
@@ -1197,7 +1311,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
       hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
       hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys, n_act);
-      hipLaunchKernelGGL(k_seg_rec, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys);
+      if (thread_mean)
+        hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys);
+      else
+        hipLaunchKernelGGL(k_seg_rec<false>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys);
       need = st->tmp.n;
       ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_nleaf, sa.leaf_off,
                                               (int)n_keys + 1, s));
@@ -1261,8 +1378,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     }
     if (level == 0 && !st->dec_lds_fixed && n_big * 50 > n_act && st->dec_lds < 48 * 1024)
       st->dec_lds += 8 * 1024;   // adaptive arena: grows while > 2% of contigs overflow
-    n_act = (int)st->host_counters[0];
-    n_keys = (int64_t)st->host_counters[1];
+    n_act = (int)(st->host_counters[0] >> 40);
+    n_keys = (int64_t)(st->host_counters[0] & ((1ull << 40) - 1));
   }
   return 0;
 }
