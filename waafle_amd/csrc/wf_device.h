@@ -683,59 +683,7 @@ struct SegAttT {
     const double body = reg ? runs_body<true>(C, st, m) : runs_body<false>(C, st, m);
     return add_tail(C, st, ln, body);
   }
-  // Whole leaf [st, st+ln) under one envelope value F (no higher attachment reaches into
-  // it): its value depends on (F, ln) only.  Register attachments only.
-  __device__ __forceinline__ bool leaf_const(int st, int ln, double& F) const {
-    const int le = st + ln;
-    F = 0.0;
-#pragma unroll
-    for (int i = 0; i < kRegAtt; ++i)
-      if (lo[i] < hi[i] && lo[i] <= st && le <= hi[i]) F = sc[i] > F ? sc[i] : F;
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < kRegAtt; ++i)
-      if (lo[i] < hi[i] && lo[i] < le && hi[i] > st && !(lo[i] <= st && le <= hi[i]) && sc[i] > F)
-        ok = false;
-    return ok;
-  }
 };
-
-// Value of a leaf of ln sites that all hold F (numpy's block: 8 accumulators over the
-// body, tree, then the tail in order).
-__device__ __forceinline__ double const_leaf_value(double F, int ln) {
-  if (!(F > 0.0)) return 0.0;
-  const int m = ln >> 3;
-  double res = m > 0 ? 8.0 * seqsum(F, m) : 0.0;
-  for (int x = m << 3; x < ln; ++x) res += F;
-  return res;
-}
-
-// Exact np.mean of one short segment (one buffer, register attachments) by one thread:
-// leaves from the length's table in tree order on a register stack.  Leaves under a single
-// envelope value reuse the last such leaf's value when (F, length) repeat -- the usual
-// case: a hit covering the locus makes every leaf constant, in <= 3 distinct lengths.
-template <class Src>
-__device__ __forceinline__ double seg_mean_thread(const SegAttT<Src>& at, const Src& src,
-                                                  const int4* lt, int nl, int len) {
-  SumStack stk;
-  double mF = -1.0, mv = 0.0;
-  int mln = -1;
-  int4 e = lt[0];
-  for (int q = 0; q < nl; ++q) {
-    const int4 cur = e;
-    if (q + 1 < nl) e = lt[q + 1];                 // next leaf's entry in flight
-    double F, v;
-    if (at.leaf_const(cur.x, cur.y, F)) {
-      if (F != mF || cur.y != mln) { mv = const_leaf_value(F, cur.y); mF = F; mln = cur.y; }
-      v = mv;
-    } else {
-      v = at.leaf(src, cur.x, cur.y);
-    }
-    stk.push(v);
-    for (int a = 0; a < cur.z; ++a) stk.add_top();
-  }
-  return (0.0 + stk.s0) / (double)len;
-}
 using SegAtt = SegAttT<KeySrc>;
 
 // Exact np.mean of one (clade, locus) site array (orgscorer.py:399-406) by one thread:

@@ -334,12 +334,42 @@ __device__ __forceinline__ int lut_count(const SArgs& S, int m) { return S.lut_o
 // Per segment: its leaf count (for the leaf offsets scan) and a self-contained record, so
 // the leaf kernels resolve a segment with one load.
 //
-// Short segments (one buffer, <= kRegAtt attachments, <= kThreadLeaves leaves: every
-// segment of a <= 2.9 kb locus at the species level) are finished right here by their own
-// thread: leaves in tree order on a register stack, exactly like k_leaf + k_seg_combine,
-// without the leaf list, the leaf values or the leaf -> segment map ever touching HBM.
-// Their leaf count is reported as 0, so the leaf kernels skip them.
+// Segments whose site array is ONE run of value v over a zero background -- a single
+// attachment (lo, hi, v), or any number of them all dominated by the highest one that covers
+// the whole locus (lo = 0, hi = len, v = that score) -- are finished right here by their own
+// thread (one buffer, <= kThreadLeaves leaves: every species-level segment of a <= 2.9 kb
+// locus).  Every leaf then has the same closed form (run_leaf), so the lanes of a wave run
+// one code path; the leaves go in tree order onto a register stack, exactly as k_leaf +
+// k_seg_combine do, without the leaf list, the leaf values or the leaf -> segment map ever
+// touching HBM.  Their leaf count is reported as 0, so the leaf kernels skip them.
 constexpr int kThreadLeaves = 32;
+constexpr int kPruneMax = 64;      // attachments scanned for whole-locus domination
+
+// numpy's leaf [st, st+ln) over sites holding v on [lo, hi) and 0 elsewhere: accumulator c
+// adds v k_c times from 0.0 (k_c in {kmin, kmin+1, kmin+2}: seqsum closed form, see
+// SegAttT::closed_body), tree of the 8, then the tail sites in order.
+__device__ __forceinline__ double run_leaf(int lo, int hi, double v, int st, int ln) {
+  const int m = ln >> 3, be = st + (m << 3);
+  hi = max(hi, lo);                                  // empty slice (--min-overlap 0 wrap)
+  double res = 0.0;
+  if (m > 0) {
+    int k[8], kmin = m;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      k[c] = below(st + c, hi, m) - below(st + c, lo, m);
+      kmin = min(kmin, k[c]);
+    }
+    double s0 = 0.0;
+    for (int i = 0; i < kmin; ++i) s0 += v;
+    const double s1 = s0 + v, s2 = s1 + v;
+    double r[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r[c] = k[c] == kmin ? s0 : (k[c] == kmin + 1 ? s1 : s2);
+    res = leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+  }
+  for (int x = be; x < st + ln; ++x) res += (x >= lo && x < hi) ? v : 0.0;
+  return res;
+}
 
 template <bool THREAD_MEAN>
 __global__ void k_seg_rec(const SArgs* __restrict__ sp, int64_t n_keys) {
@@ -351,14 +381,44 @@ __global__ void k_seg_rec(const SArgs* __restrict__ sp, int64_t n_keys) {
     const SegInfo si = seg_info(S, (int)s);
     nl = (si.len / kNpyBuf) * lut_count(S, kNpyBuf) + lut_count(S, si.len % kNpyBuf);
     S.seg_cg[s] = make_int2((int)((S.keys[si.kb] >> S.key_lb) & ((1ull << S.key_tb) - 1)), si.g);
-    if (THREAD_MEAN && si.len < kNpyBuf && si.ke - si.kb <= kRegAtt && nl <= kThreadLeaves) {
-      const SortedSrc src{S.satt_lohi, S.satt_sc};
-      SegAttT<SortedSrc> at;
-      at.load(src, si.kb, si.ke);
-      S.seg_mean[s] = seg_mean_thread(at, src, S.lut + S.lut_off[si.len], nl, si.len);
+    bool one_run = false;
+    int lo = 0, hi = 0;
+    double v = 0.0;
+    const int na = si.ke - si.kb;
+    if (THREAD_MEAN && si.len < kNpyBuf && nl <= kThreadLeaves) {
+      if (na == 1) {
+        const int2 x = S.satt_lohi[si.kb];
+        lo = x.x; hi = x.y; v = S.satt_sc[si.kb];
+        one_run = true;
+      } else if (na <= kPruneMax) {
+        double F = 0.0;                              // best whole-locus attachment
+        for (int t = si.kb; t < si.ke; ++t) {
+          const int2 x = S.satt_lohi[t];
+          const double sc = S.satt_sc[t];
+          if (x.x <= 0 && x.y >= si.len && sc > F) F = sc;
+        }
+        bool dom = true;                             // nothing else rises above it
+        for (int t = si.kb; t < si.ke && dom; ++t) {
+          const int2 x = S.satt_lohi[t];
+          if (x.x < x.y && S.satt_sc[t] > F) dom = false;
+        }
+        if (dom) { lo = 0; hi = si.len; v = F; one_run = true; }
+      }
+    }
+    if (one_run) {
+      const int4* lt = S.lut + S.lut_off[si.len];
+      SumStack stk;
+      int4 e = lt[0];
+      for (int q = 0; q < nl; ++q) {
+        const int4 cur = e;
+        if (q + 1 < nl) e = lt[q + 1];               // next leaf's entry in flight
+        stk.push(run_leaf(lo, hi, v, cur.x, cur.y));
+        for (int a = 0; a < cur.z; ++a) stk.add_top();
+      }
+      S.seg_mean[s] = (0.0 + stk.s0) / (double)si.len;
       nl = 0;
     } else {
-      S.seg_rec[s] = make_int4(si.kb, si.ke - si.kb, si.len, nl);
+      S.seg_rec[s] = make_int4(si.kb, na, si.len, nl);
     }
   }
   S.seg_nleaf[s] = nl;
