@@ -55,8 +55,7 @@ struct SArgs {
   KArgs k;                       // batch, taxonomy, params, results (k.big_ws: tier-3 slots)
   int n_hits_i;                  // hits in the batch (int range checked on the host)
   int key_lb, key_tb;            // key = crank << (tb + lb) | clade << lb | locus
-  const int32_t* hit_contig;     // [n_hits]
-  const int64_t* att_off;        // [n_hits + 1] exclusive scan of attachments per hit
+  const int64_t* catt_off;       // [n_contigs + 1] exclusive scan of attachments per contig
   int32_t *att_lo, *att_hi, *att_loc, *att_clade, *att_hit;
   double* att_sc;
   // current level

@@ -2,14 +2,19 @@
 // carrying a contig through every phase (wf_kernels.hip), each phase is a flat kernel over
 // all contigs' items, so every phase fills the chip at its own natural granularity:
 //
-//   hits        k_hit_contig, k_att_count     thread per hit: attached loci (orgscorer.py:359-369)
-//               device exclusive scan          -> attachment offsets (contiguous per contig)
-//               k_att_fill                     thread per hit: site ranges (:371-382)
-//   loci        k_annot                        thread per locus: annotation winners (:383-392)
-//   per level   k_keys_*                       (contig rank, clade, locus) keys
-//               device radix sort              -> segments = equal keys (:394-406)
+//   contigs     k_att_contig<0>                workgroup per contig, thread per hit: attached
+//                                              loci counted (orgscorer.py:359-369)
+//               device exclusive scan          -> attachment offsets per contig
+//               k_att_contig<1>                site ranges (:371-382), annotation winners
+//                                              in LDS (:383-392)
+//   per level   k_sort_contig                  per-contig LDS sort of (contig rank, clade,
+//                                              locus) keys (device radix sort for huge
+//                                              contigs) -> segments = equal keys (:394-406)
 //               k_seg_flags + scan + k_segs    segment boundaries
-//               k_leaf + k_seg_combine         lane per numpy leaf, thread per segment: exact mean
+//               k_seg_rec                      thread per one-run segment: exact mean
+//               k_leaf + k_seg_combine         lane per numpy leaf, thread per segment: exact
+//                                              mean of the other segments
+//               k_one                          wave per contig: explain_one (+ meld_one)
 //               k_decide / k_decide_big        workgroup per contig: maxes, weak loci,
 //                                              explain_one/two, melds, LGT filters
 //                                              (decide_level, shared with the fused form);
@@ -77,8 +82,7 @@ __global__ void k_lut_fill(const int32_t* off, int4* lut) {
 }
 
 // ---- contigs, hits, attachments ----------------------------------------------------------
-__global__ void k_init(const KArgs* __restrict__ kp) {
-  const KArgs& K = *kp;
+__global__ void k_init(const KArgs K) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= K.n_contigs) return;
   K.call[c] = WF_CALL_UNCLASSIFIED;
@@ -87,91 +91,176 @@ __global__ void k_init(const KArgs* __restrict__ kp) {
   K.need[c] = 0;
 }
 
-__global__ void k_hit_contig(const SArgs* __restrict__ sp, int32_t* hit_contig) {
-  const SArgs& S = *sp;
-  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= S.n_hits_i) return;
-  hit_contig[h] = upper_index(S.k.hit_off, S.k.n_contigs, h);
-}
+// Hits -> attachments, one workgroup per contig (grid-stride).  The contig's loci are
+// staged in LDS; hits are taken in chunks of kAttNT (one thread each, the contig's loci in
+// GFF order), so attachments come out in (hit, locus) order -- the order the reference
+// paints sites in (orgscorer.py:359-382).  Pass 0 only counts (attachments, a leaf bound
+// and the largest contig); pass 1 writes them at the contig's offset and does the
+// annotation transfer (orgscorer.py:383-392) for the contig's loci in LDS.
+constexpr int kAttNT = 64;       // one wave per contig: many contigs in flight
+constexpr int kAttLoc = 128;      // loci staged in LDS (more: read from HBM)
+constexpr int kAnnSlots = 256;    // (locus, system) annotation slots in LDS
 
-// Attachments per hit (cnt) and an upper bound of the numpy leaves their segments can
-// have (leaves: a segment has at most the leaves of its locus, and no more segments than
-// attachments).
-__global__ void k_att_count(const SArgs* __restrict__ sp, int64_t* cnt, int64_t* leaves) {
-  const SArgs& S = *sp;
+struct LocView {
+  int lo, len, st;
+};
+
+template <int PASS>
+__global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* ccnt,
+                                                       int64_t* cleaves, unsigned long long* cmax) {
   const KArgs& K = S.k;
-  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (h > S.n_hits_i) return;
-  if (h == S.n_hits_i) { cnt[h] = 0; leaves[h] = 0; return; }
-  int n = 0;
-  int64_t nl = 0;
-  if (K.scov[h] >= K.p.min_scov) {
-    const int c = S.hit_contig[h];
-    const int qlo = K.qlo[h], qhi = K.qhi[h], hs = K.hstrand[h];
-    for (int64_t l = K.loc_off[c]; l < K.loc_off[c + 1]; ++l) {
-      const int s = K.lstart[l], e = K.lend[l];
-      const int lo = min(s, e), len = max(s, e) - lo + 1;
-      if (attaches(K.p, qlo, qhi, hs, lo, len, K.lstrand[l])) {
-        ++n;
-        nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
-              (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+  const DevParams& P = K.p;
+  __shared__ int s_lo[kAttLoc], s_len[kAttLoc], s_nl[kAttLoc];
+  __shared__ int8_t s_st[kAttLoc];
+  __shared__ unsigned long long s_best[kAnnSlots];
+  __shared__ int s_hit[kAnnSlots];
+  __shared__ int s_scan[kAttNT / 64];
+  __shared__ long long s_red[2][kAttNT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
+    const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    const bool lds_loc = G <= kAttLoc;
+    if (lds_loc)
+      for (int g = tid; g < G; g += kAttNT) {
+        const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
+        s_lo[g] = min(a, b);
+        const int len = max(a, b) - min(a, b) + 1;
+        s_len[g] = len;
+        s_st[g] = K.lstrand[l0 + g];
+        if (PASS == 0)
+          s_nl[g] = (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+                    (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+      }
+    const int ns = K.n_sys;
+    const bool lds_ann = PASS == 1 && (int64_t)G * ns <= kAnnSlots;
+    if (lds_ann)
+      for (int i = tid; i < G * ns; i += kAttNT) { s_best[i] = 0ull; s_hit[i] = -1; }
+    __syncthreads();
+    auto locus = [&](int g) -> LocView {
+      if (lds_loc) return LocView{s_lo[g], s_len[g], s_st[g]};
+      const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
+      return LocView{min(a, b), max(a, b) - min(a, b) + 1, K.lstrand[l0 + g]};
+    };
+    long long n_tot = 0, nl_tot = 0;
+    int64_t base = PASS == 1 ? S.catt_off[c] : 0;
+    for (int64_t hb = h0; hb < h1; hb += kAttNT) {
+      const int64_t h = hb + tid;
+      int n = 0;
+      long long nl = 0;
+      int qlo = 0, qhi = 0, hs = 0;
+      const bool live = h < h1 && K.scov[h] >= P.min_scov;
+      if (live) {
+        qlo = K.qlo[h]; qhi = K.qhi[h]; hs = K.hstrand[h];
+        for (int g = 0; g < G; ++g) {
+          const LocView L = locus(g);
+          if (attaches(P, qlo, qhi, hs, L.lo, L.len, L.st)) {
+            ++n;
+            if (PASS == 0)
+              nl += lds_loc ? s_nl[g]
+                            : (L.len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+                                  (S.lut_off[L.len % kNpyBuf + 1] - S.lut_off[L.len % kNpyBuf]);
+          }
+        }
+      }
+      if (PASS == 0) {
+        n_tot += n;
+        nl_tot += nl;
+        continue;
+      }
+      // exclusive scan of n over the chunk (hit order)
+      int x = n;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      if (lane == 63) s_scan[w] = x;
+      __syncthreads();
+      int wbase = 0, total = 0;
+#pragma unroll
+      for (int i = 0; i < kAttNT / 64; ++i) {
+        wbase += i < w ? s_scan[i] : 0;
+        total += s_scan[i];
+      }
+      __syncthreads();
+      int64_t o = base + wbase + x - n;
+      base += total;
+      if (n == 0) continue;
+      int clade = K.taxon[h];
+      for (int j = 0; j < P.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
+      const double sc = K.score[h];
+      const uint32_t m = ns > 0 ? K.sysmask[h] : 0u;
+      const bool ann = m != 0 && sc >= P.annot_ref;
+      for (int g = 0; g < G; ++g) {
+        const LocView L = locus(g);
+        if (!attaches(P, qlo, qhi, hs, L.lo, L.len, L.st)) continue;
+        const int h1s = max(0, qlo - L.lo);
+        const int h2s = min(L.len - 1, qhi - L.lo);
+        const int start = min(h1s, L.len);
+        int stop = h2s + 1;                        // site[h1:h2+1], python slice rules
+        if (stop < 0) { stop += L.len; if (stop < 0) stop = 0; }
+        S.att_lo[o] = start;
+        S.att_hi[o] = stop;                        // empty when stop <= start
+        S.att_loc[o] = g;
+        S.att_clade[o] = clade;
+        S.att_hit[o] = (int)h;
+        S.att_sc[o] = sc;
+        ++o;
+        if (ann) {                                  // annotation pass 1: best score bits
+          for (int b = 0; b < ns; ++b) {
+            if (!((m >> b) & 1u)) continue;
+            if (lds_ann) atomicMax(&s_best[g * ns + b], dbits(sc));
+            else atomicMax(reinterpret_cast<unsigned long long*>(&S.annot_best[(l0 + g) * ns + b]), dbits(sc));
+          }
+        }
       }
     }
-  }
-  cnt[h] = n;
-  leaves[h] = nl;
-}
-
-__global__ void k_att_fill(const SArgs* __restrict__ sp) {
-  const SArgs& S = *sp;
-  const KArgs& K = S.k;
-  const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= S.n_hits_i) return;
-  if (!(K.scov[h] >= K.p.min_scov)) return;
-  const int c = S.hit_contig[h];
-  const int qlo = K.qlo[h], qhi = K.qhi[h], hs = K.hstrand[h];
-  int clade = K.taxon[h];
-  for (int j = 0; j < K.p.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
-  int64_t o = S.att_off[h];
-  const int64_t l0 = K.loc_off[c];
-  for (int64_t l = l0; l < K.loc_off[c + 1]; ++l) {
-    const int s = K.lstart[l], e = K.lend[l];
-    const int lo = min(s, e), len = max(s, e) - lo + 1;
-    if (!attaches(K.p, qlo, qhi, hs, lo, len, K.lstrand[l])) continue;
-    const int h1 = max(0, qlo - lo);
-    const int h2 = min(len - 1, qhi - lo);
-    const int start = min(h1, len);
-    int stop = h2 + 1;                         // site[h1:h2+1], python slice rules
-    if (stop < 0) { stop += len; if (stop < 0) stop = 0; }
-    S.att_lo[o] = start;
-    S.att_hi[o] = stop;                        // empty when stop <= start
-    S.att_loc[o] = (int)(l - l0);
-    S.att_clade[o] = clade;
-    S.att_hit[o] = (int)h;
-    S.att_sc[o] = K.score[h];
-    ++o;
-  }
-}
-
-// Annotation transfer (orgscorer.py:383-392): per (locus, system) the last hit in file
-// order whose score equals the running maximum >= threshold, i.e. the largest hit index
-// among the hits with the maximal qualifying score.  Two passes over attachments: max
-// score bits (scores are >= 0), then max hit index at that score.
-__global__ void k_annot(const SArgs* __restrict__ sp, int64_t n_att, int pass) {
-  const SArgs& S = *sp;
-  const KArgs& K = S.k;
-  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= n_att) return;
-  const int h = S.att_hit[a];
-  const uint32_t m = K.sysmask[h];
-  const double sc = S.att_sc[a];
-  if (m == 0 || !(sc >= K.p.annot_ref)) return;
-  const int64_t l = K.loc_off[S.hit_contig[h]] + S.att_loc[a];
-  for (int b = 0; b < K.n_sys; ++b) {
-    if (!((m >> b) & 1u)) continue;
-    const int64_t slot = l * K.n_sys + b;
-    if (pass == 0) atomicMax(reinterpret_cast<unsigned long long*>(&S.annot_best[slot]), dbits(sc));
-    else if (S.annot_best[slot] == dbits(sc)) atomicMax(&K.annot[slot], h);
+    if (PASS == 0) {
+      long long a = n_tot, b = nl_tot;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        b += __shfl_xor(b, off, 64);
+      }
+      if (lane == 0) { s_red[0][w] = a; s_red[1][w] = b; }
+      __syncthreads();
+      if (tid == 0) {
+        long long ta = 0, tb = 0;
+        for (int i = 0; i < kAttNT / 64; ++i) { ta += s_red[0][i]; tb += s_red[1][i]; }
+        ccnt[c] = ta;
+        cleaves[c] = tb;
+        if (ta > 0) atomicMax(cmax, (unsigned long long)ta);
+      }
+      __syncthreads();
+      continue;
+    }
+    if (ns > 0) {
+      // annotation pass 2: the last hit (largest index) at the best score, per (locus,
+      // system); every attachment of this contig is in [catt_off[c], base)
+      __syncthreads();
+      const int64_t a0 = S.catt_off[c];
+      for (int64_t a = a0 + tid; a < base; a += kAttNT) {
+        const int h = S.att_hit[a];
+        const uint32_t m = K.sysmask[h];
+        const double sc = S.att_sc[a];
+        if (m == 0 || !(sc >= P.annot_ref)) continue;
+        const int g = S.att_loc[a];
+        for (int b = 0; b < ns; ++b) {
+          if (!((m >> b) & 1u)) continue;
+          if (lds_ann) {
+            if (s_best[g * ns + b] == dbits(sc)) atomicMax(&s_hit[g * ns + b], h);
+          } else if (S.annot_best[(l0 + g) * ns + b] == dbits(sc)) {
+            atomicMax(&K.annot[(l0 + g) * ns + b], h);
+          }
+        }
+      }
+      __syncthreads();
+      if (lds_ann)
+        for (int i = tid; i < G * ns; i += kAttNT) K.annot[l0 * ns + i] = s_hit[i];
+    }
+    __syncthreads();
   }
 }
 
@@ -181,37 +270,18 @@ __device__ __forceinline__ uint64_t make_key(const SArgs& S, int crank, int a) {
          (uint64_t)S.att_loc[a];
 }
 
-__global__ void k_keys_all(const SArgs* __restrict__ sp, int64_t n_att, uint64_t* keys, int32_t* vals) {
-  const SArgs& S = *sp;
-  const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= n_att) return;
-  keys[a] = make_key(S, S.hit_contig[S.att_hit[a]], (int)a);
-  vals[a] = (int)a;
-}
-
-__global__ void k_keys_active(const SArgs* __restrict__ sp, int n_act, uint64_t* keys, int32_t* vals) {
-  const SArgs& S = *sp;
-  const KArgs& K = S.k;
+// Keys of every active contig's attachments at act_base[rank] (level 0: all contigs, at
+// their own attachment offsets).  Used with the device radix sort.
+__global__ void k_keys_active(const SArgs S, int n_act, uint64_t* keys, int32_t* vals) {
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
-    const int c = S.act[cr];
-    const int64_t a0 = S.att_off[K.hit_off[c]], a1 = S.att_off[K.hit_off[c + 1]];
-    const int64_t base = S.act_base[cr];
+    const int c = S.act ? S.act[cr] : cr;
+    const int64_t a0 = S.catt_off[c], a1 = S.catt_off[c + 1];
+    const int64_t base = S.act ? S.act_base[cr] : a0;
     for (int64_t i = threadIdx.x; i < a1 - a0; i += blockDim.x) {
       keys[base + i] = make_key(S, cr, (int)(a0 + i));
       vals[base + i] = (int)(a0 + i);
     }
   }
-}
-
-// Largest attachment count of one contig (sizes the per-contig sort; later levels only
-// hold subsets of the same contigs).
-__global__ void k_att_max(const SArgs* __restrict__ sp, unsigned long long* out) {
-  const SArgs& S = *sp;
-  const KArgs& K = S.k;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= K.n_contigs) return;
-  const int64_t n = S.att_off[K.hit_off[c + 1]] - S.att_off[K.hit_off[c]];
-  if (n > 0) atomicMax(out, (unsigned long long)n);
 }
 
 // Segments only ever group attachments of one contig, and the contigs' key blocks already
@@ -220,20 +290,18 @@ __global__ void k_att_max(const SArgs* __restrict__ sp, unsigned long long* out)
 // workgroup per contig -- gives the same sequence as one global radix sort of the level.
 // Ties keep attachment order (the pair is the sort key).  Keys are built here (no separate
 // key kernel).  Dynamic LDS: sort_cap x (8 + 4) bytes.
-constexpr int kSortNT = 256;
+constexpr int kSortNT = 64;      // one wave per contig
 constexpr int kSortMax = 4096;   // 48 KiB of LDS; larger contigs (cfg5 stress) sort faster with the radix sort
 
-__global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs* __restrict__ sp, int n_act,
+__global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_act,
                                                           int level, uint64_t* keys, int32_t* vals) {
-  const SArgs& S = *sp;
-  const KArgs& K = S.k;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem);
   int32_t* sv = reinterpret_cast<int32_t*>(sk + S.sort_cap);
   const int tid = threadIdx.x;
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const int c = S.act ? S.act[cr] : cr;
-    const int64_t a0 = S.att_off[K.hit_off[c]], a1 = S.att_off[K.hit_off[c + 1]];
+    const int64_t a0 = S.catt_off[c], a1 = S.catt_off[c + 1];
     const int n = (int)(a1 - a0);
     if (n == 0) continue;
     const int64_t base = level == 0 ? a0 : S.act_base[cr];
@@ -271,8 +339,7 @@ __global__ void k_seg_flags(const uint64_t* keys, int64_t n, int32_t* flags) {
   if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
 }
 
-__global__ void k_segs(const SArgs* __restrict__ sp, int64_t n) {
-  const SArgs& S = *sp;
+__global__ void k_segs(const SArgs S, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (S.flags[i]) {
@@ -285,8 +352,7 @@ __global__ void k_segs(const SArgs* __restrict__ sp, int64_t n) {
 
 // crank_first[cr] = first segment of active contig cr (segments are sorted by rank; ranks
 // without segments get the next rank's start), crank_first[n_act] = segment count.
-__global__ void k_crank_first(const SArgs* __restrict__ sp, int64_t n_keys, int n_act) {
-  const SArgs& S = *sp;
+__global__ void k_crank_first(const SArgs S, int64_t n_keys, int n_act) {
   const int ns = seg_count(S, n_keys);
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s > ns) return;
@@ -296,8 +362,7 @@ __global__ void k_crank_first(const SArgs* __restrict__ sp, int64_t n_keys, int 
 }
 
 // Attachments copied into sorted order, so each segment's are contiguous.
-__global__ void k_gather(const SArgs* __restrict__ sp, int64_t n) {
-  const SArgs& S = *sp;
+__global__ void k_gather(const SArgs S, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int a = S.vals[i];
@@ -372,8 +437,7 @@ __device__ __forceinline__ double run_leaf(int lo, int hi, double v, int st, int
 }
 
 template <bool THREAD_MEAN>
-__global__ void k_seg_rec(const SArgs* __restrict__ sp, int64_t n_keys) {
-  const SArgs& S = *sp;
+__global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s > n_keys) return;
   int nl = 0;
@@ -434,8 +498,7 @@ __device__ __forceinline__ int2 leaf_span(const SArgs& S, int len, int j) {
   return make_int2(chunk * kNpyBuf + e.x, e.y);
 }
 
-__global__ void k_leaf_expand(const SArgs* __restrict__ sp, int64_t n_keys) {
-  const SArgs& S = *sp;
+__global__ void k_leaf_expand(const SArgs S, int64_t n_keys) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= seg_count(S, n_keys)) return;
   const int o = S.leaf_off[s], n = S.seg_nleaf[s];
@@ -447,8 +510,7 @@ __global__ void k_leaf_expand(const SArgs* __restrict__ sp, int64_t n_keys) {
 // the j-th of them, lane c of the octet its stride accumulator c, and the eight sums are
 // combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) with xor shuffles (float addition is
 // commutative, so the result is exact).  Wave-uniform loop: every lane runs the same trips.
-__global__ void k_leaf(const SArgs* __restrict__ sp, int64_t n_keys) {
-  const SArgs& S = *sp;
+__global__ void k_leaf(const SArgs S, int64_t n_keys) {
   const int ns = seg_count(S, n_keys);
   const int TL = S.leaf_off[ns];
   const SortedSrc src{S.satt_lohi, S.satt_sc};
@@ -497,8 +559,7 @@ __global__ void k_leaf(const SArgs* __restrict__ sp, int64_t n_keys) {
   }
 }
 
-__global__ void k_seg_combine(const SArgs* __restrict__ sp, int64_t n_keys) {
-  const SArgs& S = *sp;
+__global__ void k_seg_combine(const SArgs S, int64_t n_keys) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= seg_count(S, n_keys) || S.seg_nleaf[s] == 0) return;   // 0: mean done in k_seg_rec
   const int len = S.seg_rec[s].z;
@@ -524,8 +585,7 @@ __global__ void k_seg_combine(const SArgs* __restrict__ sp, int64_t n_keys) {
 // workgroup: per-locus maxes are atomics over segments, each clade run (the clade's
 // segments, sorted by locus) scores itself, the best rank is an atomic max of its bits
 // (ranks are >= 0) and ties go to the larger clade id, like the sorted-order policy.
-__global__ void k_flat_maxes(const SArgs* __restrict__ sp, int64_t n_keys) {
-  const SArgs& S = *sp;
+__global__ void k_flat_maxes(const SArgs S, int64_t n_keys) {
   const KArgs& K = S.k;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= seg_count(S, n_keys)) return;
@@ -538,8 +598,7 @@ __global__ void k_flat_maxes(const SArgs* __restrict__ sp, int64_t n_keys) {
   atomicMax(reinterpret_cast<unsigned long long*>(&S.lmax[K.loc_off[c] + cg.y]), dbits(v));
 }
 
-__global__ void k_flat_prep(const SArgs* __restrict__ sp, int n_act, int level) {
-  const SArgs& S = *sp;
+__global__ void k_flat_prep(const SArgs S, int n_act, int level) {
   const KArgs& K = S.k;
   const int cr = blockIdx.x * blockDim.x + threadIdx.x;
   if (cr >= n_act) return;
@@ -597,8 +656,7 @@ __device__ __forceinline__ bool run_start(const SArgs& S, int s) {
 
 // pass 0: crit/rank of each clade run (Contig.score, orgscorer.py:447-461), best rank;
 // pass 1: best clade (ties -> larger id) and the options within --range (meld members)
-__global__ void k_flat_runs(const SArgs* __restrict__ sp, int64_t n_keys, int pass) {
-  const SArgs& S = *sp;
+__global__ void k_flat_runs(const SArgs S, int64_t n_keys, int pass) {
   const KArgs& K = S.k;
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   const int ns = seg_count(S, n_keys);
@@ -645,8 +703,7 @@ __global__ void k_flat_runs(const SArgs* __restrict__ sp, int64_t n_keys, int pa
 }
 
 // One thread per contig: the result of a one-clade explanation, or hand-off to explain_two.
-__global__ void k_flat_finish(const SArgs* __restrict__ sp, int n_act, int level, int64_t n_keys) {
-  const SArgs& S = *sp;
+__global__ void k_flat_finish(const SArgs S, int n_act, int level, int64_t n_keys) {
   const KArgs& K = S.k;
   const int cr = blockIdx.x * blockDim.x + threadIdx.x;
   if (cr >= n_act || S.c_gu[cr] <= 0) return;
@@ -707,9 +764,8 @@ __global__ void k_flat_finish(const SArgs* __restrict__ sp, int n_act, int level
 // dense workgroup (k_decide<1>); contigs without a one-clade option go to explain_two.
 constexpr int kOneCap = 384;
 
-__global__ __launch_bounds__(64) void k_one(const SArgs* __restrict__ sp, int n_act, int level,
+__global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
                                             int64_t n_keys) {
-  const SArgs& S = *sp;
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   __shared__ int2 s_cg[kOneCap];
@@ -847,7 +903,7 @@ __global__ __launch_bounds__(64) void k_one(const SArgs* __restrict__ sp, int n_
 // PHASE 0: the whole level (HBM-slot tier); 1: prologue + explain_one, contigs without a
 // one-clade explanation are queued for phase 2; 2: prologue + explain_two + roll-up.
 template <int NT, int PHASE>
-__device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* abase, int64_t acap,
+__device__ __forceinline__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* abase, int64_t acap,
                               Ctl& ctl, int64_t n_keys) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
@@ -969,7 +1025,7 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
   if (dec == kDecDone) return true;
   if (dec == kDecRaise && iteration + 1 <= kMaxIter) {
     // roll up (orgscorer.py:431-445): this contig's attachments move to the parent clade
-    const int64_t a0 = S.att_off[h0], a1 = S.att_off[h0 + H];
+    const int64_t a0 = S.catt_off[c], a1 = S.catt_off[c + 1];
     if (tid == 0) {
       // slot (high 24 bits) and attachment base (low 40) from ONE atomic, so the bases of
       // the next level ascend with the rank (the per-contig sort relies on it)
@@ -995,9 +1051,8 @@ __device__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* ab
 constexpr int kDecNT = 64;   // one wave per contig decision: no cross-wave barriers
 
 template <int PHASE>
-__global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs* __restrict__ sp, int n_act,
+__global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
                                                        int level, int64_t n_keys) {
-  const SArgs& S = *sp;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
   const int32_t* list = PHASE == 1 ? S.one_list : S.two_list;
@@ -1016,9 +1071,8 @@ __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs* __restrict__ sp, int level,
+__global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int level,
                                                           int64_t n_keys, int count) {
-  const SArgs& S = *sp;
   __shared__ Ctl ctl;
   char* base = S.k.big_ws + (int64_t)blockIdx.x * S.k.slot_bytes;
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
@@ -1063,12 +1117,11 @@ struct Buf {
 
 }  // namespace
 
-constexpr int kRing = 64;
 
 struct StagedState {
   int device = 0;
   int cus = 256;
-  Buf lut_off, lut, sargs, kargs_big, cnt, att_off, hit_contig, counters, pinned_dummy;
+  Buf lut_off, lut, cnt, att_off, counters, pinned_dummy;
   Buf att_lo, att_hi, att_loc, att_clade, att_hit, att_sc;
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
@@ -1079,10 +1132,8 @@ struct StagedState {
   int64_t dec_lds = 24 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
   unsigned long long* host_counters = nullptr;   // pinned
-  SArgs* ring = nullptr;                          // pinned argument snapshots
   ~StagedState() {
     if (host_counters) (void)hipHostFree(host_counters);
-    if (ring) (void)hipHostFree(ring);
   }
 };
 
@@ -1160,59 +1211,41 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   sa.lut_off = st->lut_off.as<int32_t>();
   sa.lut = st->lut.as<int4>();
   sa.dec_lds_bytes = st->dec_lds;
-  // argument snapshots: every upload gets its own pinned host slot and device slot, so no
-  // copy is overwritten before the stream consumed it (the previous call ended synchronised)
-  ST_TRY(st->sargs.ensure(kRing * sizeof(SArgs)));
-  if (!st->ring) {
-    ST_TRY(hipHostMalloc(reinterpret_cast<void**>(&st->ring), kRing * sizeof(SArgs)));
-  }
-  int ring_i = 0;
-  SArgs* dsa = st->sargs.as<SArgs>();
-  auto upload = [&]() -> hipError_t {
-    if (ring_i == kRing) {                 // wrap: wait until every snapshot was consumed
-      hipError_t e = hipStreamSynchronize(s);
-      if (e != hipSuccess) return e;
-      ring_i = 0;
-    }
-    st->ring[ring_i] = sa;
-    dsa = st->sargs.as<SArgs>() + ring_i;
-    return hipMemcpyAsync(dsa, st->ring + ring_i++, sizeof(SArgs), hipMemcpyHostToDevice, s);
-  };
+  // kernels take SArgs by value (kernarg segment): no argument uploads, and the pointers
+  // loaded from it are known to be global (global_* instead of flat_* memory operations)
   ST_TRY(st->counters.ensure(8 * sizeof(unsigned long long)));
   sa.counters = st->counters.as<unsigned long long>();
 
-  // contigs, hits -> attachments
-  ST_TRY(st->hit_contig.ensure((size_t)std::max<int64_t>(NH, 1) * sizeof(int32_t)));
-  ST_TRY(st->cnt.ensure((size_t)(NH + 1) * sizeof(int64_t)));
-  ST_TRY(st->cnt_leaves.ensure((size_t)(NH + 1) * sizeof(int64_t)));
-  ST_TRY(st->att_off.ensure((size_t)(NH + 1) * sizeof(int64_t)));
+  // contigs, hits -> attachments (per-contig counts, offsets, then the attachments)
+  ST_TRY(st->cnt.ensure((size_t)(N + 1) * sizeof(int64_t)));
+  ST_TRY(st->cnt_leaves.ensure((size_t)(N + 1) * sizeof(int64_t)));
+  ST_TRY(st->att_off.ensure((size_t)(N + 1) * sizeof(int64_t)));
   ST_TRY(st->red.ensure(2 * sizeof(int64_t)));
-  sa.hit_contig = st->hit_contig.as<int32_t>();
-  sa.att_off = st->att_off.as<int64_t>();
-  ST_TRY(upload());
-  hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, &dsa->k);
-  hipLaunchKernelGGL(k_hit_contig, dim3(grid_for(NH)), dim3(256), 0, s, dsa, st->hit_contig.as<int32_t>());
-  hipLaunchKernelGGL(k_att_count, dim3(grid_for(NH + 1)), dim3(256), 0, s, dsa, st->cnt.as<int64_t>(),
-                     st->cnt_leaves.as<int64_t>());
+  sa.catt_off = st->att_off.as<int64_t>();
+  const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * 32);
+  ST_TRY(hipMemsetAsync(st->red.p, 0, 2 * sizeof(int64_t), s));
+  ST_TRY(hipMemsetAsync(st->cnt.as<int64_t>() + N, 0, sizeof(int64_t), s));
+  ST_TRY(hipMemsetAsync(st->cnt_leaves.as<int64_t>() + N, 0, sizeof(int64_t), s));
+  hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, sa.k);
+  hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
+                     st->cnt_leaves.as<int64_t>(),
+                     reinterpret_cast<unsigned long long*>(st->red.as<int64_t>() + 1));
   ST_TRY(hipGetLastError());
   {
     size_t t1 = 0, t2 = 0;
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, st->cnt.as<int64_t>(),
-                                            st->att_off.as<int64_t>(), (int)(NH + 1), s));
+                                            st->att_off.as<int64_t>(), (int)(N + 1), s));
     ST_TRY(hipcub::DeviceReduce::Sum(nullptr, t2, st->cnt_leaves.as<int64_t>(),
-                                     st->red.as<int64_t>(), (int)(NH + 1), s));
+                                     st->red.as<int64_t>(), (int)(N + 1), s));
     ST_TRY(st->tmp.ensure(std::max(t1, t2)));
     size_t tb = st->tmp.n;
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, tb, st->cnt.as<int64_t>(),
-                                            st->att_off.as<int64_t>(), (int)(NH + 1), s));
+                                            st->att_off.as<int64_t>(), (int)(N + 1), s));
     tb = st->tmp.n;
     ST_TRY(hipcub::DeviceReduce::Sum(st->tmp.p, tb, st->cnt_leaves.as<int64_t>(),
-                                     st->red.as<int64_t>(), (int)(NH + 1), s));
+                                     st->red.as<int64_t>(), (int)(N + 1), s));
   }
-  ST_TRY(hipMemsetAsync(st->red.as<int64_t>() + 1, 0, sizeof(int64_t), s));
-  hipLaunchKernelGGL(k_att_max, dim3(grid_for(N)), dim3(256), 0, s, dsa,
-                     reinterpret_cast<unsigned long long*>(st->red.as<int64_t>() + 1));
-  ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + NH, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
   ST_TRY(hipStreamSynchronize(s));
   const int64_t A = hc[2], TLB = hc[3], max_att = hc[4];
@@ -1287,16 +1320,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   sa.annot_best = st->annot_best.as<uint64_t>();
   sa.big_list = st->big_list.as<int32_t>();
   sa.two_list = st->two_list.as<int32_t>();
-  ST_TRY(upload());
-  hipLaunchKernelGGL(k_att_fill, dim3(grid_for(NH)), dim3(256), 0, s, dsa);
-  if (n_annot > 0) {
+  if (n_annot > 0 && (int64_t)max_loci * k.n_sys > kAnnSlots) {   // HBM annotation slots
     ST_TRY(hipMemsetAsync(st->annot_best.p, 0, (size_t)n_annot * 8, s));
     ST_TRY(hipMemsetAsync(k.annot, 0xFF, (size_t)n_annot * 4, s));     // -1: no winner
-    if (A > 0) {
-      hipLaunchKernelGGL(k_annot, dim3(grid_for(A)), dim3(256), 0, s, dsa, A, 0);
-      hipLaunchKernelGGL(k_annot, dim3(grid_for(A)), dim3(256), 0, s, dsa, A, 1);
-    }
   }
+  hipLaunchKernelGGL(k_att_contig<1>, dim3(agrid), dim3(kAttNT), 0, s, sa, nullptr, nullptr, nullptr);
   ST_TRY(hipGetLastError());
 
   // flat explain_one applies to --weak-loci ignore/penalize and <= 64 loci per contig
@@ -1336,7 +1364,6 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     hipcub::DoubleBuffer<int32_t> vbuf(st->vals0.as<int32_t>(), st->vals1.as<int32_t>());
     sa.keys = nullptr;
     sa.vals = nullptr;
-    ST_TRY(upload());
     ST_TRY(hipMemsetAsync(st->counters.p, 0, 8 * sizeof(unsigned long long), s));
     if (n_keys > 0) {
       size_t need = st->tmp.n;
@@ -1348,44 +1375,38 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
                                                        (int)(kSortMax * 12));
           ST_TRY(attr);
         }
-        const int per_cu = std::max(1, (int)((160 * 1024) / lds));
+        const int per_cu = std::min(32, std::max(1, (int)((160 * 1024) / lds)));
         hipLaunchKernelGGL(k_sort_contig, dim3(std::min(n_act, st->cus * per_cu)), dim3(kSortNT), lds, s,
-                           dsa, n_act, level, kbuf.Current(), vbuf.Current());
+                           sa, n_act, level, kbuf.Current(), vbuf.Current());
       } else {
-        if (level == 0)
-          hipLaunchKernelGGL(k_keys_all, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys,
-                             kbuf.Current(), vbuf.Current());
-        else
-          hipLaunchKernelGGL(k_keys_active, dim3(std::min(n_act, st->cus * 8)), dim3(256), 0, s, dsa,
-                             n_act, kbuf.Current(), vbuf.Current());
+        hipLaunchKernelGGL(k_keys_active, dim3(std::min(n_act, st->cus * 8)), dim3(256), 0, s, sa,
+                           n_act, kbuf.Current(), vbuf.Current());
         ST_TRY(hipGetLastError());
         ST_TRY(hipcub::DeviceRadixSort::SortPairs(st->tmp.p, need, kbuf, vbuf, (int)n_keys, 0, end_bit, s));
       }
       ST_TRY(hipGetLastError());
       sa.keys = kbuf.Current();
       sa.vals = vbuf.Current();
-      ST_TRY(upload());
       hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa.keys, n_keys, sa.flags);
       need = st->tmp.n;
       ST_TRY(hipcub::DeviceScan::InclusiveSum(st->tmp.p, need, sa.flags, sa.seg_id, (int)n_keys, s));
-      hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
-      hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys, n_act);
+      hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys, n_act);
       if (thread_mean)
-        hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys);
+        hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
       else
-        hipLaunchKernelGGL(k_seg_rec<false>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, dsa, n_keys);
+        hipLaunchKernelGGL(k_seg_rec<false>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
       need = st->tmp.n;
       ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_nleaf, sa.leaf_off,
                                               (int)n_keys + 1, s));
-      hipLaunchKernelGGL(k_leaf_expand, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
-      hipLaunchKernelGGL(k_leaf, dim3(persistent), dim3(256), 0, s, dsa, n_keys);
-      hipLaunchKernelGGL(k_seg_combine, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
+      hipLaunchKernelGGL(k_leaf_expand, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_leaf, dim3(persistent), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_seg_combine, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
       ST_TRY(hipGetLastError());
     } else {
       sa.keys = kbuf.Current();
       sa.vals = vbuf.Current();
-      ST_TRY(upload());
     }
     if (st->dec_lds > 64 * 1024) {
       static hipError_t attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<1>),
@@ -1400,24 +1421,28 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
     if (flat_one) {
       ST_TRY(hipMemsetAsync(sa.lmax, 0, (size_t)std::max<int64_t>(NL, 1) * 8, s));
-      hipLaunchKernelGGL(k_flat_maxes, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys);
-      hipLaunchKernelGGL(k_flat_prep, dim3(grid_for(n_act)), dim3(256), 0, s, dsa, n_act, level);
-      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys, 0);
-      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, dsa, n_keys, 1);
-      hipLaunchKernelGGL(k_flat_finish, dim3(grid_for(n_act)), dim3(256), 0, s, dsa, n_act, level, n_keys);
+      hipLaunchKernelGGL(k_flat_maxes, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_flat_prep, dim3(grid_for(n_act)), dim3(256), 0, s, sa, n_act, level);
+      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys, 0);
+      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys, 1);
+      hipLaunchKernelGGL(k_flat_finish, dim3(grid_for(n_act)), dim3(256), 0, s, sa, n_act, level, n_keys);
     } else if (one_fast) {
-      hipLaunchKernelGGL(k_one, dim3(std::min<int64_t>(n_act, (int64_t)st->cus * 32)), dim3(64), 0, s, dsa,
+      hipLaunchKernelGGL(k_one, dim3(std::min<int64_t>(n_act, (int64_t)st->cus * 32)), dim3(64), 0, s, sa,
                          n_act, level, n_keys);
       hipLaunchKernelGGL(k_decide<1>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * 4)), dim3(kDecNT),
-                         (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
+                         (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     } else {
-      hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, dsa, n_act,
+      hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act,
                          level, n_keys);
     }
     // explain_two for the contigs phase 1 left open (count on the device: a grid of
     // rank-independent size, idle blocks exit at once)
-    hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * 4)), dim3(kDecNT),
-                       (size_t)st->dec_lds, s, dsa, n_act, level, n_keys);
+    // as many one-wave decision workgroups as the arena and 3 waves/SIMD (VGPRs) allow: the
+    // explain_two contigs are latency chains, so they should all be in flight at once
+    const unsigned dec_per_cu =
+        (unsigned)std::max<int64_t>(1, std::min<int64_t>(12, (160 * 1024) / std::max<int64_t>(st->dec_lds, 1)));
+    hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)), dim3(kDecNT),
+                       (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     ST_TRY(hipGetLastError());
     ST_TRY(hipMemcpyAsync(st->host_counters, st->counters.p, 4 * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, s));
@@ -1429,8 +1454,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       ST_TRY(st->big_ws.ensure((size_t)slot * slots));
       sa.k.big_ws = st->big_ws.as<char>();
       sa.k.slot_bytes = slot;
-      ST_TRY(upload());
-      hipLaunchKernelGGL(k_decide_big, dim3(slots), dim3(kBlock), 0, s, dsa, level, n_keys, n_big);
+      hipLaunchKernelGGL(k_decide_big, dim3(slots), dim3(kBlock), 0, s, sa, level, n_keys, n_big);
       ST_TRY(hipGetLastError());
       ST_TRY(hipMemcpyAsync(st->host_counters, st->counters.p, 4 * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, s));
