@@ -448,36 +448,94 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
     bool one_run = false;
     int lo = 0, hi = 0;
     double v = 0.0;
-    const int na = si.ke - si.kb;
-    if (THREAD_MEAN && si.len < kNpyBuf && nl <= kThreadLeaves) {
-      if (na == 1) {
+    int na = si.ke - si.kb;
+    const bool thread_ok = THREAD_MEAN && si.len < kNpyBuf && nl <= kThreadLeaves;
+    if (na == 1) {
+      if (thread_ok) {
         const int2 x = S.satt_lohi[si.kb];
         lo = x.x; hi = x.y; v = S.satt_sc[si.kb];
         one_run = true;
-      } else if (na <= kPruneMax) {
-        double F = 0.0;                              // best whole-locus attachment
-        for (int t = si.kb; t < si.ke; ++t) {
-          const int2 x = S.satt_lohi[t];
-          const double sc = S.satt_sc[t];
-          if (x.x <= 0 && x.y >= si.len && sc > F) F = sc;
+      }
+    } else if (THREAD_MEAN && na <= kPruneMax) {
+      double F = 0.0;                                // best whole-locus attachment
+#pragma unroll 4
+      for (int t = si.kb; t < si.ke; ++t) {
+        const int2 x = S.satt_lohi[t];
+        const double sc = S.satt_sc[t];
+        if (x.x <= 0 && x.y >= si.len && sc > F) F = sc;
+      }
+      // attachments at or below F (or empty) change no site: the envelope is
+      // max(F, the others).  None left: one run of F.  Otherwise the survivors are
+      // compacted in place, with F as one whole-locus attachment after them, so the leaf
+      // kernel sees few attachments (usually <= kRegAtt: register path).
+      int kept = 0;
+#pragma unroll 4
+      for (int t = si.kb; t < si.ke; ++t) {
+        const int2 x = S.satt_lohi[t];
+        const double sc = S.satt_sc[t];
+        if (x.x < x.y && sc > F) {
+          if (kept != t - si.kb) { S.satt_lohi[si.kb + kept] = x; S.satt_sc[si.kb + kept] = sc; }
+          ++kept;
         }
-        bool dom = true;                             // nothing else rises above it
-        for (int t = si.kb; t < si.ke && dom; ++t) {
-          const int2 x = S.satt_lohi[t];
-          if (x.x < x.y && S.satt_sc[t] > F) dom = false;
+      }
+      if (kept == 0 && thread_ok) {
+        lo = 0; hi = si.len; v = F; one_run = true;
+      } else {
+        // F > 0 came from an attachment that was not kept (its score is F), so the list
+        // never grows; it may have shifted, so F is always re-appended
+        if (F > 0.0) {
+          S.satt_lohi[si.kb + kept] = make_int2(0, si.len);
+          S.satt_sc[si.kb + kept] = F;
+          ++kept;
         }
-        if (dom) { lo = 0; hi = si.len; v = F; one_run = true; }
+        na = kept;
       }
     }
     if (one_run) {
+      // Three uniform phases instead of one leaf formula per loop trip (the lanes of a wave
+      // would otherwise run every leaf kind on every trip):
+      //  A. classify the leaves against the run: at most two straddle a run boundary, the
+      //     ones inside have at most 4 distinct lengths (numpy's split of one buffer);
+      //  B. the <= 2 boundary leaves by run_leaf, each inside length once (8 equal
+      //     accumulators: 8 * seqsum, exact doubling, then the tail in order);
+      //  C. the tree, picking each leaf's value (outside leaves are 0).
       const int4* lt = S.lut + S.lut_off[si.len];
-      SumStack stk;
-      int4 e = lt[0];
+      hi = max(hi, lo);
+      int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
+      int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
       for (int q = 0; q < nl; ++q) {
-        const int4 cur = e;
-        if (q + 1 < nl) e = lt[q + 1];               // next leaf's entry in flight
-        stk.push(run_leaf(lo, hi, v, cur.x, cur.y));
-        for (int a = 0; a < cur.z; ++a) stk.add_top();
+        const int4 e = lt[q];
+        const int le = e.x + e.y;
+        const bool in = lo <= e.x && le <= hi && lo < hi;
+        const bool out = le <= lo || e.x >= hi || lo >= hi;
+        if (!in && !out) {
+          if (pst0 < 0) { pst0 = e.x; pln0 = e.y; } else { pst1 = e.x; pln1 = e.y; }
+        } else if (in && e.y != L0 && e.y != L1 && e.y != L2 && e.y != L3) {
+          if (L0 < 0) L0 = e.y; else if (L1 < 0) L1 = e.y; else if (L2 < 0) L2 = e.y; else L3 = e.y;
+        }
+      }
+      const double vp0 = pst0 >= 0 ? run_leaf(lo, hi, v, pst0, pln0) : 0.0;
+      const double vp1 = pst1 >= 0 ? run_leaf(lo, hi, v, pst1, pln1) : 0.0;
+      auto inside = [&](int ln) -> double {
+        if (ln < 0) return 0.0;
+        double b = 0.0;
+        for (int i = 0; i < (ln >> 3); ++i) b += v;
+        double res = 8.0 * b;
+        for (int x = ln & ~7; x < ln; ++x) res += v;
+        return res;
+      };
+      const double V0 = inside(L0), V1 = inside(L1), V2 = inside(L2), V3 = inside(L3);
+      SumStack stk;
+      for (int q = 0; q < nl; ++q) {
+        const int4 e = lt[q];
+        const int le = e.x + e.y;
+        const bool in = lo <= e.x && le <= hi && lo < hi;
+        const bool out = le <= lo || e.x >= hi || lo >= hi;
+        double x = 0.0;
+        if (in) x = e.y == L0 ? V0 : e.y == L1 ? V1 : e.y == L2 ? V2 : V3;
+        else if (!out) x = e.x == pst0 ? vp0 : vp1;
+        stk.push(x);
+        for (int a = 0; a < e.z; ++a) stk.add_top();
       }
       S.seg_mean[s] = (0.0 + stk.s0) / (double)si.len;
       nl = 0;
