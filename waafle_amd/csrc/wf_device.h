@@ -1098,6 +1098,34 @@ __device__ __forceinline__ int decide_prologue(const KArgs& K, const Contig& C, 
   const int tid = threadIdx.x;
   const DevParams& P = K.p;
   const int G = C.G;
+  if (NT == 64 && G <= 64) {
+    // one wave, lane g owns locus g: a column max over the clade rows (no atomics, no
+    // index division), the unmasked-locus list by ballot
+    bool root = false;
+    for (int p = tid; p < Pn; p += NT) root |= C.cl_id[p] == K.root;
+    double m = 0.0;
+    if (tid < G)
+      for (int p = 0; p < Pn; ++p) {
+        const double v = C.S[(int64_t)p * G + tid];
+        if (C.cl_id[p] != K.unknown && v > m) m = v;
+      }
+    int ig = 0;
+    if (tid < G) {
+      if (P.weak == 0) ig = !(m >= P.kmin);
+      else if (P.weak == 2) C.S[(int64_t)ctl.p_unk * G + tid] = 1.0 - m;
+      C.ign[tid] = ig;
+      C.maxes[tid] = dbits(m);
+    }
+    const uint64_t keep = __ballot(tid < G && !ig);
+    if (tid < G && !ig) C.um[__popcll(keep & ((1ull << tid) - 1ull))] = tid;
+    const bool any_root = __ballot(root) != 0ull;
+    if (tid == 0) {
+      ctl.root_present = any_root ? 1 : 0;
+      ctl.Gu = __popcll(keep);
+      ctl.all_ignored = keep == 0ull;
+    }
+    __syncthreads();
+  } else {
   for (int g = tid; g < G; g += NT) C.maxes[g] = 0;
   if (tid == 0) ctl.root_present = 0;
   __syncthreads();
@@ -1124,6 +1152,7 @@ __device__ __forceinline__ int decide_prologue(const KArgs& K, const Contig& C, 
     ctl.all_ignored = (Gu == 0);
   }
   __syncthreads();
+  }
   STAMP(9);
   const int Gu = ctl.Gu;
   if (first) {
@@ -1226,19 +1255,6 @@ __device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& 
   const int G = C.G;
   const int Gu = ctl.Gu;
   (void)w; (void)NW;
-  if (P.sister_on) {                     // sister checks read listed parents per clade
-    for (int q = tid; q < Pn; q += NT) {
-      C.sib_of[q] = K.sibp[C.cl_id[q]];
-      if (C.hm) {
-        const double* row = C.S + (int64_t)q * G;
-        uint64_t m = 0;
-        for (int g = 0; g < G; ++g)
-          if (row[g] >= P.sister_thr) m |= 1ull << g;
-        C.hm[q] = m;
-      }
-    }
-    __syncthreads();
-  }
   // ================= explain_two (orgscorer.py:599-619) ============================
   {
     // potential clades: max over ALL loci >= k2 (:603-605)
@@ -1293,6 +1309,19 @@ __device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& 
     STAMP(18);
     bool have_ok = false;
     if (bk >= 0) {
+      if (P.sister_on) {                 // sister checks read listed parents per clade
+        for (int q = tid; q < Pn; q += NT) {
+          C.sib_of[q] = K.sibp[C.cl_id[q]];
+          if (C.hm) {
+            const double* row = C.S + (int64_t)q * G;
+            uint64_t m = 0;
+            for (int g = 0; g < G; ++g)
+              if (row[g] >= P.sister_thr) m |= 1ull << g;
+            C.hm[q] = m;
+          }
+        }
+        __syncthreads();
+      }
       const int bi = (int)(bk / Pp), bj = (int)(bk % Pp);
       for (int i = tid; i < (Pn + 31) / 32; i += NT) { C.bm1[i] = 0; C.bm2[i] = 0; }
       if (tid == 0) {

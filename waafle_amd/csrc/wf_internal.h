@@ -73,6 +73,7 @@ struct SArgs {
   int32_t* leaf_off;             // [segments + 1] exclusive scan of seg_nleaf
   int32_t* leaf_seg;             // [leaves] segment of each leaf
   int4* seg_rec;                 // [segments] (first sorted attachment, count, locus length, leaves)
+  int32_t* wave_list;            // segments for k_seg_wave (counters[7])
   int2* seg_cg;                  // [segments] (clade, locus)
   int32_t* crank_first;          // [active + 1] first segment of each active contig
   // flat explain_one (weak loci ignore/penalize, <= 64 loci)

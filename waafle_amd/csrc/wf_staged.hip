@@ -441,11 +441,11 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s > n_keys) return;
   int nl = 0;
+  bool one_run = false, to_wave = false;
   if (s < seg_count(S, n_keys)) {
     const SegInfo si = seg_info(S, (int)s);
     nl = (si.len / kNpyBuf) * lut_count(S, kNpyBuf) + lut_count(S, si.len % kNpyBuf);
     S.seg_cg[s] = make_int2((int)((S.keys[si.kb] >> S.key_lb) & ((1ull << S.key_tb) - 1)), si.g);
-    bool one_run = false;
     int lo = 0, hi = 0;
     double v = 0.0;
     int na = si.ke - si.kb;
@@ -541,9 +541,116 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
       nl = 0;
     } else {
       S.seg_rec[s] = make_int4(si.kb, na, si.len, nl);
+      // many attachments (higher roll-up levels): one wave per segment (k_seg_wave)
+      to_wave = THREAD_MEAN && na > kRegAtt && na <= 64 && nl <= 64 && si.len < kNpyBuf;
+      if (to_wave) nl = 0;
     }
   }
   S.seg_nleaf[s] = nl;
+  const uint64_t bm = __ballot(to_wave);            // one list append per wave
+  if (bm) {
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(bm);
+    int base = 0;
+    if (lane == leader) base = (int)atomicAdd(&S.counters[7], (unsigned long long)__popcll(bm));
+    base = __shfl(base, leader, 64);
+    if (to_wave) S.wave_list[base + __popcll(bm & ((1ull << lane) - 1ull))] = (int)s;
+  }
+}
+
+// Segments with 5..64 attachments, one wave each: the max-envelope is swept once into runs
+// (lane i holds attachment i; run value = wave max over the covering ones, run end = wave
+// min over the next boundaries), then lane q evaluates leaf q from the runs -- each of the
+// eight stride accumulators adds its sites in site order, a run of value v contributing v
+// k_c times (zero runs add nothing: x + 0.0 = x for x >= 0) -- and lane 0 folds the leaves
+// in tree order.  Same sums as k_leaf's per-leaf stride walks, without rescanning the
+// attachments for every run of every leaf.
+constexpr int kWaveRuns = 2 * 64 + 2;
+
+__global__ __launch_bounds__(64) void k_seg_wave(const SArgs S) {
+  __shared__ int r_lo[kWaveRuns], r_hi[kWaveRuns];
+  __shared__ double r_v[kWaveRuns];
+  __shared__ double s_lv[64];
+  __shared__ int s_z[64];
+  const int lane = threadIdx.x;
+  const int count = (int)S.counters[7];
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int s = S.wave_list[i];
+    const int4 rec = S.seg_rec[s];                  // (kb, attachments, length, leaves)
+    const int len = rec.z, nl = rec.w;
+    int lo = 0, hi = 0;
+    double sc = 0.0;
+    if (lane < rec.y) {
+      const int2 x = S.satt_lohi[rec.x + lane];
+      if (x.x < x.y) { lo = x.x; hi = x.y; sc = S.satt_sc[rec.x + lane]; }
+    }
+    int nr = 0;
+    for (int x = 0; x < len;) {                     // wave-uniform sweep
+      double v = (lo <= x && x < hi) ? sc : 0.0;
+      int nb = len;
+      if (lo < hi) {
+        if (lo > x) nb = lo;
+        else if (hi > x) nb = hi;
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const double v2 = __shfl_xor(v, off, 64);
+        const int n2 = __shfl_xor(nb, off, 64);
+        v = v2 > v ? v2 : v;
+        nb = n2 < nb ? n2 : nb;
+      }
+      if (v > 0.0) {
+        if (lane == 0) { r_lo[nr] = x; r_hi[nr] = nb; r_v[nr] = v; }
+        ++nr;
+      }
+      x = nb;
+    }
+    __syncthreads();
+    const int4* lt = S.lut + S.lut_off[len];
+    int4 e = make_int4(0, 0, 0, 0);
+    if (lane < nl) {
+      e = lt[lane];
+      const int st = e.x, ln = e.y, m = ln >> 3, be = st + (m << 3);
+      int j = 0;
+      while (j < nr && r_hi[j] <= st) ++j;
+      double r[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) r[c] = 0.0;
+      for (int jj = j; jj < nr && r_lo[jj] < be; ++jj) {
+        const int a = max(r_lo[jj], st), b = min(r_hi[jj], be);
+        const double v = r_v[jj];
+        int k[8], kmin = m;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          k[c] = below(st + c, b, m) - below(st + c, a, m);
+          kmin = min(kmin, k[c]);
+        }
+        for (int q = 0; q < kmin; ++q) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) r[c] += v;
+        }
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (k[c] > kmin) r[c] += v;
+      }
+      double res = m > 0 ? leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]) : 0.0;
+      for (int x = be; x < st + ln; ++x) {          // tail sites, in order
+        while (j < nr && r_hi[j] <= x) ++j;
+        res += (j < nr && r_lo[j] <= x) ? r_v[j] : 0.0;
+      }
+      s_lv[lane] = res;
+      s_z[lane] = e.z;
+    }
+    __syncthreads();
+    if (lane == 0) {
+      SumStack stk;
+      for (int q = 0; q < nl; ++q) {
+        stk.push(s_lv[q]);
+        for (int a = 0; a < s_z[q]; ++a) stk.add_top();
+      }
+      S.seg_mean[s] = (0.0 + stk.s0) / (double)len;
+    }
+    __syncthreads();
+  }
 }
 
 // leaf j of a segment: (start within the locus, length)
@@ -1183,7 +1290,7 @@ struct StagedState {
   Buf att_lo, att_hi, att_loc, att_clade, att_hit, att_sc;
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
-  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc;
+  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list;
   Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
   Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp;
   bool lut_ready = false;
@@ -1331,6 +1438,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->seg_nleaf.ensure((A1 + 1) * 4)); ST_TRY(st->leaf_off.ensure((A1 + 1) * 4));
   ST_TRY(st->leaf_seg.ensure(T1 * 4)); ST_TRY(st->leaf_val.ensure(T1 * 8));
   ST_TRY(st->seg_rec.ensure(A1 * 16)); ST_TRY(st->seg_cg.ensure(A1 * 8));
+  ST_TRY(st->wave_list.ensure(A1 * 4));
   ST_TRY(st->crank_first.ensure(((size_t)N + 1) * 4));
   ST_TRY(st->lmax.ensure((size_t)std::max<int64_t>(NL, 1) * 8));
   ST_TRY(st->c_gu.ensure((size_t)N * 4)); ST_TRY(st->c_umask.ensure((size_t)N * 8));
@@ -1378,6 +1486,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   sa.annot_best = st->annot_best.as<uint64_t>();
   sa.big_list = st->big_list.as<int32_t>();
   sa.two_list = st->two_list.as<int32_t>();
+  sa.wave_list = st->wave_list.as<int32_t>();
   if (n_annot > 0 && (int64_t)max_loci * k.n_sys > kAnnSlots) {   // HBM annotation slots
     ST_TRY(hipMemsetAsync(st->annot_best.p, 0, (size_t)n_annot * 8, s));
     ST_TRY(hipMemsetAsync(k.annot, 0xFF, (size_t)n_annot * 4, s));     // -1: no winner
@@ -1451,8 +1560,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
       hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
       hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys, n_act);
-      if (thread_mean)
+      if (thread_mean) {
         hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
+        hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 8), dim3(64), 0, s, sa);
+      }
       else
         hipLaunchKernelGGL(k_seg_rec<false>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
       need = st->tmp.n;
