@@ -19,8 +19,8 @@ NAMES = {0: "loci+leaf counts", 1: "attach count+scan", 2: "leaf tables+attach f
          11: "meld_one+write", 12: "two: pass 2 + meld", 20: "contigs (count)", 21: "levels (count)",
          22: "site: classify segments", 23: "site: 8-lane groups", 24: "site: 16-lane groups",
          25: "site: 32-lane groups", 26: "site: 64-lane groups", 16: "two: potential scan",
-         17: "two: masks", 18: "two: pass 1 (best pair)"}
-PHASES = list(range(13)) + list(range(16, 19)) + list(range(22, 27))
+         17: "two: masks", 18: "two: pass 1 (best pair)", 19: "roll-up re-key (staged)"}
+PHASES = list(range(13)) + list(range(16, 20)) + list(range(22, 27))
 LAPS = {13: "round: load segment+atts", 14: "round: leaf value", 15: "round: combine+store"}
 COUNTS = {27: "segments in 8-lane class", 28: "segments in 16-lane class",
           29: "segments in 32-lane class", 30: "segments in 64-lane class",

@@ -982,6 +982,7 @@ __device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int
   const bool unk = C.cl_id[pa] == K.unknown || C.cl_id[pb] == K.unknown;
   OptEval e;
   e.swapped = 0;
+#pragma unroll 8
   for (int g = 0; g < G; ++g) {  // "^[^A]*B" -> swap (orgscorer.py:537-540)
     uint8_t c = two_char(K, C, pa, pb, unk, g);
     if (c == 'A') break;
@@ -997,6 +998,7 @@ __device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int
   bool dir_ok = true;
   int64_t tot = 0, amb = 0;
   e.same = 1;
+#pragma unroll 8
   for (int g = 0; g < G; ++g) {
     uint8_t c = fin(g);
     if (out) out[g] = c;
@@ -1074,6 +1076,7 @@ __device__ __forceinline__ double pair_crit(const Contig& C, int pa, int pb, int
   const double* ra = C.S + (int64_t)pa * C.G;
   const double* rb = C.S + (int64_t)pb * C.G;
   double m = 0.0;
+#pragma unroll 8
   for (int u = 0; u < Gu; ++u) {
     double a = ra[C.um[u]], b = rb[C.um[u]];
     double x = a < b ? b : a;
@@ -1105,6 +1108,7 @@ __device__ __forceinline__ int decide_prologue(const KArgs& K, const Contig& C, 
     for (int p = tid; p < Pn; p += NT) root |= C.cl_id[p] == K.root;
     double m = 0.0;
     if (tid < G)
+#pragma unroll 8
       for (int p = 0; p < Pn; ++p) {
         const double v = C.S[(int64_t)p * G + tid];
         if (C.cl_id[p] != K.unknown && v > m) m = v;
@@ -1264,6 +1268,7 @@ __device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& 
     auto potential = [&](int p) -> bool {
       const double* row = C.S + (int64_t)p * G;
       double mx = row[0];
+#pragma unroll 8
       for (int g = 1; g < G; ++g) mx = row[g] > mx ? row[g] : mx;
       return mx >= P.k2;
     };
@@ -1282,6 +1287,7 @@ __device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& 
       for (int i = tid; i < Pp; i += NT) {
         const double* row = C.S + (int64_t)C.pot[i] * G;
         uint64_t m = 0;
+#pragma unroll 8
         for (int u = 0; u < Gu; ++u)
           if (row[C.um[u]] >= P.k2) m |= 1ull << u;
         C.mask[i] = m;

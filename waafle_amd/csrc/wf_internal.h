@@ -93,6 +93,8 @@ struct SArgs {
   const int4* lut;               // (start, length, parent adds) per leaf
   int64_t dec_lds_bytes;         // LDS arena of the decision workgroup
   int sort_cap;                  // per-contig LDS sort capacity (power of 2; 0: device radix sort)
+  const unsigned long long* in_counts;   // this level's counts on the device (null: the
+                                         // kernel arguments are exact)
 };
 
 struct StagedState;

@@ -55,6 +55,17 @@ __device__ __forceinline__ int lower_bound_i32(const int32_t* a, int n, int x) {
   return lo;
 }
 
+// Counts of the current level: from the host (kernel arguments) when it knows them, else
+// from the previous level's device counter word (rank slots << 40 | attachments) -- the
+// pipelined levels (staged_score) enqueue a level before the host has read that word.
+__device__ __forceinline__ void lvl_counts(const SArgs& S, int& n_act, int64_t& n_keys) {
+  if (S.in_counts) {
+    const unsigned long long v = *S.in_counts;
+    n_act = (int)(v >> 40);
+    n_keys = (int64_t)(v & ((1ull << 40) - 1));
+  }
+}
+
 __device__ __forceinline__ int seg_count(const SArgs& S, int64_t n_keys) {
   return n_keys > 0 ? S.seg_id[n_keys - 1] : 0;
 }
@@ -295,6 +306,8 @@ constexpr int kSortMax = 4096;   // 48 KiB of LDS; larger contigs (cfg5 stress) 
 
 __global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_act,
                                                           int level, uint64_t* keys, int32_t* vals) {
+  int64_t n_keys_ = 0;
+  lvl_counts(S, n_act, n_keys_);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem);
   int32_t* sv = reinterpret_cast<int32_t*>(sk + S.sort_cap);
@@ -334,12 +347,16 @@ __global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_ac
   }
 }
 
-__global__ void k_seg_flags(const uint64_t* keys, int64_t n, int32_t* flags) {
+__global__ void k_seg_flags(const SArgs S, int64_t n) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) flags[i] = (i == 0 || keys[i] != keys[i - 1]) ? 1 : 0;
+  if (i < n) S.flags[i] = (i == 0 || S.keys[i] != S.keys[i - 1]) ? 1 : 0;
 }
 
 __global__ void k_segs(const SArgs S, int64_t n) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (S.flags[i]) {
@@ -353,6 +370,7 @@ __global__ void k_segs(const SArgs S, int64_t n) {
 // crank_first[cr] = first segment of active contig cr (segments are sorted by rank; ranks
 // without segments get the next rank's start), crank_first[n_act] = segment count.
 __global__ void k_crank_first(const SArgs S, int64_t n_keys, int n_act) {
+  lvl_counts(S, n_act, n_keys);
   const int ns = seg_count(S, n_keys);
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s > ns) return;
@@ -363,6 +381,8 @@ __global__ void k_crank_first(const SArgs S, int64_t n_keys, int n_act) {
 
 // Attachments copied into sorted order, so each segment's are contiguous.
 __global__ void k_gather(const SArgs S, int64_t n) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n);
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int a = S.vals[i];
@@ -438,6 +458,8 @@ __device__ __forceinline__ double run_leaf(int lo, int hi, double v, int st, int
 
 template <bool THREAD_MEAN>
 __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n_keys);
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s > n_keys) return;
   int nl = 0;
@@ -664,6 +686,8 @@ __device__ __forceinline__ int2 leaf_span(const SArgs& S, int len, int j) {
 }
 
 __global__ void k_leaf_expand(const SArgs S, int64_t n_keys) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n_keys);
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= seg_count(S, n_keys)) return;
   const int o = S.leaf_off[s], n = S.seg_nleaf[s];
@@ -676,6 +700,8 @@ __global__ void k_leaf_expand(const SArgs S, int64_t n_keys) {
 // combined as ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)) with xor shuffles (float addition is
 // commutative, so the result is exact).  Wave-uniform loop: every lane runs the same trips.
 __global__ void k_leaf(const SArgs S, int64_t n_keys) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n_keys);
   const int ns = seg_count(S, n_keys);
   const int TL = S.leaf_off[ns];
   const SortedSrc src{S.satt_lohi, S.satt_sc};
@@ -725,6 +751,8 @@ __global__ void k_leaf(const SArgs S, int64_t n_keys) {
 }
 
 __global__ void k_seg_combine(const SArgs S, int64_t n_keys) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n_keys);
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= seg_count(S, n_keys) || S.seg_nleaf[s] == 0) return;   // 0: mean done in k_seg_rec
   const int len = S.seg_rec[s].z;
@@ -931,6 +959,7 @@ constexpr int kOneCap = 384;
 
 __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
                                             int64_t n_keys) {
+  lvl_counts(S, n_act, n_keys);
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   __shared__ int2 s_cg[kOneCap];
@@ -1201,7 +1230,24 @@ __device__ __forceinline__ bool decide_contig(const SArgs& S, int c, int cr, int
       S.act_base_next[slot] = (int64_t)(old & ((1ull << 40) - 1));
       K.pair_evals[c] = pair_evals;
     }
-    for (int64_t a = a0 + tid; a < a1; a += NT) S.att_clade[a] = K.parent[S.att_clade[a]];
+    // re-key to the parent clade, 4 attachments per lane in flight (two dependent loads each)
+    for (int64_t ab = a0; ab < a1; ab += 4 * NT) {
+      int cl[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t a = ab + r * NT + tid;
+        cl[r] = a < a1 ? S.att_clade[a] : 0;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cl[r] = K.parent[cl[r]];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t a = ab + r * NT + tid;
+        if (a < a1) S.att_clade[a] = cl[r];
+      }
+    }
+    STAMP_SYNC();
+    STAMP(19);
     return true;
   }
   if (tid == 0) {                                // unclassified after evaluation
@@ -1218,6 +1264,7 @@ constexpr int kDecNT = 64;   // one wave per contig decision: no cross-wave barr
 template <int PHASE>
 __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
                                                        int level, int64_t n_keys) {
+  lvl_counts(S, n_act, n_keys);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
   const int32_t* list = PHASE == 1 ? S.one_list : S.two_list;
@@ -1238,6 +1285,9 @@ __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
 
 __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int level,
                                                           int64_t n_keys, int count) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n_keys);
+  count = (int)S.counters[2];
   __shared__ Ctl ctl;
   char* base = S.k.big_ws + (int64_t)blockIdx.x * S.k.slot_bytes;
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
@@ -1246,6 +1296,19 @@ __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int lev
     if (!ok && threadIdx.x == 0) S.k.status[c] = WF_E_NOMEM;
     __syncthreads();
   }
+}
+
+// Upper bound of decide_contig's arena for P clade rows (segments + 1) and G loci: every
+// take() of decide_contig with its 16-byte alignment, plus the mask-class workspace.
+int64_t arena_bound(int64_t P, int64_t G) {
+  int64_t cls = 0;
+  if (P >= kClsMin) {
+    int64_t n2 = 1;
+    while (n2 < P) n2 <<= 1;
+    cls = n2 * 8 + (P + 1) * 4 + kClsMaxPairs * 8 + (kClsMaxPairs + 1) * 8 + 64;
+  }
+  return 20 * 16 + P * (4 + 4 + 8 + 4 + 4 + 4 + 8 + 4) + 8 * P * G + G * (8 + 4 + 4 + 1 + 4) +
+         8 * (P / 32 + 2) + cls;
 }
 
 int bits_for(int64_t v) {   // bits to hold values 0..v
@@ -1290,7 +1353,10 @@ struct StagedState {
   Buf att_lo, att_hi, att_loc, att_clade, att_hit, att_sc;
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
-  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list;
+  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list, lvl_ctr;
+  unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
+  hipEvent_t lvl_ev[2] = {nullptr, nullptr};
+  int big_slots = 512;
   Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
   Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp;
   bool lut_ready = false;
@@ -1299,6 +1365,9 @@ struct StagedState {
   unsigned long long* host_counters = nullptr;   // pinned
   ~StagedState() {
     if (host_counters) (void)hipHostFree(host_counters);
+    if (host_lvl) (void)hipHostFree(host_lvl);
+    for (hipEvent_t e : lvl_ev)
+      if (e) (void)hipEventDestroy(e);
   }
 };
 
@@ -1309,6 +1378,11 @@ StagedState* staged_create(int device) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) st->cus = prop.multiProcessorCount;
   if (hipHostMalloc(reinterpret_cast<void**>(&st->host_counters), 8 * sizeof(unsigned long long)) != hipSuccess)
     st->host_counters = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&st->host_lvl), (kMaxIter + 2) * sizeof(unsigned long long)) !=
+      hipSuccess)
+    st->host_lvl = nullptr;
+  for (hipEvent_t& e : st->lvl_ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
   return st;
 }
 
@@ -1358,7 +1432,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   const int N = k.n_contigs;
   if (N <= 0) return 0;
   g_sync_stream = s;
-  if (!st->host_counters) { *err = "pinned host allocation failed"; return -2; }
+  if (!st->host_counters || !st->host_lvl || !st->lvl_ev[0] || !st->lvl_ev[1]) {
+    *err = "pinned host allocation / event creation failed";
+    return -2;
+  }
   int rc = build_lut(st, s, err);
   if (rc) return rc;
   int64_t* hc = reinterpret_cast<int64_t*>(st->host_counters);   // pinned
@@ -1516,9 +1593,27 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   // k_leaf grid: blocks per CU (WF_LEAF_GRID overrides; measurement aid)
   static const char* lg_env = getenv("WF_LEAF_GRID");
   const unsigned persistent = (unsigned)st->cus * (lg_env ? (unsigned)atoi(lg_env) : 8u);
+  // Level counters: level L counts into block L; level L+1 reads block L's word 0.  Level 0
+  // and the radix-sort path run synchronously (the host reads the counts after each level).
+  // Optionally, with the per-contig sort, levels >= 1 are pipelined: the host enqueues level L+1 with
+  // upper-bound grids (active sets only shrink) and the kernels read the real counts on the
+  // device, while the host waits for level L-1's count word -- the GPU never idles on a
+  // host round trip, and one empty level is enqueued at the end.
+  const int n_lv = kMaxIter + 2;
+  ST_TRY(st->lvl_ctr.ensure((size_t)n_lv * 8 * sizeof(unsigned long long)));
+  ST_TRY(hipMemsetAsync(st->lvl_ctr.p, 0, (size_t)n_lv * 8 * sizeof(unsigned long long), s));
+  unsigned long long* lvl_ctr = st->lvl_ctr.as<unsigned long long>();
+  // Measured on cfg2: the host round trips it removes (~0.1 ms per pass) are paid back by
+  // the trailing empty level and the always-launched HBM-slot kernel, so it is opt-in
+  // (WF_PIPELINE=1) until a level has fewer launches.
+  static const char* pipe_env = getenv("WF_PIPELINE");
+  const bool pipelined = sa.sort_cap > 0 && !flat_one && pipe_env && pipe_env[0] == '1';
   int n_act = N;
   int64_t n_keys = A;
-  for (int level = 0; n_act > 0; ++level) {
+  for (int level = 0; n_act > 0 && level <= kMaxIter; ++level) {
+    const bool async = pipelined && level >= 1;
+    sa.counters = lvl_ctr + 8 * level;
+    sa.in_counts = async ? lvl_ctr + 8 * (level - 1) : nullptr;
     const int cur = level & 1;
     sa.act = level == 0 ? nullptr : act[cur]->as<int32_t>();
     sa.act_base = level == 0 ? nullptr : base[cur]->as<int64_t>();
@@ -1531,7 +1626,6 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     hipcub::DoubleBuffer<int32_t> vbuf(st->vals0.as<int32_t>(), st->vals1.as<int32_t>());
     sa.keys = nullptr;
     sa.vals = nullptr;
-    ST_TRY(hipMemsetAsync(st->counters.p, 0, 8 * sizeof(unsigned long long), s));
     if (n_keys > 0) {
       size_t need = st->tmp.n;
       if (sa.sort_cap > 0) {
@@ -1554,7 +1648,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       ST_TRY(hipGetLastError());
       sa.keys = kbuf.Current();
       sa.vals = vbuf.Current();
-      hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa.keys, n_keys, sa.flags);
+      hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
       need = st->tmp.n;
       ST_TRY(hipcub::DeviceScan::InclusiveSum(st->tmp.p, need, sa.flags, sa.seg_id, (int)n_keys, s));
       hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
@@ -1613,7 +1707,20 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)), dim3(kDecNT),
                        (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     ST_TRY(hipGetLastError());
-    ST_TRY(hipMemcpyAsync(st->host_counters, st->counters.p, 4 * sizeof(unsigned long long),
+    if (async) {
+      // HBM-slot decisions on the device count (slots sized for the largest contig)
+      hipLaunchKernelGGL(k_decide_big, dim3(st->big_slots), dim3(kBlock), 0, s, sa, level, n_keys, 0);
+      ST_TRY(hipGetLastError());
+      ST_TRY(hipMemcpyAsync(st->host_lvl + level, sa.counters, sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, s));
+      ST_TRY(hipEventRecord(st->lvl_ev[level & 1], s));
+      if (level >= 2) {                 // level `level`'s own count, produced by level - 1
+        ST_TRY(hipEventSynchronize(st->lvl_ev[(level - 1) & 1]));
+        if ((st->host_lvl[level - 1] >> 40) == 0) break;   // this level was empty: done
+      }
+      continue;                         // n_act / n_keys stay the upper bounds
+    }
+    ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, s));
     ST_TRY(hipStreamSynchronize(s));
     const int n_big = (int)st->host_counters[2];
@@ -1625,7 +1732,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       sa.k.slot_bytes = slot;
       hipLaunchKernelGGL(k_decide_big, dim3(slots), dim3(kBlock), 0, s, sa, level, n_keys, n_big);
       ST_TRY(hipGetLastError());
-      ST_TRY(hipMemcpyAsync(st->host_counters, st->counters.p, 4 * sizeof(unsigned long long),
+      ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, s));
       ST_TRY(hipStreamSynchronize(s));
     }
@@ -1633,7 +1740,16 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       st->dec_lds += 8 * 1024;   // adaptive arena: grows while > 2% of contigs overflow
     n_act = (int)(st->host_counters[0] >> 40);
     n_keys = (int64_t)(st->host_counters[0] & ((1ull << 40) - 1));
+    if (pipelined && level == 0 && n_act > 0) {
+      // HBM decision slots for the pipelined levels, sized for the largest possible contig
+      const int64_t slot = (arena_bound(max_att + 2, max_loci) + 255) & ~int64_t(255);
+      st->big_slots = st->cus * 2;
+      ST_TRY(st->big_ws.ensure((size_t)slot * st->big_slots));
+      sa.k.big_ws = st->big_ws.as<char>();
+      sa.k.slot_bytes = slot;
+    }
   }
+  if (pipelined) ST_TRY(hipStreamSynchronize(s));
   return 0;
 }
 
