@@ -35,7 +35,7 @@ def parse_args():
     ap.add_argument("--lds-bytes", type=int, default=None)
     ap.add_argument("--threads", type=int, default=None, help="threads per contig (64/128/256)")
     ap.add_argument("--mode", default="staged", choices=["staged", "fused"])
-    ap.add_argument("--cpu-sample", type=int, default=1500,
+    ap.add_argument("--cpu-sample", type=int, default=6000,
                     help="contigs timed on the CPU oracle (rank 0, N=1); 0 disables")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_cfg2.json"))
     return ap.parse_args()
