@@ -76,6 +76,7 @@ struct SArgs {
   int32_t* wave_list;            // segments for k_seg_wave (counters[7])
   int2* seg_cg;                  // [segments] (clade, locus)
   int32_t* crank_first;          // [active + 1] first segment of each active contig
+  int32_t* seg_cnt;              // [active + 1] segments per active contig (per-contig sort)
   // flat explain_one (weak loci ignore/penalize, <= 64 loci)
   uint64_t* lmax;                // [n_loci] per-locus max score bits over known clades
   int32_t* c_gu;                 // [active] unmasked loci (-1: contig needs no decision)

@@ -242,7 +242,6 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* c
         for (int i = 0; i < kAttNT / 64; ++i) { ta += s_red[0][i]; tb += s_red[1][i]; }
         ccnt[c] = ta;
         cleaves[c] = tb;
-        if (ta > 0) atomicMax(cmax, (unsigned long long)ta);
       }
       __syncthreads();
       continue;
@@ -316,7 +315,10 @@ __global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_ac
     const int c = S.act ? S.act[cr] : cr;
     const int64_t a0 = S.catt_off[c], a1 = S.catt_off[c + 1];
     const int n = (int)(a1 - a0);
-    if (n == 0) continue;
+    if (n == 0) {
+      if (tid == 0) S.seg_cnt[cr] = 0;
+      continue;
+    }
     const int64_t base = level == 0 ? a0 : S.act_base[cr];
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
@@ -339,11 +341,58 @@ __global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_ac
         __syncthreads();
       }
     }
+    int ns = 0;                                      // distinct keys = segments
     for (int t = tid; t < n; t += kSortNT) {
       keys[base + t] = sk[t];
       vals[base + t] = sv[t];
+      ns += (t == 0 || sk[t] != sk[t - 1]) ? 1 : 0;
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off, 64);
+    if (tid == 0) S.seg_cnt[cr] = ns;
     __syncthreads();
+  }
+  if (blockIdx.x == 0 && tid == 0) S.seg_cnt[n_act] = 0;   // exclusive scan -> crank_first
+}
+
+// Segments of each contig from its sorted keys (one wave per contig), at the contig's
+// offset from the scan of per-contig segment counts: segment starts and ranks, the
+// attachments gathered into sorted order, the rank -> first segment map and the segment
+// total.  Replaces the flag / scan / segment / gather / rank-map kernels of the radix path.
+__global__ __launch_bounds__(64) void k_seg_build(const SArgs S, int n_act, int level, int64_t n_keys) {
+  lvl_counts(S, n_act, n_keys);
+  const int lane = threadIdx.x;
+  if (blockIdx.x == 0 && lane == 0 && n_keys > 0) {
+    const int total = S.crank_first[n_act];
+    S.seg_start[total] = (int)n_keys;
+    S.seg_id[n_keys - 1] = total;                    // seg_count()
+  }
+  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const int c = S.act ? S.act[cr] : cr;
+    const int n = (int)(S.catt_off[c + 1] - S.catt_off[c]);
+    const int64_t base = level == 0 ? S.catt_off[c] : S.act_base[cr];
+    int sbase = S.crank_first[cr];
+    for (int t0 = 0; t0 < n; t0 += 64) {
+      const int t = t0 + lane;
+      const bool live = t < n;
+      uint64_t key = 0, prev = 0;
+      int a = 0;
+      if (live) {
+        key = S.keys[base + t];
+        prev = t > 0 ? S.keys[base + t - 1] : ~key;
+        a = S.vals[base + t];
+        S.satt_lohi[base + t] = make_int2(S.att_lo[a], S.att_hi[a]);
+        S.satt_sc[base + t] = S.att_sc[a];
+      }
+      const bool head = live && key != prev;
+      const uint64_t hm = __ballot(head);
+      if (head) {
+        const int seg = sbase + __popcll(hm & ((1ull << lane) - 1ull));
+        S.seg_start[seg] = (int)(base + t);
+        S.seg_crank[seg] = cr;
+      }
+      sbase += __popcll(hm);
+    }
   }
 }
 
@@ -1267,6 +1316,26 @@ __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
   lvl_counts(S, n_act, n_keys);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
+  if constexpr (PHASE == 3) {
+    // one launch for both lists: the contigs k_one handed over get the whole level
+    // (PHASE 0 logic), the contigs it left open get explain_two (PHASE 2)
+    const int c1 = (int)S.counters[6], c2 = (int)S.counters[5];
+    for (int i = blockIdx.x; i < c1 + c2; i += gridDim.x) {
+      const bool whole = i < c1;
+      const int32_t* L = whole ? S.one_list : S.two_list;
+      const int j = whole ? i : i - c1;
+      const int cr = L[2 * j], c = L[2 * j + 1];
+      const bool ok = whole ? decide_contig<kDecNT, 0>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys)
+                            : decide_contig<kDecNT, 2>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
+      if (!ok && threadIdx.x == 0) {
+        const int slot = (int)atomicAdd(&S.counters[2], 1ull);
+        S.big_list[2 * slot] = cr;
+        S.big_list[2 * slot + 1] = c;
+        atomicMax(&S.counters[3], (unsigned long long)S.k.need[c]);
+      }
+      __syncthreads();
+    }
+  } else {
   const int32_t* list = PHASE == 1 ? S.one_list : S.two_list;
   const int count = PHASE == 1 ? (list ? (int)S.counters[6] : n_act) : (int)S.counters[5];
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
@@ -1280,6 +1349,7 @@ __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
       atomicMax(&S.counters[3], (unsigned long long)S.k.need[c]);
     }
     __syncthreads();
+  }
   }
 }
 
@@ -1353,7 +1423,7 @@ struct StagedState {
   Buf att_lo, att_hi, att_loc, att_clade, att_hit, att_sc;
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
-  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list, lvl_ctr;
+  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list, lvl_ctr, seg_cnt;
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
   int big_slots = 512;
@@ -1464,7 +1534,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->att_off.ensure((size_t)(N + 1) * sizeof(int64_t)));
   ST_TRY(st->red.ensure(2 * sizeof(int64_t)));
   sa.catt_off = st->att_off.as<int64_t>();
-  const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * 32);
+  static const char* ag_env = getenv("WF_ATT_GRID");        // blocks per CU (measurement aid)
+  const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * (ag_env ? atoi(ag_env) : 32));
   ST_TRY(hipMemsetAsync(st->red.p, 0, 2 * sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt.as<int64_t>() + N, 0, sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt_leaves.as<int64_t>() + N, 0, sizeof(int64_t), s));
@@ -1479,13 +1550,20 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
                                             st->att_off.as<int64_t>(), (int)(N + 1), s));
     ST_TRY(hipcub::DeviceReduce::Sum(nullptr, t2, st->cnt_leaves.as<int64_t>(),
                                      st->red.as<int64_t>(), (int)(N + 1), s));
-    ST_TRY(st->tmp.ensure(std::max(t1, t2)));
+    size_t t3 = 0;
+    ST_TRY(hipcub::DeviceReduce::Max(nullptr, t3, st->cnt.as<int64_t>(), st->red.as<int64_t>() + 1,
+                                     (int)(N + 1), s));
+    ST_TRY(st->tmp.ensure(std::max(t1, std::max(t2, t3))));
     size_t tb = st->tmp.n;
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, tb, st->cnt.as<int64_t>(),
                                             st->att_off.as<int64_t>(), (int)(N + 1), s));
     tb = st->tmp.n;
     ST_TRY(hipcub::DeviceReduce::Sum(st->tmp.p, tb, st->cnt_leaves.as<int64_t>(),
                                      st->red.as<int64_t>(), (int)(N + 1), s));
+    // largest contig (a reduction, not one global atomic per contig: those serialise)
+    tb = st->tmp.n;
+    ST_TRY(hipcub::DeviceReduce::Max(st->tmp.p, tb, st->cnt.as<int64_t>(), st->red.as<int64_t>() + 1,
+                                     (int)(N + 1), s));
   }
   ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -1517,6 +1595,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   ST_TRY(st->seg_rec.ensure(A1 * 16)); ST_TRY(st->seg_cg.ensure(A1 * 8));
   ST_TRY(st->wave_list.ensure(A1 * 4));
   ST_TRY(st->crank_first.ensure(((size_t)N + 1) * 4));
+  ST_TRY(st->seg_cnt.ensure(((size_t)N + 1) * 4));
   ST_TRY(st->lmax.ensure((size_t)std::max<int64_t>(NL, 1) * 8));
   ST_TRY(st->c_gu.ensure((size_t)N * 4)); ST_TRY(st->c_umask.ensure((size_t)N * 8));
   ST_TRY(st->c_best.ensure((size_t)N * 8)); ST_TRY(st->c_bestcl.ensure((size_t)N * 4));
@@ -1541,7 +1620,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
                                             st->seg_id.as<int32_t>(), (int)A1, s));
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, st->seg_nleaf.as<int32_t>(),
                                             st->leaf_off.as<int32_t>(), (int)A1 + 1, s));
-    ST_TRY(st->tmp.ensure(std::max(t1, std::max(t2, t3))));
+    size_t t4 = 0;
+    ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t4, st->seg_cnt.as<int32_t>(),
+                                            st->crank_first.as<int32_t>(), N + 1, s));
+    ST_TRY(st->tmp.ensure(std::max(std::max(t1, t4), std::max(t2, t3))));
   }
   sa.att_lo = st->att_lo.as<int32_t>(); sa.att_hi = st->att_hi.as<int32_t>();
   sa.att_loc = st->att_loc.as<int32_t>(); sa.att_clade = st->att_clade.as<int32_t>();
@@ -1554,6 +1636,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   sa.seg_rec = st->seg_rec.as<int4>();
   sa.seg_cg = st->seg_cg.as<int2>();
   sa.crank_first = st->crank_first.as<int32_t>();
+  sa.seg_cnt = st->seg_cnt.as<int32_t>();
   sa.lmax = st->lmax.as<uint64_t>();
   sa.c_gu = st->c_gu.as<int32_t>(); sa.c_umask = st->c_umask.as<uint64_t>();
   sa.c_best = st->c_best.as<unsigned long long>(); sa.c_bestcl = st->c_bestcl.as<int32_t>();
@@ -1648,12 +1731,19 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       ST_TRY(hipGetLastError());
       sa.keys = kbuf.Current();
       sa.vals = vbuf.Current();
-      hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
-      need = st->tmp.n;
-      ST_TRY(hipcub::DeviceScan::InclusiveSum(st->tmp.p, need, sa.flags, sa.seg_id, (int)n_keys, s));
-      hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
-      hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
-      hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys, n_act);
+      if (sa.sort_cap > 0) {
+        need = st->tmp.n;
+        ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_cnt, sa.crank_first, n_act + 1, s));
+        hipLaunchKernelGGL(k_seg_build, dim3(std::min(n_act, st->cus * 32)), dim3(64), 0, s, sa, n_act,
+                           level, n_keys);
+      } else {
+        hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+        need = st->tmp.n;
+        ST_TRY(hipcub::DeviceScan::InclusiveSum(st->tmp.p, need, sa.flags, sa.seg_id, (int)n_keys, s));
+        hipLaunchKernelGGL(k_segs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+        hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+        hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys, n_act);
+      }
       if (thread_mean) {
         hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
         hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 8), dim3(64), 0, s, sa);
@@ -1678,8 +1768,12 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       static hipError_t attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<2>),
                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
                                                     160 * 1024 - 1024);
+      static hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    160 * 1024 - 1024);
       ST_TRY(attr1);
       ST_TRY(attr2);
+      ST_TRY(attr3);
     }
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
     if (flat_one) {
@@ -1692,8 +1786,6 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     } else if (one_fast) {
       hipLaunchKernelGGL(k_one, dim3(std::min<int64_t>(n_act, (int64_t)st->cus * 32)), dim3(64), 0, s, sa,
                          n_act, level, n_keys);
-      hipLaunchKernelGGL(k_decide<1>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * 4)), dim3(kDecNT),
-                         (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     } else {
       hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act,
                          level, n_keys);
@@ -1704,8 +1796,12 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     // explain_two contigs are latency chains, so they should all be in flight at once
     const unsigned dec_per_cu =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>(12, (160 * 1024) / std::max<int64_t>(st->dec_lds, 1)));
-    hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)), dim3(kDecNT),
-                       (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
+    if (one_fast)                       // k_one's overflow list and its open contigs
+      hipLaunchKernelGGL(k_decide<3>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
+                         dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
+    else
+      hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
+                         dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     ST_TRY(hipGetLastError());
     if (async) {
       // HBM-slot decisions on the device count (slots sized for the largest contig)
