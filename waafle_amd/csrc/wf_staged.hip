@@ -799,11 +799,7 @@ __global__ void k_leaf(const SArgs S, int64_t n_keys) {
   }
 }
 
-__global__ void k_seg_combine(const SArgs S, int64_t n_keys) {
-  int n_act_ = 0;
-  lvl_counts(S, n_act_, n_keys);
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= seg_count(S, n_keys) || S.seg_nleaf[s] == 0) return;   // 0: mean done in k_seg_rec
+__device__ __forceinline__ void seg_combine_one(const SArgs& S, int s) {
   const int len = S.seg_rec[s].z;
   const double* lv = S.leaf_val + S.leaf_off[s];
   double total = 0.0;
@@ -821,6 +817,21 @@ __global__ void k_seg_combine(const SArgs S, int64_t n_keys) {
   }
   S.seg_mean[s] = total / (double)len;
 }
+
+// One thread per leaf-path segment, found from the leaf side (the thread of a segment's
+// first leaf): a grid-stride loop over the level's leaves instead of a thread for every
+// segment of the level (most of which k_seg_rec already finished).
+__global__ void k_seg_combine(const SArgs S, int64_t n_keys) {
+  int n_act_ = 0;
+  lvl_counts(S, n_act_, n_keys);
+  const int TL = S.leaf_off[seg_count(S, n_keys)];
+  for (int jl = blockIdx.x * blockDim.x + threadIdx.x; jl < TL; jl += gridDim.x * blockDim.x) {
+    const int s = S.leaf_seg[jl];
+    if (jl != S.leaf_off[s]) continue;
+    seg_combine_one(S, s);
+  }
+}
+
 
 // ---- flat explain_one (orgscorer.py:407-429, 585-597, 621-631) -------------------------
 // For --weak-loci ignore/penalize and <= 64 loci, the one-clade search needs no per-contig
@@ -1755,7 +1766,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
                                               (int)n_keys + 1, s));
       hipLaunchKernelGGL(k_leaf_expand, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
       hipLaunchKernelGGL(k_leaf, dim3(persistent), dim3(256), 0, s, sa, n_keys);
-      hipLaunchKernelGGL(k_seg_combine, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_seg_combine, dim3(st->cus * 4), dim3(256), 0, s, sa, n_keys);
       ST_TRY(hipGetLastError());
     } else {
       sa.keys = kbuf.Current();
