@@ -141,6 +141,41 @@ typedef struct wf_timing {
   int64_t overflow_contigs;   /* contigs that went to the overflow kernel (host mode) */
 } wf_timing;
 
+/* ---- waafle_genecaller (waafle_genecaller.py:107-233) -------------------------------
+ * Gene calls from one blastout: per contig group (a run of consecutive rows with the same
+ * qseqid, utils.py:255-270), hits with scov_modified >= min_scov become intervals, the
+ * connected components of overlapping intervals (calc_overlap >= min_overlap) are merged
+ * (min start, max stop, strand of the longest member, ties to '-'), and merged genes of
+ * length >= min_gene_length are returned in component order.  Replaces the per-contig
+ * hits2ints / overlap_intervals / merge_inodes calls of the reference's main loop. */
+typedef struct wf_gc_batch {
+  int32_t n_groups;           /* contig groups, blastout order */
+  int32_t device_resident;    /* 1: device pointers (enqueue only); 0: host arrays */
+  int64_t n_hits;
+  const int64_t* hit_off;     /* [n_groups + 1] hit range of each group */
+  const int32_t* hit_qlo;     /* [n_hits] qstart / qend, either order */
+  const int32_t* hit_qhi;
+  const int8_t* hit_strand;   /* 0 '+', 1 '-' (sstrand "minus", utils.py:214) */
+  const double* hit_scov;     /* scov_modified (utils.py:227) */
+} wf_gc_batch;
+
+typedef struct wf_gc_params {
+  double min_overlap;         /* --min-overlap, default 0.1 */
+  double min_scov;            /* --min-scov, default 0.75 */
+  double min_gene_length;     /* --min-gene-length, default 200 */
+  int32_t stranded;           /* accepted, no effect: dead upstream (genecaller.py:212-215) */
+  int32_t _pad;
+} wf_gc_params;
+
+typedef struct wf_gc_result { /* same residency as the batch */
+  int32_t* n_genes;           /* [n_groups] */
+  int32_t* gene_start;        /* [n_hits]: group g's genes at [hit_off[g], hit_off[g] + n_genes[g]) */
+  int32_t* gene_stop;
+  int8_t*  gene_strand;       /* 0 '+', 1 '-' */
+} wf_gc_result;
+
+int wf_genecall(wf_ctx* ctx, const wf_gc_batch* batch, const wf_gc_params* params, wf_gc_result* out);
+
 int wf_abi_version(void);
 int wf_device_count(int* count);
 int wf_init(int device, wf_ctx** out);

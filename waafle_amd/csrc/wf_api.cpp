@@ -26,6 +26,8 @@ struct wf_ctx {
   // taxonomy
   int32_t tax_n = 0, root = -1, unknown = -1;
   DevBuf parent, depth, sibp, leaves, lin;
+  // genecaller staging (host-resident calls)
+  DevBuf gc_off, gc_qlo, gc_qhi, gc_strand, gc_scov, gc_ngenes, gc_gstart, gc_gstop, gc_gstrand, gc_status;
   bool have_lin = false;
   // overflow work list + counter
   DevBuf ovf_list, ovf2_list, ovf_count;
@@ -220,7 +222,9 @@ void wf_free(wf_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->lin, &ctx->ovf_list,
+  DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->lin, &ctx->gc_off,
+                    &ctx->gc_qlo, &ctx->gc_qhi, &ctx->gc_strand, &ctx->gc_scov, &ctx->gc_ngenes,
+                    &ctx->gc_gstart, &ctx->gc_gstop, &ctx->gc_gstrand, &ctx->gc_status, &ctx->ovf_list,
                     &ctx->ovf2_list, &ctx->kargs,
                     &ctx->ovf_count, &ctx->retry_list, &ctx->retry_count, &ctx->big_ws,
                     &ctx->b_hit_off, &ctx->b_qlo, &ctx->b_qhi, &ctx->b_taxon, &ctx->b_hstrand,
@@ -559,6 +563,81 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
     if (r->status[c] != 0)
       return fail(ctx, r->status[c] == wf::kPending ? WF_E_NOMEM : r->status[c],
                   "contig %d failed with status %d", c, r->status[c]);
+  return WF_OK;
+}
+
+int wf_genecall(wf_ctx* ctx, const wf_gc_batch* b, const wf_gc_params* p, wf_gc_result* r) {
+  if (!ctx) return WF_E_BADINPUT;
+  if (!b || !p || !r) return fail(ctx, WF_E_BADINPUT, "null batch/params/result");
+  if (b->n_groups < 0 || b->n_hits < 0) return fail(ctx, WF_E_BADINPUT, "negative sizes");
+  if (!b->hit_off || (b->n_hits > 0 && (!b->hit_qlo || !b->hit_qhi || !b->hit_strand || !b->hit_scov)))
+    return fail(ctx, WF_E_BADINPUT, "null hit arrays");
+  if (!r->n_genes || !r->gene_start || !r->gene_stop || !r->gene_strand)
+    return fail(ctx, WF_E_BADINPUT, "null result arrays");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int64_t G = b->n_groups, NH = b->n_hits;
+  if (G == 0) return WF_OK;
+  // largest group (LDS capacity of the kernel): from the offsets, on the host
+  std::vector<int64_t> off;
+  const int64_t* hoff = b->hit_off;
+  if (b->device_resident) {
+    off.resize(G + 1);
+    HIP_TRY(ctx, hipMemcpyAsync(off.data(), b->hit_off, sizeof(int64_t) * (G + 1), hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    hoff = off.data();
+  }
+  if (hoff[0] != 0 || hoff[G] != NH) return fail(ctx, WF_E_BADINPUT, "hit_off must span [0, n_hits]");
+  int64_t mx = 0;
+  for (int64_t g = 0; g < G; ++g) {
+    if (hoff[g + 1] < hoff[g]) return fail(ctx, WF_E_BADINPUT, "hit_off decreases at group %lld", (long long)g);
+    mx = std::max(mx, hoff[g + 1] - hoff[g]);
+  }
+  constexpr int64_t kCapMax = 4096;
+  wf::GcArgs a{};
+  a.n_groups = (int)G;
+  a.cap = 64;
+  while (a.cap < std::min(mx, kCapMax)) a.cap <<= 1;
+  a.min_overlap = p->min_overlap;
+  a.min_scov = p->min_scov;
+  a.min_gene_length = p->min_gene_length;
+  int rc;
+  if (b->device_resident) {
+    a.hit_off = b->hit_off; a.qlo = b->hit_qlo; a.qhi = b->hit_qhi; a.strand = b->hit_strand;
+    a.scov = b->hit_scov;
+    a.n_genes = r->n_genes; a.gene_start = r->gene_start; a.gene_stop = r->gene_stop;
+    a.gene_strand = r->gene_strand;
+  } else {
+    if ((rc = upload(ctx, ctx->gc_off, b->hit_off, G + 1, &a.hit_off)) ||
+        (rc = upload(ctx, ctx->gc_qlo, b->hit_qlo, NH, &a.qlo)) ||
+        (rc = upload(ctx, ctx->gc_qhi, b->hit_qhi, NH, &a.qhi)) ||
+        (rc = upload(ctx, ctx->gc_strand, b->hit_strand, NH, &a.strand)) ||
+        (rc = upload(ctx, ctx->gc_scov, b->hit_scov, NH, &a.scov)) ||
+        (rc = alloc_out(ctx, ctx->gc_ngenes, G, &a.n_genes)) ||
+        (rc = alloc_out(ctx, ctx->gc_gstart, NH, &a.gene_start)) ||
+        (rc = alloc_out(ctx, ctx->gc_gstop, NH, &a.gene_stop)) ||
+        (rc = alloc_out(ctx, ctx->gc_gstrand, NH, &a.gene_strand)))
+      return rc;
+  }
+  if ((rc = alloc_out(ctx, ctx->gc_status, G, &a.status))) return rc;
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess) cus = prop.multiProcessorCount;
+  HIP_TRY(ctx, wf::launch_genecall(a, cus, ctx->stream));
+  std::vector<int32_t> status(G);
+  if ((rc = download(ctx, status.data(), a.status, G))) return rc;
+  if (!b->device_resident) {
+    if ((rc = download(ctx, r->n_genes, a.n_genes, G)) ||
+        (rc = download(ctx, r->gene_start, a.gene_start, NH)) ||
+        (rc = download(ctx, r->gene_stop, a.gene_stop, NH)) ||
+        (rc = download(ctx, r->gene_strand, a.gene_strand, NH)))
+      return rc;
+  }
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  for (int64_t g = 0; g < G; ++g)
+    if (status[g] != 0)
+      return fail(ctx, WF_E_NOMEM, "contig group %lld has more than %lld intervals", (long long)g,
+                  (long long)kCapMax);
   return WF_OK;
 }
 

@@ -77,6 +77,7 @@ struct SArgs {
   int2* seg_cg;                  // [segments] (clade, locus)
   int32_t* crank_first;          // [active + 1] first segment of each active contig
   int32_t* seg_cnt;              // [active + 1] segments per active contig (per-contig sort)
+  int32_t* seg_len;              // [segments] locus length (k_seg_build; null on the radix path)
   // flat explain_one (weak loci ignore/penalize, <= 64 loci)
   uint64_t* lmax;                // [n_loci] per-locus max score bits over known clades
   int32_t* c_gu;                 // [active] unmasked loci (-1: contig needs no decision)
@@ -97,6 +98,17 @@ struct SArgs {
   const unsigned long long* in_counts;   // this level's counts on the device (null: the
                                          // kernel arguments are exact)
 };
+
+// waafle_genecaller (wf_genecall.hip): one contig group per wave
+struct GcArgs {
+  int n_groups, cap;                       // cap: intervals held in LDS per group (power of 2)
+  const int64_t* hit_off; const int32_t* qlo; const int32_t* qhi; const int8_t* strand;
+  const double* scov;
+  double min_overlap, min_scov, min_gene_length;
+  int32_t* n_genes; int32_t* gene_start; int32_t* gene_stop; int8_t* gene_strand;
+  int32_t* status;                         // per group: 0, or -4 when it exceeds cap
+};
+hipError_t launch_genecall(const GcArgs& a, int cus, hipStream_t s);
 
 struct StagedState;
 StagedState* staged_create(int device);

@@ -367,11 +367,20 @@ __global__ __launch_bounds__(64) void k_seg_build(const SArgs S, int n_act, int 
     S.seg_start[total] = (int)n_keys;
     S.seg_id[n_keys - 1] = total;                    // seg_count()
   }
+  const KArgs& K = S.k;
+  const uint64_t lmask = (1ull << S.key_lb) - 1, tmask = (1ull << S.key_tb) - 1;
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const int c = S.act ? S.act[cr] : cr;
     const int n = (int)(S.catt_off[c + 1] - S.catt_off[c]);
     const int64_t base = level == 0 ? S.catt_off[c] : S.act_base[cr];
     int sbase = S.crank_first[cr];
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    int glen = 0;                                    // lane g: length of locus g (G <= 64)
+    if (lane < G) {
+      const int a = K.lstart[l0 + lane], b = K.lend[l0 + lane];
+      glen = max(a, b) - min(a, b) + 1;
+    }
     for (int t0 = 0; t0 < n; t0 += 64) {
       const int t = t0 + lane;
       const bool live = t < n;
@@ -386,10 +395,18 @@ __global__ __launch_bounds__(64) void k_seg_build(const SArgs S, int n_act, int 
       }
       const bool head = live && key != prev;
       const uint64_t hm = __ballot(head);
+      const int g = (int)(key & lmask);
+      int len = __shfl(glen, g & 63, 64);
       if (head) {
+        if (G > 64) {
+          const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
+          len = max(a, b) - min(a, b) + 1;
+        }
         const int seg = sbase + __popcll(hm & ((1ull << lane) - 1ull));
         S.seg_start[seg] = (int)(base + t);
         S.seg_crank[seg] = cr;
+        S.seg_cg[seg] = make_int2((int)((key >> S.key_lb) & tmask), g);
+        S.seg_len[seg] = len;
       }
       sbase += __popcll(hm);
     }
@@ -514,9 +531,16 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
   int nl = 0;
   bool one_run = false, to_wave = false;
   if (s < seg_count(S, n_keys)) {
-    const SegInfo si = seg_info(S, (int)s);
+    SegInfo si;
+    if (S.seg_len) {                                 // k_seg_build wrote length and (clade, locus)
+      si.kb = S.seg_start[s];
+      si.ke = S.seg_start[s + 1];
+      si.len = S.seg_len[s];
+    } else {
+      si = seg_info(S, (int)s);
+      S.seg_cg[s] = make_int2((int)((S.keys[si.kb] >> S.key_lb) & ((1ull << S.key_tb) - 1)), si.g);
+    }
     nl = (si.len / kNpyBuf) * lut_count(S, kNpyBuf) + lut_count(S, si.len % kNpyBuf);
-    S.seg_cg[s] = make_int2((int)((S.keys[si.kb] >> S.key_lb) & ((1ull << S.key_tb) - 1)), si.g);
     int lo = 0, hi = 0;
     double v = 0.0;
     int na = si.ke - si.kb;
@@ -574,6 +598,7 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
       hi = max(hi, lo);
       int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
       int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
+#pragma unroll 4
       for (int q = 0; q < nl; ++q) {
         const int4 e = lt[q];
         const int le = e.x + e.y;
@@ -597,6 +622,7 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
       };
       const double V0 = inside(L0), V1 = inside(L1), V2 = inside(L2), V3 = inside(L3);
       SumStack stk;
+#pragma unroll 4
       for (int q = 0; q < nl; ++q) {
         const int4 e = lt[q];
         const int le = e.x + e.y;
@@ -1434,7 +1460,7 @@ struct StagedState {
   Buf att_lo, att_hi, att_loc, att_clade, att_hit, att_sc;
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
-  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list, lvl_ctr, seg_cnt;
+  Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list, lvl_ctr, seg_cnt, seg_len;
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
   int big_slots = 512;
@@ -1648,6 +1674,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   sa.seg_cg = st->seg_cg.as<int2>();
   sa.crank_first = st->crank_first.as<int32_t>();
   sa.seg_cnt = st->seg_cnt.as<int32_t>();
+  ST_TRY(st->seg_len.ensure(A1 * 4));
+  sa.seg_len = sa.sort_cap > 0 ? st->seg_len.as<int32_t>() : nullptr;   // set by k_seg_build
   sa.lmax = st->lmax.as<uint64_t>();
   sa.c_gu = st->c_gu.as<int32_t>(); sa.c_umask = st->c_umask.as<uint64_t>();
   sa.c_best = st->c_best.as<unsigned long long>(); sa.c_bestcl = st->c_bestcl.as<int32_t>();

@@ -54,6 +54,21 @@ class WfTiming(C.Structure):
                 ("launches", C.c_int64), ("overflow_contigs", C.c_int64)]
 
 
+class WfGcBatch(C.Structure):
+    _fields_ = [("n_groups", C.c_int32), ("device_resident", C.c_int32), ("n_hits", C.c_int64),
+                ("hit_off", _P), ("hit_qlo", _P), ("hit_qhi", _P), ("hit_strand", _P),
+                ("hit_scov", _P)]
+
+
+class WfGcParams(C.Structure):
+    _fields_ = [("min_overlap", C.c_double), ("min_scov", C.c_double),
+                ("min_gene_length", C.c_double), ("stranded", C.c_int32), ("_pad", C.c_int32)]
+
+
+class WfGcResult(C.Structure):
+    _fields_ = [("n_genes", _P), ("gene_start", _P), ("gene_stop", _P), ("gene_strand", _P)]
+
+
 # every symbol the header declares, with its ctypes signature
 SIGNATURES = {
     "wf_abi_version": (C.c_int, []),
@@ -72,6 +87,8 @@ SIGNATURES = {
     "wf_synchronize": (C.c_int, [C.c_void_p]),
     "wf_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "wf_timing_read": (C.c_int, [C.c_void_p, C.POINTER(WfTiming)]),
+    "wf_genecall": (C.c_int, [C.c_void_p, C.POINTER(WfGcBatch), C.POINTER(WfGcParams),
+                              C.POINTER(WfGcResult)]),
 }
 
 _lib = None
