@@ -389,7 +389,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
       HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
     }
     std::string err;
-    rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, ctx->stream, &err);
+    rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->n_hits, b->n_loci, ctx->stream, &err);
     if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : WF_E_HIP, "%s", err.c_str());
     if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
     ++ctx->launches;

@@ -116,8 +116,8 @@ void staged_destroy(StagedState* st);
 void staged_set_lds(StagedState* st, int64_t bytes);
 // Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2 with
 // the message in *err (-1 bad input, -2 HIP failure).
-int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipStream_t s,
-                 std::string* err);
+int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t n_hits,
+                 int64_t n_loci, hipStream_t s, std::string* err);
 
 // `dk` points to a device copy of the host-side `k` (enqueued before the launch).
 hipError_t launch_lds_kernel(const KArgs& k, const KArgs* dk, hipStream_t s);

@@ -1534,8 +1534,18 @@ static inline unsigned grid_for(int64_t n, int block = 256) {
 
 // Runs the whole path for one batch on stream `s` (synchronising on it between levels).
 // `k` carries device pointers for batch, taxonomy, params and results.
-int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipStream_t s,
-                 std::string* err) {
+// Host waits inside a pass: an event polled in a loop wakes the host within microseconds,
+// where a blocking stream synchronisation took tens of microseconds per level.
+static hipError_t spin_sync(hipStream_t s, hipEvent_t ev) {
+  hipError_t e = hipEventRecord(ev, s);
+  if (e != hipSuccess) return e;
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) {
+  }
+  return e;
+}
+
+int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t NH, int64_t NL,
+                 hipStream_t s, std::string* err) {
   const int N = k.n_contigs;
   if (N <= 0) return 0;
   g_sync_stream = s;
@@ -1546,10 +1556,6 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   int rc = build_lut(st, s, err);
   if (rc) return rc;
   int64_t* hc = reinterpret_cast<int64_t*>(st->host_counters);   // pinned
-  ST_TRY(hipMemcpyAsync(&hc[0], k.hit_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  ST_TRY(hipMemcpyAsync(&hc[1], k.loc_off + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  ST_TRY(hipStreamSynchronize(s));
-  const int64_t NH = hc[0], NL = hc[1];
   if (NH >= (int64_t(1) << 31) - 1) { *err = "too many hits for one batch (split it)"; return -1; }
 
   SArgs sa{};
@@ -1604,7 +1610,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
   }
   ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  ST_TRY(hipStreamSynchronize(s));
+  ST_TRY(spin_sync(s, st->lvl_ev[0]));
   const int64_t A = hc[2], TLB = hc[3], max_att = hc[4];
   // per-contig LDS sort when every contig's attachments fit one workgroup's LDS
   // (WF_LDS_SORT=0: device radix sort of the whole level; measurement aid)
@@ -1857,7 +1863,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
     }
     ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, s));
-    ST_TRY(hipStreamSynchronize(s));
+    ST_TRY(spin_sync(s, st->lvl_ev[0]));
     const int n_big = (int)st->host_counters[2];
     if (n_big > 0) {
       const int64_t slot = ((int64_t)st->host_counters[3] + 255) & ~int64_t(255);
@@ -1869,7 +1875,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, hipSt
       ST_TRY(hipGetLastError());
       ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, s));
-      ST_TRY(hipStreamSynchronize(s));
+      ST_TRY(spin_sync(s, st->lvl_ev[0]));
     }
     if (level == 0 && !st->dec_lds_fixed && n_big * 50 > n_act && st->dec_lds < 48 * 1024)
       st->dec_lds += 8 * 1024;   // adaptive arena: grows while > 2% of contigs overflow
