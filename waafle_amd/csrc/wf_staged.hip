@@ -300,16 +300,17 @@ __global__ void k_keys_active(const SArgs S, int n_act, uint64_t* keys, int32_t*
 // workgroup per contig -- gives the same sequence as one global radix sort of the level.
 // Ties keep attachment order (the pair is the sort key).  Keys are built here (no separate
 // key kernel).  Dynamic LDS: sort_cap x (8 + 4) bytes.
-constexpr int kSortNT = 64;      // one wave per contig
 constexpr int kSortMax = 4096;   // 48 KiB of LDS; larger contigs (cfg5 stress) sort faster with the radix sort
 
-__global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_act,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_sort_contig(const SArgs S, int n_act,
                                                           int level, uint64_t* keys, int32_t* vals) {
   int64_t n_keys_ = 0;
   lvl_counts(S, n_act, n_keys_);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem);
   int32_t* sv = reinterpret_cast<int32_t*>(sk + S.sort_cap);
+  __shared__ int s_red[NT / 64];
   const int tid = threadIdx.x;
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const int c = S.act ? S.act[cr] : cr;
@@ -322,14 +323,14 @@ __global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_ac
     const int64_t base = level == 0 ? a0 : S.act_base[cr];
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
-    for (int t = tid; t < n2; t += kSortNT) {
+    for (int t = tid; t < n2; t += NT) {
       sk[t] = t < n ? make_key(S, cr, (int)(a0 + t)) : ~0ull;
       sv[t] = t < n ? (int)(a0 + t) : 0x7fffffff;
     }
     __syncthreads();
     for (int k = 2; k <= n2; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < (n2 >> 1); i += kSortNT) {
+        for (int i = tid; i < (n2 >> 1); i += NT) {
           const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));   // i with a 0 inserted at bit j
           const int hi = lo | j;
           const bool up = (lo & k) == 0;
@@ -342,13 +343,19 @@ __global__ __launch_bounds__(kSortNT) void k_sort_contig(const SArgs S, int n_ac
       }
     }
     int ns = 0;                                      // distinct keys = segments
-    for (int t = tid; t < n; t += kSortNT) {
+    for (int t = tid; t < n; t += NT) {
       keys[base + t] = sk[t];
       vals[base + t] = sv[t];
       ns += (t == 0 || sk[t] != sk[t - 1]) ? 1 : 0;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off, 64);
+    if (NT > 64) {
+      if ((tid & 63) == 0) s_red[tid >> 6] = ns;
+      __syncthreads();
+      if (tid == 0)
+        for (int w = 1; w < NT / 64; ++w) ns += s_red[w];
+    }
     if (tid == 0) S.seg_cnt[cr] = ns;
     __syncthreads();
   }
@@ -1347,9 +1354,9 @@ __device__ __forceinline__ bool decide_contig(const SArgs& S, int c, int cr, int
 
 constexpr int kDecNT = 64;   // one wave per contig decision: no cross-wave barriers
 
-template <int PHASE>
-__global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
-                                                       int level, int64_t n_keys) {
+template <int PHASE, int NT = kDecNT>
+__global__ __launch_bounds__(NT, 2) void k_decide(const SArgs S, int n_act,
+                                                   int level, int64_t n_keys) {
   lvl_counts(S, n_act, n_keys);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ Ctl ctl;
@@ -1362,8 +1369,8 @@ __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
       const int32_t* L = whole ? S.one_list : S.two_list;
       const int j = whole ? i : i - c1;
       const int cr = L[2 * j], c = L[2 * j + 1];
-      const bool ok = whole ? decide_contig<kDecNT, 0>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys)
-                            : decide_contig<kDecNT, 2>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
+      const bool ok = whole ? decide_contig<NT, 0>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys)
+                            : decide_contig<NT, 2>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
       if (!ok && threadIdx.x == 0) {
         const int slot = (int)atomicAdd(&S.counters[2], 1ull);
         S.big_list[2 * slot] = cr;
@@ -1378,7 +1385,7 @@ __global__ __launch_bounds__(kDecNT, 2) void k_decide(const SArgs S, int n_act,
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const int cr = list ? list[2 * i] : i;
     const int c = list ? list[2 * i + 1] : (S.act ? S.act[cr] : cr);
-    const bool ok = decide_contig<kDecNT, PHASE>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
+    const bool ok = decide_contig<NT, PHASE>(S, c, cr, level, smem, S.dec_lds_bytes, ctl, n_keys);
     if (!ok && threadIdx.x == 0) {
       const int slot = (int)atomicAdd(&S.counters[2], 1ull);
       S.big_list[2 * slot] = cr;
@@ -1759,14 +1766,24 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
       if (sa.sort_cap > 0) {
         const size_t lds = (size_t)sa.sort_cap * 12;
         if (lds > 64 * 1024) {
-          static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig),
+          static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<64>),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)(kSortMax * 12));
+          static hipError_t attr4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<256>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        (int)(kSortMax * 12));
           ST_TRY(attr);
+          ST_TRY(attr4);
         }
         const int per_cu = std::min(32, std::max(1, (int)((160 * 1024) / lds)));
-        hipLaunchKernelGGL(k_sort_contig, dim3(std::min(n_act, st->cus * per_cu)), dim3(kSortNT), lds, s,
-                           sa, n_act, level, kbuf.Current(), vbuf.Current());
+        // level 0: one wave per contig (10^4+ contigs fill the chip); later levels have
+        // few contigs, so four waves shorten each contig's sort
+        if (level == 0)
+          hipLaunchKernelGGL(k_sort_contig<64>, dim3(std::min(n_act, st->cus * per_cu)), dim3(64), lds, s,
+                             sa, n_act, level, kbuf.Current(), vbuf.Current());
+        else
+          hipLaunchKernelGGL(k_sort_contig<256>, dim3(std::min(n_act, st->cus * per_cu)), dim3(256), lds,
+                             s, sa, n_act, level, kbuf.Current(), vbuf.Current());
       } else {
         hipLaunchKernelGGL(k_keys_active, dim3(std::min(n_act, st->cus * 8)), dim3(256), 0, s, sa,
                            n_act, kbuf.Current(), vbuf.Current());
@@ -1816,9 +1833,13 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
       static hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3>),
                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
                                                     160 * 1024 - 1024);
+      static hipError_t attr5 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3, 256>),
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                    160 * 1024 - 1024);
       ST_TRY(attr1);
       ST_TRY(attr2);
       ST_TRY(attr3);
+      ST_TRY(attr5);
     }
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
     if (flat_one) {
@@ -1841,7 +1862,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     // explain_two contigs are latency chains, so they should all be in flight at once
     const unsigned dec_per_cu =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>(12, (160 * 1024) / std::max<int64_t>(st->dec_lds, 1)));
-    if (one_fast)                       // k_one's overflow list and its open contigs
+    if (one_fast && level > 0)          // few open contigs: four waves each
+      hipLaunchKernelGGL((k_decide<3, 256>), dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
+                         dim3(256), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
+    else if (one_fast)                  // k_one's overflow list and its open contigs
       hipLaunchKernelGGL(k_decide<3>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
                          dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     else
