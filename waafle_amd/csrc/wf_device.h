@@ -856,7 +856,7 @@ struct MaskClasses {
 
 // Builds the classes (block-wide).  Returns false when they would not pay off or fit.
 template <int NT>
-__device__ bool build_mask_classes(const Contig& C, Ctl& ctl, int Pp, int Gu, uint64_t full,
+__device__ __forceinline__ bool build_mask_classes(const Contig& C, Ctl& ctl, int Pp, int Gu, uint64_t full,
                                    MaskClasses& M) {
   const int tid = threadIdx.x;
   int ib = 1;
@@ -982,6 +982,83 @@ __device__ __forceinline__ OptEval eval_two(const KArgs& K, const Contig& C, int
   const bool unk = C.cl_id[pa] == K.unknown || C.cl_id[pb] == K.unknown;
   OptEval e;
   e.swapped = 0;
+  if (G <= 64) {
+    // the synteny as four locus masks, built in one pass over the two score rows; the
+    // swap rule, the counts, the direction pattern and the sister test are bit operations
+    uint64_t mi = 0, mm = 0, ma = 0, mb = 0;         // '~', '*', 'A', 'B' ('!': the rest)
+#pragma unroll 8
+    for (int g = 0; g < G; ++g) {
+      const uint64_t bit = 1ull << g;
+      const double s1 = C.S[(int64_t)pa * G + g], s2 = C.S[(int64_t)pb * G + g];
+      const double mn = s2 < s1 ? s2 : s1;
+      if (C.ign[g]) mi |= bit;
+      else if (mn >= P.k_amb && !unk) mm |= bit;
+      else if (s1 >= P.k2) ma |= bit;
+      else if (s2 >= P.k2) mb |= bit;
+    }
+    const uint64_t ab = ma | mb;                     // "^[^A]*B" -> swap (:537-540)
+    e.swapped = (ab && ((mb >> __builtin_ctzll(ab)) & 1ull)) ? 1 : 0;
+    const uint64_t mA = e.swapped ? mb : ma, mB = e.swapped ? ma : mb;
+    auto ch = [&](int g) -> uint8_t {
+      const uint64_t bit = 1ull << g;
+      return (mi & bit) ? '~' : (mm & bit) ? '*' : (mA & bit) ? 'A' : (mB & bit) ? 'B' : '!';
+    };
+    e.same = 1;
+    int64_t tot = 0, amb = 0;
+    int state = 0;
+    bool dir_ok = true;
+    for (int g = 0; g < G; ++g) {
+      const uint8_t c = ch(g);
+      if (out) out[g] = c;
+      if (best && best[g] != c) e.same = 0;
+      if (c == 'A' || c == 'B' || c == '*') {
+        const int len = C.loc_len[g];
+        tot += len;
+        if (c == '*') amb += len;
+      }
+      if (c != '~') {  // "^A+B+A+$" on synteny without '~' (orgscorer.py:542)
+        if (state == 0) { if (c == 'A') state = 1; else dir_ok = false; }
+        else if (state == 1) { if (c == 'B') state = 2; else if (c != 'A') dir_ok = false; }
+        else if (state == 2) { if (c == 'A') state = 3; else if (c != 'B') dir_ok = false; }
+        else { if (c != 'A') dir_ok = false; }
+      }
+    }
+    const int nA = __popcll(mA), nB = __popcll(mB);
+    e.dir = (dir_ok && state == 3) ? 1 : 0;
+    e.c1p = e.swapped ? pb : pa;
+    e.c2p = e.swapped ? pa : pb;
+    e.ok = 1;
+    if ((double)amb / (double)tot > P.amb_frac) e.ok = 0;           // :693-702
+    if (P.clade_genes >= 0 && min(nA, nB) < P.clade_genes) e.ok = 0; // :704-708
+    const int X = C.cl_id[e.c1p], Y = C.cl_id[e.c2p];
+    if (P.clade_leaves >= 0) {                                       // :710-715
+      const int64_t lc = e.dir ? K.leaves[Y] : min(K.leaves[X], K.leaves[Y]);
+      if (lc < P.clade_leaves) e.ok = 0;
+    }
+    if (P.sister_on && e.ok) {                                       // :717-744
+      const int px = K.parent[X], py = K.parent[Y];
+      uint64_t fa = 0, fb = 0;
+#pragma unroll 8
+      for (int q = 0; q < Pcount; ++q) {
+        const int sp = C.sib_of[q];
+        if (sp != px && sp != py) continue;
+        const int s = C.cl_id[q];
+        if (s == X || s == Y) continue;
+        uint64_t h;
+        if (C.hm) {
+          h = C.hm[q];
+        } else {
+          h = 0;
+          for (int g = 0; g < G; ++g)
+            if (C.S[(int64_t)q * G + g] >= P.sister_thr) h |= 1ull << g;
+        }
+        if (sp == px) fb |= h;
+        if (sp == py) fa |= h;
+      }
+      if ((fb & mB) || (!e.dir && (fa & mA))) e.ok = 0;
+    }
+    return e;
+  }
 #pragma unroll 8
   for (int g = 0; g < G; ++g) {  // "^[^A]*B" -> swap (orgscorer.py:537-540)
     uint8_t c = two_char(K, C, pa, pb, unk, g);
