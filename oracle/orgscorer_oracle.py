@@ -525,13 +525,47 @@ def _ok(o):
     return o is not None and o.ok
 
 
-def evaluate_contig(C, tax):
+def gene_spans(C, clade):
+    """make_gene_spans_field (orgscorer.py:770-789): per locus, the 1-based sites with
+    exactly one nonzero neighbour (starts and ends of nonzero runs longer than one site);
+    "None" where the clade has no site array.  An all-zero site array raises IndexError
+    upstream (boolean mask of length 1 over an empty index array)."""
+    out = []
+    per = C.sites.get(clade)
+    for g in range(len(C.loci)):
+        if per is None or g not in per:
+            out.append(MISSING_ANNOT)
+            continue
+        nzi = 1 + np.nonzero(per[g])[0]
+        if len(nzi) == 0:
+            raise OracleError("IndexError in make_gene_spans_field (all-zero site scores)")
+        ldiff = np.concatenate([[0], nzi[1:] - nzi[:-1]])
+        rdiff = np.concatenate([nzi[1:] - nzi[:-1], [0]])
+        nzi = nzi[np.logical_xor(ldiff == 1, rdiff == 1)]
+        out.append(":".join(str(k) for k in nzi))
+    return "|".join(out)
+
+
+def write_details(details, C, iteration):
+    """write_details (orgscorer.py:802-812) as rows; clades in name order (upstream: set
+    order); an empty field prints as "--" (utils.py:139)."""
+    if details is None:
+        return
+    for clade in _ordered(C.clades):
+        scores = "|".join("{:.3f}".format(v) for v in C.genes[clade])
+        details.append([C.name, str(iteration), clade, scores or "--",
+                        gene_spans(C, clade) or "--"])
+
+
+def evaluate_contig(C, tax, details=None):
     """orgscorer.py:566-583 (roll-up loop; runaway guard at 100 iterations)."""
     it = 1
+    write_details(details, C, it)
     one = one_clade(C, tax)
     two = two_clade(C, tax) if not _ok(one) else None
     while C.clades and ROOT not in C.clades and not _ok(one) and not _ok(two):
         C.raise_level(tax)
+        write_details(details, C, it)
         one = one_clade(C, tax)
         two = two_clade(C, tax) if not _ok(one) else None
         it += 1
@@ -545,8 +579,9 @@ def evaluate_contig(C, tax):
 # driver + writer (orgscorer.py:750-964, utils.py:122-143)
 # ---------------------------------------------------------------------------
 
-def score_contigs(lengths, loci_groups, hit_groups, tax, params, warn=None):
-    """orgscorer.py:900-960 without the file writing: returns {name: ContigModel}."""
+def score_contigs(lengths, loci_groups, hit_groups, tax, params, warn=None, details=None):
+    """orgscorer.py:900-960 without the file writing: returns {name: ContigModel}.
+    `details`: a list that collects the --write-details rows (orgscorer.py:931-937)."""
     contigs = OrderedDict()
     for name, n in lengths.items():
         contigs[name] = ContigModel(name, n, params)
@@ -568,7 +603,7 @@ def score_contigs(lengths, loci_groups, hit_groups, tax, params, warn=None):
             for _ in range(params.jump_taxonomy):
                 C.raise_level(tax)
         if not all(L.ignore for L in C.loci):
-            evaluate_contig(C, tax)
+            evaluate_contig(C, tax, details)
     return contigs
 
 
@@ -612,12 +647,13 @@ def render_rows(contigs, tax):
     return out
 
 
-def run(contigs_path, blastout_path, gff_path, taxonomy_path, params, warn=None):
+def run(contigs_path, blastout_path, gff_path, taxonomy_path, params, warn=None,
+        details=None):
     """File-level entry point: returns ({name: ContigModel}, Taxonomy)."""
     tax = Taxonomy.from_file(taxonomy_path)
     lengths = fasta_lengths(contigs_path)
     contigs = score_contigs(lengths, gff_groups(gff_path), blast_groups(blastout_path),
-                            tax, params, warn=warn)
+                            tax, params, warn=warn, details=details)
     return contigs, tax
 
 

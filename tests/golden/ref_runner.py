@@ -49,6 +49,20 @@ def main():
     elif mode != "hash":
         raise SystemExit("bad mode " + mode)
 
+    if "--write-details" in sys.argv:
+        # --write-details raises on Python 3 upstream: try_open() hands print() a binary
+        # GzipFile (utils.py:60-72, orgscorer.py:931-937).  Open that one file in text
+        # mode; everything written to it is still the reference's own write_details().
+        import gzip
+        opener = ws.wu.try_open
+
+        def try_open(path, *args):
+            if path.endswith(".details.tsv.gz") and args == ("w",):
+                return gzip.open(path, "wt")
+            return opener(path, *args)
+
+        ws.wu.try_open = try_open
+
     with_scores = os.environ.get("REF_DUMP_SCORES", "0") == "1"
     write = ws.write_main_output_files
 

@@ -16,7 +16,14 @@ DEMO_FILES = {
 
 def case_names():
     return sorted(os.path.basename(p)[:-len(".json.gz")]
-                  for p in glob.glob(os.path.join(GOLDEN, "*.json.gz")))
+                  for p in glob.glob(os.path.join(GOLDEN, "*.json.gz"))
+                  if not os.path.basename(p).startswith("details_"))
+
+
+def details_names():
+    """--write-details fixtures (make_details.py)."""
+    return sorted(os.path.basename(p)[:-len(".json.gz")]
+                  for p in glob.glob(os.path.join(GOLDEN, "details_*.json.gz")))
 
 
 def load(name):
