@@ -176,6 +176,33 @@ typedef struct wf_gc_result { /* same residency as the batch */
 
 int wf_genecall(wf_ctx* ctx, const wf_gc_batch* batch, const wf_gc_params* params, wf_gc_result* out);
 
+/* ---- --write-details (orgscorer.py:766-812, 931-937) --------------------------------
+ * With details on, the next wf_score (staged mode) also records, for every roll-up level,
+ * the contigs it evaluated and each (contig, clade, locus) segment of that level: its gene
+ * score (Contig.update_gene_scores :394-406, the exact numpy mean) and its gene spans
+ * (make_gene_spans_field :770-789: first and last 1-based site of every nonzero run longer
+ * than one site).  The caller renders the reference's rows from them (clades per contig
+ * and level, 'Unknown' = 1 - max for --weak-loci assign-unknown).  Replaces the
+ * write_details(details, contig, iteration) calls of evaluate_contig (:566-583).
+ * Arrays stay valid until the next wf_score or wf_free.  Synchronous; a diagnostic path. */
+typedef struct wf_details {
+  int64_t n_evals;            /* evaluated (contig, level) pairs, level-major */
+  const int32_t* eval_contig;
+  const int32_t* eval_level;
+  int64_t n_segs;             /* segment records, level-major */
+  const int32_t* seg_level;
+  const int32_t* seg_contig;
+  const int32_t* seg_clade;   /* taxonomy id at that level */
+  const int32_t* seg_locus;   /* index among the contig's kept loci */
+  const double* seg_mean;     /* gene score */
+  const int32_t* seg_nspan;   /* runs listed; -1: the site array is all zero (upstream raises) */
+  const int64_t* span_off;    /* [n_segs + 1] first run of each segment */
+  const int32_t* spans;       /* [2 * span_off[n_segs]] (first, last) 1-based site pairs */
+} wf_details;
+
+int wf_details_enable(wf_ctx* ctx, int on);
+int wf_details_read(wf_ctx* ctx, wf_details* out);
+
 int wf_abi_version(void);
 int wf_device_count(int* count);
 int wf_init(int device, wf_ctx** out);

@@ -62,3 +62,22 @@ def test_gpu_details_all_zero_sites_refused(tmp_path):
     with pytest.raises(SystemExit):
         orgscorer.main(paths + ["--outdir", str(tmp_path), "--quiet", "--write-details",
                                 "--min-overlap", "0"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [[], ["--jump-taxonomy", "1"], ["--weak-loci", "assign-unknown"]])
+def test_gpu_details_match_oracle_synthetic(flags, tmp_path):
+    """cfg2-shaped synthetic contigs (200 clades): the HIP records against the oracle."""
+    from waafle_amd import orgscorer, synth
+    sub = str(tmp_path / "in")
+    synth.write_text(synth.generate(n=300, genes=8, clades=200, seed=2), sub, "synth")
+    paths = [os.path.join(sub, "synth" + e) for e in (".fna", ".blastout", ".gff", ".taxonomy.tsv")]
+    out = tmp_path / "out"
+    out.mkdir()
+    orgscorer.main(paths + ["--outdir", str(out), "--basename", "case", "--quiet",
+                            "--write-details"] + flags)
+    with gzip.open(os.path.join(str(out), "case.details.tsv.gz"), "rt") as fh:
+        got = fh.read()
+    want = _oracle_text(paths, flags)
+    assert got.count("\n") > 300
+    assert got == want

@@ -54,6 +54,12 @@ struct wf_ctx {
   int mode = WF_MODE_STAGED;
   bool lds_set = false;            // wf_set_lds_bytes called: also the staged decision arena
   wf::StagedState* staged = nullptr;
+  // --write-details
+  bool details_on = false;
+  wf::DetailsSink det;
+  std::vector<int32_t> d_eval_contig, d_eval_level, d_level, d_contig, d_clade, d_locus, d_nspan, d_spans;
+  std::vector<double> d_mean;
+  std::vector<int64_t> d_span_off;
 };
 
 namespace {
@@ -377,6 +383,8 @@ static int check_batch(wf_ctx* ctx, const wf_batch* b, const wf_params* p, const
 // overflow list).  Everything is enqueued on the context stream; no host synchronisation.
 static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   int rc;
+  if (ctx->details_on && ctx->mode != WF_MODE_STAGED)
+    return fail(ctx, WF_E_STATE, "--write-details needs the staged mode");
   if (ctx->mode == WF_MODE_STAGED) {
     K.root = ctx->root;
     K.unknown = ctx->unknown;
@@ -389,7 +397,8 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
       HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
     }
     std::string err;
-    rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->n_hits, b->n_loci, ctx->stream, &err);
+    rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->n_hits, b->n_loci, ctx->stream, &err,
+                          ctx->details_on ? &ctx->det : nullptr);
     if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : WF_E_HIP, "%s", err.c_str());
     if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
     ++ctx->launches;
@@ -638,6 +647,52 @@ int wf_genecall(wf_ctx* ctx, const wf_gc_batch* b, const wf_gc_params* p, wf_gc_
     if (status[g] != 0)
       return fail(ctx, WF_E_NOMEM, "contig group %lld has more than %lld intervals", (long long)g,
                   (long long)kCapMax);
+  return WF_OK;
+}
+
+int wf_details_enable(wf_ctx* ctx, int on) {
+  if (!ctx) return WF_E_BADINPUT;
+  if (on && ctx->mode != WF_MODE_STAGED)
+    return fail(ctx, WF_E_STATE, "--write-details needs the staged mode");
+  ctx->details_on = on != 0;
+  ctx->det.levels.clear();
+  return WF_OK;
+}
+
+int wf_details_read(wf_ctx* ctx, wf_details* out) {
+  if (!ctx || !out) return WF_E_BADINPUT;
+  if (!ctx->details_on) return fail(ctx, WF_E_STATE, "details are not enabled");
+  ctx->d_eval_contig.clear(); ctx->d_eval_level.clear();
+  ctx->d_level.clear(); ctx->d_contig.clear(); ctx->d_clade.clear(); ctx->d_locus.clear();
+  ctx->d_nspan.clear(); ctx->d_spans.clear(); ctx->d_mean.clear(); ctx->d_span_off.assign(1, 0);
+  for (const wf::DetailsLevel& L : ctx->det.levels) {
+    for (int32_t c : L.act) { ctx->d_eval_contig.push_back(c); ctx->d_eval_level.push_back(L.level); }
+    const size_t ns = L.seg_crank.size();
+    for (size_t i = 0; i < ns; ++i) {
+      ctx->d_level.push_back(L.level);
+      ctx->d_contig.push_back(L.act[L.seg_crank[i]]);
+      ctx->d_clade.push_back(L.seg_cg[2 * i]);
+      ctx->d_locus.push_back(L.seg_cg[2 * i + 1]);
+      ctx->d_mean.push_back(L.seg_mean[i]);
+      const int n = L.span_cnt[i];
+      ctx->d_nspan.push_back(n);
+      const size_t at = 2 * (size_t)L.seg_start[i];
+      for (int r = 0; r < 2 * n; ++r) ctx->d_spans.push_back(L.spans[at + r]);
+      ctx->d_span_off.push_back(ctx->d_span_off.back() + (n > 0 ? n : 0));
+    }
+  }
+  out->n_evals = (int64_t)ctx->d_eval_contig.size();
+  out->eval_contig = ctx->d_eval_contig.data();
+  out->eval_level = ctx->d_eval_level.data();
+  out->n_segs = (int64_t)ctx->d_contig.size();
+  out->seg_level = ctx->d_level.data();
+  out->seg_contig = ctx->d_contig.data();
+  out->seg_clade = ctx->d_clade.data();
+  out->seg_locus = ctx->d_locus.data();
+  out->seg_mean = ctx->d_mean.data();
+  out->seg_nspan = ctx->d_nspan.data();
+  out->span_off = ctx->d_span_off.data();
+  out->spans = ctx->d_spans.data();
   return WF_OK;
 }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 namespace wf {
 
@@ -110,6 +111,22 @@ struct GcArgs {
 };
 hipError_t launch_genecall(const GcArgs& a, int cus, hipStream_t s);
 
+// --write-details: per roll-up level, the evaluated (active) contigs and the segment
+// records of the level, copied to the host (wf_staged.hip details_level)
+struct DetailsLevel {
+  int level = 0;
+  std::vector<int32_t> act;                  // active contigs (level 0: every contig)
+  std::vector<int32_t> seg_start;            // [segments + 1] first sorted attachment
+  std::vector<int32_t> seg_crank;            // active rank of each segment's contig
+  std::vector<int32_t> seg_cg;               // (clade, locus) pairs
+  std::vector<double> seg_mean;              // gene score
+  std::vector<int32_t> span_cnt;             // runs (-1: all-zero site array)
+  std::vector<int32_t> spans;                // (first, last) 1-based pairs at 2 * seg_start
+};
+struct DetailsSink {
+  std::vector<DetailsLevel> levels;
+};
+
 struct StagedState;
 StagedState* staged_create(int device);
 void staged_destroy(StagedState* st);
@@ -117,7 +134,7 @@ void staged_set_lds(StagedState* st, int64_t bytes);
 // Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2 with
 // the message in *err (-1 bad input, -2 HIP failure).
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t n_hits,
-                 int64_t n_loci, hipStream_t s, std::string* err);
+                 int64_t n_loci, hipStream_t s, std::string* err, DetailsSink* det = nullptr);
 
 // `dk` points to a device copy of the host-side `k` (enqueued before the launch).
 hipError_t launch_lds_kernel(const KArgs& k, const KArgs* dk, hipStream_t s);

@@ -529,6 +529,46 @@ __device__ __forceinline__ double run_leaf(int lo, int hi, double v, int st, int
   return res;
 }
 
+
+// --write-details gene spans (make_gene_spans_field, orgscorer.py:770-789), thread per
+// segment, before k_seg_rec compacts the attachment ranges.  The clade's site array at the
+// locus is nonzero exactly on the union of its attachments' [lo, hi) ranges with score > 0;
+// the reference lists the first and last site (1-based) of every maximal nonzero run
+// longer than one site.  Runs come out in site order by repeated selection (a segment has
+// few attachments; this is a diagnostic output).  span_cnt = -1: no nonzero site (upstream
+// raises IndexError).  Runs go to spans[2 * seg_start[s] ...] (at most one per attachment).
+__global__ void k_seg_spans(const SArgs S, int64_t n_keys, int32_t* span_cnt, int32_t* spans) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= seg_count(S, n_keys)) return;
+  const int t0 = S.seg_start[s], t1 = S.seg_start[s + 1];
+  int pos = 0, cnt = 0;
+  bool any = false;
+  for (;;) {
+    int lo = INT_MAX;                                // next run: smallest live start >= pos
+    for (int t = t0; t < t1; ++t) {
+      const int2 x = S.satt_lohi[t];
+      if (S.satt_sc[t] > 0.0 && x.y > x.x && x.x >= pos && x.x < lo) lo = x.x;
+    }
+    if (lo == INT_MAX) break;
+    any = true;
+    int hi = lo;
+    for (bool grew = true; grew;) {                  // absorb every range reaching the run
+      grew = false;
+      for (int t = t0; t < t1; ++t) {
+        const int2 x = S.satt_lohi[t];
+        if (S.satt_sc[t] > 0.0 && x.y > x.x && x.x <= hi && x.y > hi) { hi = x.y; grew = true; }
+      }
+    }
+    if (hi - lo >= 2) {
+      spans[2 * ((int64_t)t0 + cnt)] = lo + 1;
+      spans[2 * ((int64_t)t0 + cnt) + 1] = hi;
+      ++cnt;
+    }
+    pos = hi;
+  }
+  span_cnt[s] = any ? cnt : -1;
+}
+
 template <bool THREAD_MEAN>
 __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
   int n_act_ = 0;
@@ -1468,6 +1508,7 @@ struct StagedState {
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
   Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list, lvl_ctr, seg_cnt, seg_len;
+  Buf span_cnt, spans;                              // --write-details only
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
   int big_slots = 512;
@@ -1551,8 +1592,51 @@ static hipError_t spin_sync(hipStream_t s, hipEvent_t ev) {
   return e;
 }
 
+// --write-details: this level's evaluated contigs and segment records (gene scores =
+// segment means, spans from k_seg_spans) to the host.  Synchronous; diagnostic output.
+static hipError_t details_level(StagedState* st, const SArgs& sa, int level, int n_act, int64_t n_keys,
+                                hipStream_t s, DetailsSink* det) {
+  det->levels.emplace_back();
+  DetailsLevel& L = det->levels.back();
+  L.level = level;
+  L.act.resize((size_t)n_act);
+  hipError_t e = hipSuccess;
+  if (level == 0) {
+    for (int i = 0; i < n_act; ++i) L.act[i] = i;
+  } else if (n_act > 0) {
+    e = hipMemcpyAsync(L.act.data(), sa.act, (size_t)n_act * 4, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+  }
+  int ns = 0;
+  if (n_keys > 0) {
+    e = hipMemcpyAsync(&ns, sa.seg_id + n_keys - 1, 4, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+  }
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess || ns == 0) return e;
+  L.seg_start.resize((size_t)ns + 1);
+  L.seg_crank.resize(ns);
+  L.seg_cg.resize(2 * (size_t)ns);
+  L.seg_mean.resize(ns);
+  L.span_cnt.resize(ns);
+  L.spans.resize(2 * (size_t)n_keys);
+  const struct { void* dst; const void* src; size_t n; } cp[] = {
+      {L.seg_start.data(), sa.seg_start, ((size_t)ns + 1) * 4},
+      {L.seg_crank.data(), sa.seg_crank, (size_t)ns * 4},
+      {L.seg_cg.data(), sa.seg_cg, (size_t)ns * 8},
+      {L.seg_mean.data(), sa.seg_mean, (size_t)ns * 8},
+      {L.span_cnt.data(), st->span_cnt.p, (size_t)ns * 4},
+      {L.spans.data(), st->spans.p, (size_t)n_keys * 8}};
+  for (const auto& c : cp) {
+    e = hipMemcpyAsync(c.dst, c.src, c.n, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipStreamSynchronize(s);
+}
+
+
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t NH, int64_t NL,
-                 hipStream_t s, std::string* err) {
+                 hipStream_t s, std::string* err, DetailsSink* det) {
   const int N = k.n_contigs;
   if (N <= 0) return 0;
   g_sync_stream = s;
@@ -1742,9 +1826,14 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   // the trailing empty level and the always-launched HBM-slot kernel, so it is opt-in
   // (WF_PIPELINE=1) until a level has fewer launches.
   static const char* pipe_env = getenv("WF_PIPELINE");
-  const bool pipelined = sa.sort_cap > 0 && !flat_one && pipe_env && pipe_env[0] == '1';
+  const bool pipelined = sa.sort_cap > 0 && !flat_one && !det && pipe_env && pipe_env[0] == '1';
   int n_act = N;
   int64_t n_keys = A;
+  if (det) {
+    det->levels.clear();
+    ST_TRY(st->span_cnt.ensure(A1 * 4));
+    ST_TRY(st->spans.ensure(A1 * 8));
+  }
   for (int level = 0; n_act > 0 && level <= kMaxIter; ++level) {
     const bool async = pipelined && level >= 1;
     sa.counters = lvl_ctr + 8 * level;
@@ -1806,6 +1895,9 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
         hipLaunchKernelGGL(k_gather, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
         hipLaunchKernelGGL(k_crank_first, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys, n_act);
       }
+      if (det)
+        hipLaunchKernelGGL(k_seg_spans, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys,
+                           st->span_cnt.as<int32_t>(), st->spans.as<int32_t>());
       if (thread_mean) {
         hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
         hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 8), dim3(64), 0, s, sa);
@@ -1841,6 +1933,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
       ST_TRY(attr3);
       ST_TRY(attr5);
     }
+    if (det) ST_TRY(details_level(st, sa, level, n_act, n_keys, s, det));
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
     if (flat_one) {
       ST_TRY(hipMemsetAsync(sa.lmax, 0, (size_t)std::max<int64_t>(NL, 1) * 8, s));

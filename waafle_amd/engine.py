@@ -142,6 +142,37 @@ class GpuScorer:
             raise err
         return res
 
+    def score_details(self, batch, params):
+        """wf_score with --write-details records on: (Results, {name: numpy array}) with the
+        evaluated (contig, level) pairs and the per-level segment records
+        (include/waafle_hip.h wf_details)."""
+        self._check(self.lib.wf_details_enable(self.h, 1))
+        try:
+            res = self.score(batch, params)
+            d = L.WfDetails()
+            self._check(self.lib.wf_details_read(self.h, C.byref(d)))
+
+            def arr(ptr, n, dt):
+                if n == 0:
+                    return np.zeros(0, dtype=dt)
+                ct = np.ctypeslib.as_ctypes_type(np.dtype(dt))
+                return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(n,)).copy()
+
+            ne, ns = int(d.n_evals), int(d.n_segs)
+            out = dict(eval_contig=arr(d.eval_contig, ne, np.int32),
+                       eval_level=arr(d.eval_level, ne, np.int32),
+                       seg_level=arr(d.seg_level, ns, np.int32),
+                       seg_contig=arr(d.seg_contig, ns, np.int32),
+                       seg_clade=arr(d.seg_clade, ns, np.int32),
+                       seg_locus=arr(d.seg_locus, ns, np.int32),
+                       seg_mean=arr(d.seg_mean, ns, np.float64),
+                       seg_nspan=arr(d.seg_nspan, ns, np.int32),
+                       span_off=arr(d.span_off, ns + 1, np.int64))
+            out["spans"] = arr(d.spans, 2 * int(out["span_off"][-1]), np.int32)
+            return res, out
+        finally:
+            self._check(self.lib.wf_details_enable(self.h, 0))
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.wf_free(self.h)

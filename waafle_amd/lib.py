@@ -69,6 +69,13 @@ class WfGcResult(C.Structure):
     _fields_ = [("n_genes", _P), ("gene_start", _P), ("gene_stop", _P), ("gene_strand", _P)]
 
 
+class WfDetails(C.Structure):
+    _fields_ = [("n_evals", C.c_int64), ("eval_contig", _P), ("eval_level", _P),
+                ("n_segs", C.c_int64), ("seg_level", _P), ("seg_contig", _P), ("seg_clade", _P),
+                ("seg_locus", _P), ("seg_mean", _P), ("seg_nspan", _P), ("span_off", _P),
+                ("spans", _P)]
+
+
 # every symbol the header declares, with its ctypes signature
 SIGNATURES = {
     "wf_abi_version": (C.c_int, []),
@@ -89,6 +96,8 @@ SIGNATURES = {
     "wf_timing_read": (C.c_int, [C.c_void_p, C.POINTER(WfTiming)]),
     "wf_genecall": (C.c_int, [C.c_void_p, C.POINTER(WfGcBatch), C.POINTER(WfGcParams),
                               C.POINTER(WfGcResult)]),
+    "wf_details_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "wf_details_read": (C.c_int, [C.c_void_p, C.POINTER(WfDetails)]),
 }
 
 _lib = None

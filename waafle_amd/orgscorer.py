@@ -9,6 +9,7 @@ import sys
 import time
 
 from . import cli, engine, inputs, lib, output
+from . import details as wdetails
 from . import dist as wdist
 
 
@@ -19,8 +20,6 @@ def die(*args):
 
 def main(argv=None):
     args = cli.build_parser().parse_args(argv)
-    if args.write_details:
-        die("--write-details is not supported by this build (it raises on Python 3 upstream)")
     say = (lambda *a: None) if args.quiet else inputs.say
     t0 = time.time()
     say("Loading inputs.")
@@ -41,8 +40,19 @@ def main(argv=None):
         import torch.distributed as group
         torch.cuda.set_device(local)
         group.init_process_group("nccl", device_id=torch.device("cuda", local))
+    det = None
     try:
-        if group is None:
+        if args.write_details:
+            # per-level records come from one context (a diagnostic output: one GPU)
+            if group is not None or args.gpus != 1:
+                die("--write-details runs on one GPU (--gpus 1, no torch.distributed launch)")
+            scorer = engine.GpuScorer(0)
+            try:
+                scorer.set_taxonomy(tax)
+                res, det = scorer.score_details(batch, cli.param_dict(args))
+            finally:
+                scorer.close()
+        elif group is None:
             res = engine.score(batch, tax, cli.param_dict(args), gpus=args.gpus)
         else:
             scorer = engine.GpuScorer(local)
@@ -63,6 +73,12 @@ def main(argv=None):
         group.destroy_process_group()
         if rank != 0:
             return
+    if det is not None:
+        try:
+            wdetails.write(wdetails.render(batch, tax, cli.param_dict(args), det),
+                           args.outdir, args.basename)
+        except wdetails.DetailsError as exc:
+            die(str(exc))
     say("Initializing outputs.")
     rows = output.render(batch, tax, res)
     output.write(rows, args.outdir, args.basename)
