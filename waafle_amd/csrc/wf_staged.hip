@@ -26,6 +26,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -1518,7 +1519,12 @@ struct StagedState {
   int64_t dec_lds = 24 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
   unsigned long long* host_counters = nullptr;   // pinned
+  // host-coherent mailbox: k_publish writes counts + a sequence word, the host spins on it
+  unsigned long long* mbox = nullptr;
+  unsigned long long* mbox_dev = nullptr;
+  unsigned long long mbox_seq = 0;
   ~StagedState() {
+    if (mbox) (void)hipHostFree(mbox);
     if (host_counters) (void)hipHostFree(host_counters);
     if (host_lvl) (void)hipHostFree(host_lvl);
     for (hipEvent_t e : lvl_ev)
@@ -1538,6 +1544,13 @@ StagedState* staged_create(int device) {
     st->host_lvl = nullptr;
   for (hipEvent_t& e : st->lvl_ev)
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+  if (hipHostMalloc(reinterpret_cast<void**>(&st->mbox), 16 * sizeof(unsigned long long),
+                    hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&st->mbox_dev), st->mbox, 0) != hipSuccess) {
+    if (st->mbox) (void)hipHostFree(st->mbox);
+    st->mbox = nullptr;
+    st->mbox_dev = nullptr;
+  }
   return st;
 }
 
@@ -1584,6 +1597,38 @@ static inline unsigned grid_for(int64_t n, int block = 256) {
 // `k` carries device pointers for batch, taxonomy, params and results.
 // Host waits inside a pass: an event polled in a loop wakes the host within microseconds,
 // where a blocking stream synchronisation took tens of microseconds per level.
+// Counts to the host without a copy dispatch or an event: one thread stores them into the
+// host-coherent mailbox, then (system-scope release) the sequence word the host spins on.
+__global__ void k_publish(unsigned long long* box, unsigned long long seq,
+                          const unsigned long long* a, int na, const unsigned long long* b, int nb) {
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < na; ++i) box[i] = a[i];
+  for (int i = 0; i < nb; ++i) box[na + i] = b[i];
+  __threadfence_system();
+  __hip_atomic_store(&box[15], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static hipError_t publish_sync(StagedState* st, hipStream_t s, const void* a, int na, const void* b, int nb,
+                               unsigned long long* out) {
+  const unsigned long long seq = ++st->mbox_seq;
+  hipLaunchKernelGGL(k_publish, dim3(1), dim3(64), 0, s, st->mbox_dev, seq,
+                     static_cast<const unsigned long long*>(a), na,
+                     static_cast<const unsigned long long*>(b), nb);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  volatile unsigned long long* box = st->mbox;
+  for (unsigned it = 1; box[15] != seq; ++it) {
+    if ((it & 4095u) == 0) {           // a failed stream must not spin forever
+      e = hipStreamQuery(s);
+      if (e != hipSuccess && e != hipErrorNotReady) return e;
+      if (e == hipSuccess && box[15] != seq) return hipErrorUnknown;
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  for (int i = 0; i < na + nb; ++i) out[i] = box[i];
+  return hipSuccess;
+}
+
 static hipError_t spin_sync(hipStream_t s, hipEvent_t ev) {
   hipError_t e = hipEventRecord(ev, s);
   if (e != hipSuccess) return e;
@@ -1699,9 +1744,16 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     ST_TRY(hipcub::DeviceReduce::Max(st->tmp.p, tb, st->cnt.as<int64_t>(), st->red.as<int64_t>() + 1,
                                      (int)(N + 1), s));
   }
-  ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  ST_TRY(spin_sync(s, st->lvl_ev[0]));
+  static const char* mb_env = getenv("WF_MAILBOX");         // 0: copy + event (measurement aid)
+  const bool mailbox = st->mbox && !(mb_env && mb_env[0] == '0');
+  if (mailbox) {
+    ST_TRY(publish_sync(st, s, st->att_off.as<int64_t>() + N, 1, st->red.p, 2,
+                        reinterpret_cast<unsigned long long*>(&hc[2])));
+  } else {
+    ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    ST_TRY(spin_sync(s, st->lvl_ev[0]));
+  }
   const int64_t A = hc[2], TLB = hc[3], max_att = hc[4];
   // per-contig LDS sort when every contig's attachments fit one workgroup's LDS
   // (WF_LDS_SORT=0: device radix sort of the whole level; measurement aid)
@@ -1978,9 +2030,13 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
       }
       continue;                         // n_act / n_keys stay the upper bounds
     }
-    ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
-                          hipMemcpyDeviceToHost, s));
-    ST_TRY(spin_sync(s, st->lvl_ev[0]));
+    if (mailbox) {
+      ST_TRY(publish_sync(st, s, sa.counters, 4, nullptr, 0, st->host_counters));
+    } else {
+      ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
+                            hipMemcpyDeviceToHost, s));
+      ST_TRY(spin_sync(s, st->lvl_ev[0]));
+    }
     const int n_big = (int)st->host_counters[2];
     if (n_big > 0) {
       const int64_t slot = ((int64_t)st->host_counters[3] + 255) & ~int64_t(255);
