@@ -1597,6 +1597,34 @@ static inline unsigned grid_for(int64_t n, int block = 256) {
 // `k` carries device pointers for batch, taxonomy, params and results.
 // Host waits inside a pass: an event polled in a loop wakes the host within microseconds,
 // where a blocking stream synchronisation took tens of microseconds per level.
+// Exclusive scan of n ints by one workgroup (per-contig segment counts -> first segment):
+// one launch with no host-side temp-storage query, where the device scan costs two
+// launches and a host call that is slower than the scan itself.  Thread t owns a
+// contiguous chunk; the chunk sums are scanned in LDS.
+constexpr int kScanNT = 1024;
+__global__ __launch_bounds__(kScanNT) void k_scan_small(const int32_t* in, int32_t* out, int n) {
+  __shared__ int s_part[kScanNT];
+  const int t = threadIdx.x;
+  const int per = (n + kScanNT - 1) / kScanNT;
+  const int b = min(n, t * per), e = min(n, b + per);
+  int sum = 0;
+  for (int i = b; i < e; ++i) sum += in[i];
+  s_part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < kScanNT; off <<= 1) {
+    const int v = t >= off ? s_part[t - off] : 0;
+    __syncthreads();
+    s_part[t] += v;
+    __syncthreads();
+  }
+  int run = s_part[t] - sum;
+  for (int i = b; i < e; ++i) {
+    const int x = in[i];
+    out[i] = run;
+    run += x;
+  }
+}
+
 // Counts to the host without a copy dispatch or an event: one thread stores them into the
 // host-coherent mailbox, then (system-scope release) the sequence word the host spins on.
 __global__ void k_publish(unsigned long long* box, unsigned long long seq,
@@ -1936,7 +1964,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
       sa.vals = vbuf.Current();
       if (sa.sort_cap > 0) {
         need = st->tmp.n;
-        ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_cnt, sa.crank_first, n_act + 1, s));
+        static const char* ss_env = getenv("WF_SMALL_SCAN");   // 0: device scan (measurement aid)
+        if (!(ss_env && ss_env[0] == '0') && n_act < 32 * kScanNT)   // <= 32 items a thread
+          hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanNT), 0, s, sa.seg_cnt, sa.crank_first, n_act + 1);
+        else
+          ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_cnt, sa.crank_first, n_act + 1, s));
         hipLaunchKernelGGL(k_seg_build, dim3(std::min(n_act, st->cus * 32)), dim3(64), 0, s, sa, n_act,
                            level, n_keys);
       } else {
