@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 1
+#define WF_ABI_VERSION 2
 
 enum wf_status {
   WF_OK = 0,
@@ -38,13 +38,12 @@ enum wf_status {
 
 enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
 
-/* Execution form of wf_score (same results either way):
- *  WF_MODE_STAGED (default): one flat kernel per phase over all contigs (hits, attachments,
- *    a device radix sort per roll-up level, segments, per-contig decisions); synchronises
- *    on the context stream between roll-up levels.
- *  WF_MODE_FUSED: one workgroup carries a contig through every phase (LDS tiers + an HBM
- *    workspace tier); fully asynchronous when the batch is device resident. */
-enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_FUSED = 1 };
+/* Execution form of wf_score.  WF_MODE_STAGED (the only form since ABI 2): one kernel per
+ * phase over all contigs (attachments, per-contig sort, segment means, per-contig
+ * decisions) and one pass of them per roll-up level.  The ABI-1 WF_MODE_FUSED form (one
+ * workgroup per contig through every phase) measured 2.3x slower and was retired;
+ * wf_set_mode rejects it with WF_E_BADINPUT. */
+enum wf_mode { WF_MODE_STAGED = 0 };
 
 typedef struct wf_ctx wf_ctx;
 
@@ -132,13 +131,11 @@ typedef struct wf_result {
   int64_t* need_bytes;        /* [n] workspace bytes asked for when status == WF_E_NOMEM */
 } wf_result;
 
-/* Kernel timing accumulated while enabled (HIP events on the context stream around
- * the per-contig kernel launches). */
+/* Pass timing accumulated while enabled: HIP events recorded on the context stream
+ * around every kernel of each wf_score pass. */
 typedef struct wf_timing {
-  double lds_kernel_ms;       /* sum over launches of the LDS-resident contig kernel */
-  double big_kernel_ms;       /* sum over launches of the overflow (HBM-workspace) kernel */
-  int64_t launches;           /* number of wf_score calls timed */
-  int64_t overflow_contigs;   /* contigs that went to the overflow kernel (host mode) */
+  double pass_ms;             /* sum over timed passes */
+  int64_t passes;             /* number of wf_score calls timed */
 } wf_timing;
 
 /* ---- waafle_genecaller (waafle_genecaller.py:107-233) -------------------------------
@@ -209,10 +206,8 @@ int wf_init(int device, wf_ctx** out);
 void wf_free(wf_ctx* ctx);
 const char* wf_last_error(const wf_ctx* ctx);
 int wf_set_stream(wf_ctx* ctx, void* hip_stream);     /* NULL = the context's own stream */
-int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes);     /* dynamic LDS per workgroup */
-int wf_set_workgroup(wf_ctx* ctx, int threads);       /* threads per contig: 64, 128, 256 */
-int wf_set_tier2_lds_bytes(wf_ctx* ctx, int64_t bytes); /* LDS of the overflow tier */
-int wf_set_mode(wf_ctx* ctx, int mode);               /* WF_MODE_STAGED / WF_MODE_FUSED */
+int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes);     /* decision arena per workgroup (LDS) */
+int wf_set_mode(wf_ctx* ctx, int mode);               /* WF_MODE_STAGED only (ABI 2) */
 int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* tax);
 int wf_score(wf_ctx* ctx, const wf_batch* batch, const wf_params* params, wf_result* out);
 int wf_synchronize(wf_ctx* ctx);

@@ -69,6 +69,14 @@ class OracleError(RuntimeError):
     """Stands in for the reference's `die()` (utils.py:49-52)."""
 
 
+class RunawayError(OracleError):
+    """The runaway-recursion die of evaluate_contig (orgscorer.py:580-581)."""
+
+    def __init__(self, contig):
+        super().__init__("  Warning: Runaway taxonomic recursion for " + contig)
+        self.contig = contig
+
+
 # ---------------------------------------------------------------------------
 # parameters: orgscorer.py:135-303 + genecaller.py:81-101 (shared args)
 # ---------------------------------------------------------------------------
@@ -570,7 +578,7 @@ def evaluate_contig(C, tax, details=None):
         two = two_clade(C, tax) if not _ok(one) else None
         it += 1
         if it > 100:
-            raise OracleError("  Warning: Runaway taxonomic recursion for " + C.name)
+            raise RunawayError(C.name)
     C.best_one, C.best_two = one, two
     C.iterations = it
 

@@ -64,6 +64,17 @@ SYNTH = {
     "syn_short": (dict(n=200, genes=8, clades=60, seed=7, short_frac=0.25, decoys=8),
                   [[], ["--min-gene-length", "100"]]),
     "syn_stress": (dict(n=3, genes=20, clades=600, seed=5, stress=True), [[]]),
+    # size-dependent device paths (round 2): full cfg5 stress contigs (5000 clades, ~5000
+    # attachments: device radix sort + mask-class explain_two), > 4096 attachments with a
+    # small potential set, and > 64 / > 128 loci (non-mask two-clade test, HBM loci)
+    "syn_cfg5": (dict(n=2, genes=20, clades=5000, seed=5, stress=True), [[]]),
+    "syn_bigatt": (dict(n=2, genes=10, clades=100, seed=21, decoys=600, lgt_frac=0.5),
+                   [[], ["-k1", "0.9"]]),
+    "syn_loci70": (dict(n=4, genes=70, clades=60, seed=22, decoys=4, lgt_frac=0.75),
+                   [[], ["--weak-loci", "assign-unknown"], ["-k1", "0.9"],
+                    ["-k1", "0.9", "--weak-loci", "assign-unknown"]]),
+    "syn_loci150": (dict(n=3, genes=150, clades=80, seed=23, decoys=3, lgt_frac=0.75),
+                    [[], ["-k1", "0.9"]]),
 }
 
 
@@ -147,7 +158,8 @@ def main():
                 if only and name not in only:
                     continue
                 make_case(name, inputs, flags, dict(kind="synth", params=kw), tmp,
-                          dump_scores=(not flags and kw["n"] <= 300))
+                          dump_scores=(not flags and kw["n"] <= 300
+                                       and kw["clades"] * kw["genes"] <= 20000))
         tie_dir = os.path.join(HERE, "tie_inputs")
         inputs = [os.path.join(tie_dir, f) for f in
                   ("tie.fna", "tie.blastout", "tie.gff", "tie.taxonomy.tsv")]

@@ -17,7 +17,25 @@ DEMO_FILES = {
 def case_names():
     return sorted(os.path.basename(p)[:-len(".json.gz")]
                   for p in glob.glob(os.path.join(GOLDEN, "*.json.gz"))
-                  if not os.path.basename(p).startswith("details_"))
+                  if not os.path.basename(p).startswith("details_")
+                  and ".runaway." not in os.path.basename(p))
+
+
+# fixtures whose explain_two is too large for the scalar oracle (cfg5 stress contigs:
+# 12.5 M clade pairs each): the HIP path is compared with the reference-generated fixture
+# (TSVs + decision dump) only, never with a re-run oracle
+HEAVY = {"syn_cfg5_default"}
+
+
+def runaway_names():
+    """Deep-taxonomy fixtures (make_deep.py): reference TSVs or its runaway die."""
+    return sorted(os.path.basename(p)[:-len(".runaway.json.gz")]
+                  for p in glob.glob(os.path.join(GOLDEN, "*.runaway.json.gz")))
+
+
+def load_runaway(name):
+    with gzip.open(os.path.join(GOLDEN, name + ".runaway.json.gz"), "rt") as fh:
+        return json.load(fh)
 
 
 def details_names():
@@ -47,8 +65,9 @@ def materialize(fixture, tmpdir):
         return [demo_file(f, tmpdir) for f in DEMO_FILES[recipe["gff"]]]
     if recipe["kind"] == "files":
         d = os.path.join(GOLDEN, recipe["dir"])
-        return [os.path.join(d, f) for f in
-                ("tie.fna", "tie.blastout", "tie.gff", "tie.taxonomy.tsv")]
+        stem = recipe.get("stem", "tie")
+        return [os.path.join(d, stem + e) for e in
+                (".fna", ".blastout", ".gff", ".taxonomy.tsv")]
     from waafle_amd import synth
     sub = os.path.join(str(tmpdir), "synth_" + "_".join(
         "{}{}".format(k, v) for k, v in sorted(recipe["params"].items())))

@@ -4,6 +4,11 @@ Bar: bit-exact for every integer/index/string field and for the float64 crit/ran
 (the kernels follow numpy's summation order), TSV bytes identical to the reference
 goldens except tie-flagged contigs (output must be one of the reference's outcomes).
 """
+import os
+import subprocess
+import sys
+import threading
+
 import numpy as np
 import pytest
 
@@ -11,7 +16,7 @@ import golden_cases as gc
 from oracle_bridge import (oracle_hits_from_batch, oracle_loci_from_batch, oracle_results,
                            run_oracle)
 from oracle import orgscorer_oracle as orc
-from waafle_amd import cli, engine, inputs, output, synth
+from waafle_amd import cli, engine, inputs, lib, output, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -20,10 +25,9 @@ FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n
           "n_meld2", "annot_hit", "pair_evals", "iterations", "status")
 
 
-@pytest.fixture(scope="module", params=["staged", "fused"])
-def scorer(request):
-    s = engine.GpuScorer(0, mode=request.param)
-    s.mode = request.param
+@pytest.fixture(scope="module")
+def scorer():
+    s = engine.GpuScorer(0)
     yield s
     s.close()
 
@@ -67,6 +71,27 @@ def assert_same_results(got, want, batch, skip=()):
     assert bad == []
 
 
+def assert_matches_dump(fx, batch, res):
+    """crit/rank bit-exact against the reference's own decision dump (float64 hex of the
+    reported option, sorted-iteration run) -- no oracle involved."""
+    bad = []
+    for c, name in enumerate(batch.contig_names):
+        if name in fx["ties"]:
+            continue
+        rec = fx["dump"].get(name, {})
+        call = int(res.call[c])
+        tag = {lib.CALL_NO_LGT: "one", lib.CALL_LGT: "two"}.get(call)
+        if tag is None:
+            if any(rec.get(t) and rec[t][0] for t in ("one", "two")):
+                bad.append((name, "unclassified here, OK upstream"))
+            continue
+        want = rec.get(tag)
+        got = [float(res.crit[c]).hex(), float(res.rank[c]).hex()]
+        if want is None or not want[0] or want[1:3] != got:
+            bad.append((name, tag, want, got))
+    assert bad == []
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_gpu_matches_goldens_and_oracle(name, scorer, tmp_path):
     fx = gc.load(name)
@@ -77,9 +102,38 @@ def test_gpu_matches_goldens_and_oracle(name, scorer, tmp_path):
     rows = output.render(batch, tax, res)
     texts = {k: "\n".join(v) + "\n" for k, v in rows.items()}
     assert gc.compare_tsv(fx, texts) == []
+    assert_matches_dump(fx, batch, res)
+    if name in gc.HEAVY:       # cfg5 stress: the fixture is the only reference
+        return
     contigs, _ = run_oracle(paths, fx["flags"])
     want = oracle_results(contigs, batch, tax)
     assert_same_results(res, want, batch)
+
+
+@pytest.mark.parametrize("name", gc.runaway_names())
+def test_gpu_deep_taxonomy_and_runaway(name, scorer, tmp_path):
+    """Roll-up depth past the 16-level lineage table and the > 100 iteration guard
+    (orgscorer.py:566-583): the reference's TSVs, or WF_E_RUNAWAY on the contig the
+    reference dies on, and the CLI's die message (make_deep.py fixtures)."""
+    fx = gc.load_runaway(name)
+    paths = gc.materialize(fx, tmp_path)
+    batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
+    if fx["returncode"] == 0:
+        res = gpu_score(scorer, batch, tax, fx["flags"])
+        rows = output.render(batch, tax, res)
+        assert {k: "\n".join(v) + "\n" for k, v in rows.items()} == fx["tsv"]
+        return
+    with pytest.raises(lib.WaafleHipError) as exc:
+        gpu_score(scorer, batch, tax, fx["flags"])
+    assert exc.value.code == lib.WF_E_RUNAWAY
+    assert batch.contig_names[int(exc.value.contigs[0])] in fx["stderr"]
+    cmd = [sys.executable, "-m", "waafle_amd.orgscorer"] + paths + \
+          ["--outdir", str(tmp_path), "--quiet"] + fx["flags"]
+    run = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert run.returncode == fx["returncode"]
+    want = fx["stderr"].strip().splitlines()
+    assert run.stderr.strip().splitlines()[-len(want):] == want
 
 
 def synth_case(tmp_path, flags=(), **kw):
@@ -161,12 +215,9 @@ def test_full_size_cfg2_properties(scorer):
     a = scorer.score(batch, params)
     b = scorer.score(batch, params)
     assert_same_results(a, b, batch)
-    for kw in (dict(mode=scorer.mode, lds_bytes=8192),        # fused: tier 1 -> tier 2;
-                                                              # staged: HBM decision slots
-               dict(mode="fused", lds_bytes=8192, tier2_lds_bytes=8192),  # -> tier 3
-               dict(mode="fused", threads=256, lds_bytes=36864),  # 4 waves per contig
-               dict(mode="fused", threads=128, lds_bytes=24576),
-               dict(mode="staged")):
+    for kw in (dict(lds_bytes=8192),          # small decision arena: HBM decision slots
+               dict(lds_bytes=65536),         # large arena: every contig in LDS
+               dict()):
         small = engine.GpuScorer(0, **kw)
         small.set_taxonomy(tax)
         c = small.score(batch, params)
@@ -188,3 +239,76 @@ def test_full_size_cfg2_properties(scorer):
     want = oracle_results(contigs, sub, tax)
     got = scorer.score(sub, params)
     assert_same_results(got, want, sub)
+
+
+def test_concurrent_contexts_share_a_device():
+    """Two and three contexts on device 0, each scoring its shard from its own host thread
+    at the same time (engine.score's device map), equal the one-context result field by
+    field.  Each context drains only its own stream before replacing scratch buffers."""
+    data = synth.generate(n=3000, genes=8, clades=200, seed=61)
+    batch, tax = synth.to_batch(data)
+    params = cli.param_dict(cli.parse_flags([]))
+    want = engine.score(batch, tax, params, gpus=1)
+    for n in (2, 3):
+        got = engine.score(batch, tax, params, gpus=n, devices=[0] * n)
+        assert_same_results(got, want, batch)
+    # the same contexts re-used while another thread grows and shrinks its batch
+    a, b = engine.GpuScorer(0), engine.GpuScorer(0)
+    a.set_taxonomy(tax)
+    b.set_taxonomy(tax)
+    out, errs = {}, []
+
+    def run(key, s, parts):
+        try:
+            out[key] = [s.score(batch.slice(x, y), params) for x, y in parts]
+        except Exception as exc:      # re-raised below
+            errs.append(exc)
+    ta = threading.Thread(target=run, args=("a", a, [(0, 100), (0, 3000), (0, 50), (0, 3000)]))
+    tb = threading.Thread(target=run, args=("b", b, [(0, 3000), (0, 10), (0, 3000)]))
+    ta.start(); tb.start(); ta.join(); tb.join()
+    a.close(); b.close()
+    assert errs == []
+    for res in (out["a"][1], out["a"][3], out["b"][0], out["b"][2]):
+        assert_same_results(res, want, batch)
+
+
+def test_many_contigs_device_scan_branch():
+    """> 32K active contigs at level 0 takes the hipcub segment-offset scan instead of the
+    one-workgroup scan: the whole batch must equal its shards (each below the threshold)
+    and the oracle on a sample."""
+    data = synth.generate(n=40000, genes=2, clades=30, seed=71, decoys=1, lgt_frac=0.2)
+    batch, tax = synth.to_batch(data)
+    params = cli.param_dict(cli.parse_flags([]))
+    s = engine.GpuScorer(0)
+    s.set_taxonomy(tax)
+    whole = s.score(batch, params)
+    parts = [s.score(batch.slice(x, x + 20000), params) for x in (0, 20000)]
+    s.close()
+    assert_same_results(whole, engine.Results.concat(parts, [0, int(batch.hit_off[20000])]), batch)
+    sub = batch.slice(30000, 30400)
+    otax = orc.Taxonomy(data.tax.edges)
+    contigs = orc.score_contigs(dict(zip(sub.contig_names, sub.contig_lengths.tolist())),
+                                oracle_loci_from_batch(sub), oracle_hits_from_batch(sub, tax),
+                                otax, orc.Params(**params))
+    got = engine.Results(**{f: getattr(whole, f) for f in engine.Results.__dataclass_fields__})
+    got = _slice_results(got, batch, 30000, 30400)
+    assert_same_results(got, oracle_results(contigs, sub, tax), sub)
+
+
+def _slice_results(res, batch, a, b):
+    h0, h1 = int(batch.hit_off[a]), int(batch.hit_off[b])
+    l0, l1 = int(batch.loc_off[a]), int(batch.loc_off[b])
+    nsys = len(batch.systems)
+    out = {}
+    for f in engine.Results.__dataclass_fields__:
+        v = getattr(res, f)
+        if f == "synteny":
+            out[f] = v[l0:l1]
+        elif f == "annot_hit":
+            w = v[l0 * nsys:l1 * nsys]
+            out[f] = np.where(w >= 0, w - h0, -1).astype(np.int32)
+        elif f == "meld":
+            out[f] = v[2 * h0 + 2 * a:2 * h1 + 2 * b]
+        else:
+            out[f] = v[a:b]
+    return engine.Results(**out)

@@ -1,5 +1,5 @@
 // C-ABI of libwaafle_hip.so (see include/waafle_hip.h): context/device management,
-// taxonomy upload, batch staging and the two-kernel launch sequence.
+// taxonomy upload, batch staging and the staged kernel sequence (wf_staged.hip).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,17 +29,7 @@ struct wf_ctx {
   // genecaller staging (host-resident calls)
   DevBuf gc_off, gc_qlo, gc_qhi, gc_strand, gc_scov, gc_ngenes, gc_gstart, gc_gstop, gc_gstrand, gc_status;
   bool have_lin = false;
-  // overflow work list + counter
-  DevBuf ovf_list, ovf2_list, ovf_count;
-  DevBuf retry_list, retry_count;
-  DevBuf big_ws;
-  DevBuf kargs;                    // device copies of the per-tier kernel argument blocks
-  std::vector<wf::KArgs> kargs_host;
-  int64_t lds_bytes = 24 * 1024;   // tier 1: two waves per contig (VGPR-bound: 4 per CU)
-  int lds_threads = 128;
-  int64_t lds2_bytes = 76 * 1024;  // tier 2: 256 threads, 2 workgroups per CU
-  int tier2_grid = 512;
-  int big_slots = 512;
+  int64_t lds_bytes = 24 * 1024;   // decision arena per workgroup (wf_set_lds_bytes)
   // staging for host-resident batches
   DevBuf b_hit_off, b_qlo, b_qhi, b_taxon, b_hstrand, b_score, b_scov, b_sysmask;
   DevBuf b_loc_off, b_lstart, b_lend, b_lstrand;
@@ -48,10 +38,8 @@ struct wf_ctx {
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<int, int>> ev_lds, ev_big;  // indices into ev_pool
-  int64_t launches = 0, overflow_contigs = 0;
-  // path: WF_MODE_STAGED (flat kernels per phase) or WF_MODE_FUSED (workgroup per contig)
-  int mode = WF_MODE_STAGED;
+  std::vector<std::pair<int, int>> ev_lds;   // indices into ev_pool (one pair per pass)
+  int64_t launches = 0;
   bool lds_set = false;            // wf_set_lds_bytes called: also the staged decision arena
   wf::StagedState* staged = nullptr;
   // --write-details
@@ -173,17 +161,6 @@ wf::DevParams derive_params(const wf_params& p) {
   return d;
 }
 
-int64_t slot_estimate(const wf_batch* b) {
-  // persistent (loci + leaves + attachments) + one level (keys, segments, clades, S)
-  const int64_t H = std::max(b->max_hits, 1), G = std::max(b->max_loci, 1);
-  const int64_t A = 2 * H + 64;
-  int64_t npow = 1;
-  while (npow < A + 1) npow <<= 1;
-  const int64_t P = H + 1;
-  return 64 * G + 16 * (G * 24 + 8) + 36 * A + 8 * npow + 12 * (A + 2) +
-         P * (8 * G + 56) + G * 32 + 8 * G * std::max(b->n_systems, 1) + 4096;
-}
-
 }  // namespace
 
 extern "C" {
@@ -215,11 +192,6 @@ int wf_init(int device, wf_ctx** out) {
     return WF_E_HIP;
   }
   ctx->stream = ctx->own_stream;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
-    ctx->big_slots = std::max(64, prop.multiProcessorCount * 2);
-    ctx->tier2_grid = std::max(64, prop.multiProcessorCount * 2);
-  }
   *out = ctx;
   return WF_OK;
 }
@@ -230,9 +202,7 @@ void wf_free(wf_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->lin, &ctx->gc_off,
                     &ctx->gc_qlo, &ctx->gc_qhi, &ctx->gc_strand, &ctx->gc_scov, &ctx->gc_ngenes,
-                    &ctx->gc_gstart, &ctx->gc_gstop, &ctx->gc_gstrand, &ctx->gc_status, &ctx->ovf_list,
-                    &ctx->ovf2_list, &ctx->kargs,
-                    &ctx->ovf_count, &ctx->retry_list, &ctx->retry_count, &ctx->big_ws,
+                    &ctx->gc_gstart, &ctx->gc_gstop, &ctx->gc_gstrand, &ctx->gc_status,
                     &ctx->b_hit_off, &ctx->b_qlo, &ctx->b_qhi, &ctx->b_taxon, &ctx->b_hstrand,
                     &ctx->b_score, &ctx->b_scov, &ctx->b_sysmask, &ctx->b_loc_off,
                     &ctx->b_lstart, &ctx->b_lend, &ctx->b_lstrand, &ctx->r_call, &ctx->r_crit,
@@ -263,27 +233,10 @@ int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes) {
   return WF_OK;
 }
 
-int wf_set_workgroup(wf_ctx* ctx, int threads) {
-  if (!ctx) return WF_E_BADINPUT;
-  if (threads != 64 && threads != 128 && threads != 256)
-    return fail(ctx, WF_E_BADINPUT, "threads per contig must be 64, 128 or 256");
-  ctx->lds_threads = threads;
-  return WF_OK;
-}
-
-int wf_set_tier2_lds_bytes(wf_ctx* ctx, int64_t bytes) {
-  if (!ctx) return WF_E_BADINPUT;
-  if (bytes < 4096 || bytes > 152 * 1024)
-    return fail(ctx, WF_E_BADINPUT, "LDS budget %lld out of [4096, 155648]", (long long)bytes);
-  ctx->lds2_bytes = bytes;
-  return WF_OK;
-}
-
 int wf_set_mode(wf_ctx* ctx, int mode) {
   if (!ctx) return WF_E_BADINPUT;
-  if (mode != WF_MODE_STAGED && mode != WF_MODE_FUSED)
-    return fail(ctx, WF_E_BADINPUT, "mode must be WF_MODE_STAGED (0) or WF_MODE_FUSED (1)");
-  ctx->mode = mode;
+  if (mode != WF_MODE_STAGED)
+    return fail(ctx, WF_E_BADINPUT, "mode must be WF_MODE_STAGED (0): the fused form is retired");
   return WF_OK;
 }
 
@@ -378,82 +331,23 @@ static int check_batch(wf_ctx* ctx, const wf_batch* b, const wf_params* p, const
   return WF_OK;
 }
 
-// Tier 1 (one wave per contig, small LDS) -> tier 2 (256 threads, large LDS, persistent
-// over tier 1's overflow list) -> tier 3 (HBM workspace slots, persistent over tier 2's
-// overflow list).  Everything is enqueued on the context stream; no host synchronisation.
+// The staged sequence on the context stream (wf_staged.hip), bracketed by timing events.
 static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
-  int rc;
-  if (ctx->details_on && ctx->mode != WF_MODE_STAGED)
-    return fail(ctx, WF_E_STATE, "--write-details needs the staged mode");
-  if (ctx->mode == WF_MODE_STAGED) {
-    K.root = ctx->root;
-    K.unknown = ctx->unknown;
-    if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
-    if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
-    std::pair<int, int> el{-1, -1};
-    if (ctx->timing) {
-      take_event_pair(ctx, ctx->ev_lds);
-      el = ctx->ev_lds.back();
-      HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
-    }
-    std::string err;
-    rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->n_hits, b->n_loci, ctx->stream, &err,
-                          ctx->details_on ? &ctx->det : nullptr);
-    if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : WF_E_HIP, "%s", err.c_str());
-    if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
-    ++ctx->launches;
-    return WF_OK;
-  }
-  const size_t list_bytes = sizeof(int32_t) * (size_t)std::max(b->n_contigs, 1);
-  if ((rc = ensure(ctx, ctx->ovf_list, list_bytes)) || (rc = ensure(ctx, ctx->ovf2_list, list_bytes)) ||
-      (rc = ensure(ctx, ctx->ovf_count, 64)))
-    return rc;
-  int32_t* counts = static_cast<int32_t*>(ctx->ovf_count.p);
-  HIP_TRY(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(int32_t), ctx->stream));
-  const int64_t slot = slot_estimate(b);
-  const int slots = std::min(ctx->big_slots, std::max(b->n_contigs, 1));
-  if ((rc = ensure(ctx, ctx->big_ws, (size_t)slot * slots))) return rc;
-  K.big_ws = static_cast<char*>(ctx->big_ws.p);
-  K.slot_bytes = slot;
   K.root = ctx->root;
   K.unknown = ctx->unknown;
-
-  wf::KArgs k1 = K, k2 = K, k3 = K;
-  k1.lds_bytes = ctx->lds_bytes;
-  k1.lds_threads = ctx->lds_threads;
-  k1.ovf_list = static_cast<int32_t*>(ctx->ovf_list.p);
-  k1.ovf_count = counts;
-  k2.lds_bytes = ctx->lds2_bytes;
-  k2.lds_threads = 256;
-  k2.work_list = k1.ovf_list;
-  k2.work_count = counts;
-  k2.ovf_list = static_cast<int32_t*>(ctx->ovf2_list.p);
-  k2.ovf_count = counts + 1;
-  k3.work_list = k2.ovf_list;
-  k3.work_count = counts + 1;
-  K = k3;   // the host-mode retry loop reuses the tier-3 arguments
-  if ((rc = ensure(ctx, ctx->kargs, 4 * sizeof(wf::KArgs)))) return rc;
-  wf::KArgs* dk = static_cast<wf::KArgs*>(ctx->kargs.p);
-  ctx->kargs_host.assign({k1, k2, k3});
-  HIP_TRY(ctx, hipMemcpyAsync(dk, ctx->kargs_host.data(), 3 * sizeof(wf::KArgs),
-                              hipMemcpyHostToDevice, ctx->stream));
-
-  std::pair<int, int> el{-1, -1}, eb{-1, -1};
+  if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
+  if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
+  std::pair<int, int> el{-1, -1};
   if (ctx->timing) {
-    take_event_pair(ctx, ctx->ev_lds);
+    if (take_event_pair(ctx, ctx->ev_lds) < 0) return fail(ctx, WF_E_HIP, "hipEventCreate failed");
     el = ctx->ev_lds.back();
-    take_event_pair(ctx, ctx->ev_big);
-    eb = ctx->ev_big.back();
+    HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
   }
-  if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
-  HIP_TRY(ctx, wf::launch_lds_kernel(k1, dk, ctx->stream));
+  std::string err;
+  const int rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->n_hits, b->n_loci, ctx->stream,
+                                  &err, ctx->details_on ? &ctx->det : nullptr);
+  if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : WF_E_HIP, "%s", err.c_str());
   if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
-  if (eb.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[eb.first], ctx->stream));
-  HIP_TRY(ctx, wf::launch_lds_list_kernel(k2, dk + 1,
-                                          std::min(ctx->tier2_grid, std::max(b->n_contigs, 1)),
-                                          ctx->stream));
-  HIP_TRY(ctx, wf::launch_big_kernel(dk + 2, slots, ctx->stream));
-  if (eb.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[eb.second], ctx->stream));
   ++ctx->launches;
   return WF_OK;
 }
@@ -487,7 +381,7 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
     return run_kernels(ctx, K, b);
   }
 
-  // host-resident: stage, run, copy back, retry workspace overflows with exact sizes
+  // host-resident: stage, run, copy back
   if ((rc = upload(ctx, ctx->b_hit_off, b->hit_off, N + 1, &K.hit_off)) ||
       (rc = upload(ctx, ctx->b_qlo, b->hit_qlo, NH, &K.qlo)) ||
       (rc = upload(ctx, ctx->b_qhi, b->hit_qhi, NH, &K.qhi)) ||
@@ -521,43 +415,6 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
     return rc;
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
 
-  // contigs whose state outgrew the estimated HBM slot: rerun with an exact slot size
-  for (int attempt = 0; attempt < 4; ++attempt) {
-    std::vector<int32_t> retry;
-    int64_t need = 0;
-    for (int32_t c = 0; c < b->n_contigs; ++c)
-      if (r->status[c] == WF_E_NOMEM || r->status[c] == wf::kPending) {
-        retry.push_back(c);
-        need = std::max(need, r->need_bytes[c]);
-      }
-    if (retry.empty()) break;
-    ctx->overflow_contigs += (int64_t)retry.size();
-    need = std::max<int64_t>(need * 2, 1 << 20);
-    const int slots = std::min<int>(ctx->big_slots, (int)retry.size());
-    const int32_t count = (int32_t)retry.size();
-    if ((rc = ensure(ctx, ctx->big_ws, (size_t)need * slots)) ||
-        (rc = ensure(ctx, ctx->retry_list, sizeof(int32_t) * retry.size())) ||
-        (rc = ensure(ctx, ctx->retry_count, 64)))
-      return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->retry_list.p, retry.data(), sizeof(int32_t) * retry.size(),
-                                hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->retry_count.p, &count, sizeof(int32_t), hipMemcpyHostToDevice,
-                                ctx->stream));
-    K.work_list = static_cast<const int32_t*>(ctx->retry_list.p);
-    K.work_count = static_cast<const int32_t*>(ctx->retry_count.p);
-    K.big_ws = static_cast<char*>(ctx->big_ws.p);
-    K.slot_bytes = need;
-    wf::KArgs* dk = static_cast<wf::KArgs*>(ctx->kargs.p) + 3;
-    ctx->kargs_host.assign({K});
-    HIP_TRY(ctx, hipMemcpyAsync(dk, ctx->kargs_host.data(), sizeof(wf::KArgs),
-                                hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, wf::launch_big_kernel(dk, slots, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if ((rc = download(ctx, r->status, K.status, N)) ||
-        (rc = download(ctx, r->need_bytes, K.need, N)))
-      return rc;
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  }
   if ((rc = download(ctx, r->call, K.call, N)) || (rc = download(ctx, r->crit, K.crit, N)) ||
       (rc = download(ctx, r->rank, K.rank, N)) || (rc = download(ctx, r->clade1, K.c1, N)) ||
       (rc = download(ctx, r->clade2, K.c2, N)) || (rc = download(ctx, r->direction, K.dir, N)) ||
@@ -570,8 +427,7 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   for (int32_t c = 0; c < b->n_contigs; ++c)
     if (r->status[c] != 0)
-      return fail(ctx, r->status[c] == wf::kPending ? WF_E_NOMEM : r->status[c],
-                  "contig %d failed with status %d", c, r->status[c]);
+      return fail(ctx, r->status[c], "contig %d failed with status %d", c, r->status[c]);
   return WF_OK;
 }
 
@@ -652,8 +508,6 @@ int wf_genecall(wf_ctx* ctx, const wf_gc_batch* b, const wf_gc_params* p, wf_gc_
 
 int wf_details_enable(wf_ctx* ctx, int on) {
   if (!ctx) return WF_E_BADINPUT;
-  if (on && ctx->mode != WF_MODE_STAGED)
-    return fail(ctx, WF_E_STATE, "--write-details needs the staged mode");
   ctx->details_on = on != 0;
   ctx->det.levels.clear();
   return WF_OK;
@@ -710,9 +564,7 @@ int wf_timing_enable(wf_ctx* ctx, int on) {
   for (hipEvent_t ev : ctx->ev_pool) (void)hipEventDestroy(ev);
   ctx->ev_pool.clear();
   ctx->ev_lds.clear();
-  ctx->ev_big.clear();
   ctx->launches = 0;
-  ctx->overflow_contigs = 0;
   ctx->timing = on != 0;
   return WF_OK;
 }
@@ -721,21 +573,14 @@ int wf_timing_read(wf_ctx* ctx, wf_timing* out) {
   if (!ctx || !out) return WF_E_BADINPUT;
   HIP_TRY(ctx, hipSetDevice(ctx->device));
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-  double lds = 0.0, big = 0.0;
+  double total = 0.0;
   for (auto& pr : ctx->ev_lds) {
     float ms = 0.f;
     HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev_pool[pr.first], ctx->ev_pool[pr.second]));
-    lds += ms;
+    total += ms;
   }
-  for (auto& pr : ctx->ev_big) {
-    float ms = 0.f;
-    HIP_TRY(ctx, hipEventElapsedTime(&ms, ctx->ev_pool[pr.first], ctx->ev_pool[pr.second]));
-    big += ms;
-  }
-  out->lds_kernel_ms = lds;
-  out->big_kernel_ms = big;
-  out->launches = (int64_t)ctx->ev_lds.size();
-  out->overflow_contigs = ctx->overflow_contigs;
+  out->pass_ms = total;
+  out->passes = (int64_t)ctx->ev_lds.size();
   return WF_OK;
 }
 

@@ -1,5 +1,5 @@
-// Internal definitions shared by the HIP kernels (wf_kernels.hip) and the C-ABI
-// implementation (wf_api.cpp).  Not part of the public interface.
+// Internal definitions shared by the HIP kernels (wf_staged.hip, wf_genecall.hip) and the
+// C-ABI implementation (wf_api.cpp).  Not part of the public interface.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -15,7 +15,6 @@ constexpr int kLeafMax = 128;           // numpy pairwise-sum leaf size (PW_BLOC
 constexpr int kNpyBuf = 8192;           // numpy reduction buffer (NPY_BUFSIZE)
 constexpr int kLeafSlots = 160;         // >= leaves of one 8192-element buffer
 constexpr int kMaxIter = 100;           // orgscorer.py:580
-constexpr int kPending = 1;             // status: handed to the overflow kernel
 constexpr int kLin = 16;                // lineage row: ancestors at depths 0..15 (64 B)
 
 // Parameters with the derived thresholds precomputed on the host
@@ -44,10 +43,8 @@ struct KArgs {
   int8_t* call; double* crit; double* rank; int32_t* c1; int32_t* c2; int8_t* dir;
   int16_t* iters; uint8_t* syn; int32_t* nm1; int32_t* nm2; int32_t* meld; int32_t* annot;
   int64_t* pair_evals; int32_t* status; int64_t* need;
-  // overflow work list (filled by the LDS kernel, drained by the HBM-workspace kernel)
-  int32_t* ovf_list; int32_t* ovf_count;
-  const int32_t* work_list; const int32_t* work_count;   // list the big kernel drains
-  char* big_ws; int64_t slot_bytes; int64_t lds_bytes; int lds_threads;
+  // HBM decision slots for contigs whose state outgrows the LDS arena (k_decide_big)
+  char* big_ws; int64_t slot_bytes;
 };
 
 // Staged pipeline state (wf_staged.hip): flat kernels over all hits / attachments /
@@ -135,10 +132,5 @@ void staged_set_lds(StagedState* st, int64_t bytes);
 // the message in *err (-1 bad input, -2 HIP failure).
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t n_hits,
                  int64_t n_loci, hipStream_t s, std::string* err, DetailsSink* det = nullptr);
-
-// `dk` points to a device copy of the host-side `k` (enqueued before the launch).
-hipError_t launch_lds_kernel(const KArgs& k, const KArgs* dk, hipStream_t s);
-hipError_t launch_lds_list_kernel(const KArgs& k, const KArgs* dk, int grid, hipStream_t s);
-hipError_t launch_big_kernel(const KArgs* dk, int grid, hipStream_t s);
 
 }  // namespace wf

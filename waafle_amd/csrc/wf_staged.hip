@@ -1472,20 +1472,19 @@ int bits_for(int64_t v) {   // bits to hold values 0..v
   return b;
 }
 
-hipStream_t g_sync_stream = nullptr;   // stream drained before any buffer is reallocated
-
+// Device scratch owned by one context's StagedState.  `drain` is the stream the context's
+// kernels run on: it is drained before an allocation is replaced (queued kernels may still
+// use the old one).  Per call, never a process global: contexts on different host threads
+// must not drain -- or race on -- each other's streams.
 struct Buf {
   void* p = nullptr;
   size_t n = 0;
   ~Buf() { if (p) (void)hipFree(p); }
-  hipError_t ensure(size_t bytes) {
+  hipError_t ensure(hipStream_t drain, size_t bytes) {
     if (bytes <= n) return hipSuccess;
     if (p) {
-      // queued kernels may still use the old allocation: drain the stream first
-      if (g_sync_stream) {
-        hipError_t e = hipStreamSynchronize(g_sync_stream);
-        if (e != hipSuccess) return e;
-      }
+      hipError_t e = hipStreamSynchronize(drain);
+      if (e != hipSuccess) return e;
       (void)hipFree(p);
       p = nullptr;
       n = 0;
@@ -1569,9 +1568,9 @@ void staged_set_lds(StagedState* st, int64_t bytes) {
 
 static int build_lut(StagedState* st, hipStream_t s, std::string* err) {
   if (st->lut_ready) return 0;
-  ST_TRY(st->lut_off.ensure((kNpyBuf + 2) * sizeof(int32_t)));
+  ST_TRY(st->lut_off.ensure(s, (kNpyBuf + 2) * sizeof(int32_t)));
   Buf counts;
-  ST_TRY(counts.ensure((kNpyBuf + 2) * sizeof(int32_t)));
+  ST_TRY(counts.ensure(s, (kNpyBuf + 2) * sizeof(int32_t)));
   hipLaunchKernelGGL(k_lut_count, dim3((kNpyBuf + 256) / 256), dim3(256), 0, s, counts.as<int32_t>());
   ST_TRY(hipGetLastError());
   std::vector<int32_t> h(kNpyBuf + 2, 0);
@@ -1579,7 +1578,7 @@ static int build_lut(StagedState* st, hipStream_t s, std::string* err) {
   ST_TRY(hipStreamSynchronize(s));
   std::vector<int32_t> off(kNpyBuf + 2, 0);
   for (int n = 0; n <= kNpyBuf; ++n) off[n + 1] = off[n] + h[n];
-  ST_TRY(st->lut.ensure((size_t)off[kNpyBuf + 1] * sizeof(int4)));
+  ST_TRY(st->lut.ensure(s, (size_t)off[kNpyBuf + 1] * sizeof(int4)));
   ST_TRY(hipMemcpyAsync(st->lut_off.p, off.data(), (kNpyBuf + 2) * sizeof(int32_t), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_lut_fill, dim3((kNpyBuf + 256) / 256), dim3(256), 0, s, st->lut_off.as<int32_t>(),
                      st->lut.as<int4>());
@@ -1712,7 +1711,6 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
                  hipStream_t s, std::string* err, DetailsSink* det) {
   const int N = k.n_contigs;
   if (N <= 0) return 0;
-  g_sync_stream = s;
   if (!st->host_counters || !st->host_lvl || !st->lvl_ev[0] || !st->lvl_ev[1]) {
     *err = "pinned host allocation / event creation failed";
     return -2;
@@ -1732,14 +1730,14 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   sa.dec_lds_bytes = st->dec_lds;
   // kernels take SArgs by value (kernarg segment): no argument uploads, and the pointers
   // loaded from it are known to be global (global_* instead of flat_* memory operations)
-  ST_TRY(st->counters.ensure(8 * sizeof(unsigned long long)));
+  ST_TRY(st->counters.ensure(s, 8 * sizeof(unsigned long long)));
   sa.counters = st->counters.as<unsigned long long>();
 
   // contigs, hits -> attachments (per-contig counts, offsets, then the attachments)
-  ST_TRY(st->cnt.ensure((size_t)(N + 1) * sizeof(int64_t)));
-  ST_TRY(st->cnt_leaves.ensure((size_t)(N + 1) * sizeof(int64_t)));
-  ST_TRY(st->att_off.ensure((size_t)(N + 1) * sizeof(int64_t)));
-  ST_TRY(st->red.ensure(2 * sizeof(int64_t)));
+  ST_TRY(st->cnt.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
+  ST_TRY(st->cnt_leaves.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
+  ST_TRY(st->att_off.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
+  ST_TRY(st->red.ensure(s, 2 * sizeof(int64_t)));
   sa.catt_off = st->att_off.as<int64_t>();
   static const char* ag_env = getenv("WF_ATT_GRID");        // blocks per CU (measurement aid)
   const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * (ag_env ? atoi(ag_env) : 32));
@@ -1760,7 +1758,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     size_t t3 = 0;
     ST_TRY(hipcub::DeviceReduce::Max(nullptr, t3, st->cnt.as<int64_t>(), st->red.as<int64_t>() + 1,
                                      (int)(N + 1), s));
-    ST_TRY(st->tmp.ensure(std::max(t1, std::max(t2, t3))));
+    ST_TRY(st->tmp.ensure(s, std::max(t1, std::max(t2, t3))));
     size_t tb = st->tmp.n;
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, tb, st->cnt.as<int64_t>(),
                                             st->att_off.as<int64_t>(), (int)(N + 1), s));
@@ -1796,33 +1794,33 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     return -1;
   }
   const size_t A1 = (size_t)std::max<int64_t>(A, 1), T1 = (size_t)std::max<int64_t>(TLB, 1);
-  ST_TRY(st->att_lo.ensure(A1 * 4)); ST_TRY(st->att_hi.ensure(A1 * 4));
-  ST_TRY(st->att_loc.ensure(A1 * 4)); ST_TRY(st->att_clade.ensure(A1 * 4));
-  ST_TRY(st->att_hit.ensure(A1 * 4)); ST_TRY(st->att_sc.ensure(A1 * 8));
-  ST_TRY(st->keys0.ensure(A1 * 8)); ST_TRY(st->keys1.ensure(A1 * 8));
-  ST_TRY(st->vals0.ensure(A1 * 4)); ST_TRY(st->vals1.ensure(A1 * 4));
-  ST_TRY(st->flags.ensure(A1 * 4)); ST_TRY(st->seg_id.ensure(A1 * 4));
-  ST_TRY(st->seg_start.ensure((A1 + 1) * 4)); ST_TRY(st->seg_crank.ensure(A1 * 4));
-  ST_TRY(st->seg_mean.ensure(A1 * 8));
-  ST_TRY(st->seg_nleaf.ensure((A1 + 1) * 4)); ST_TRY(st->leaf_off.ensure((A1 + 1) * 4));
-  ST_TRY(st->leaf_seg.ensure(T1 * 4)); ST_TRY(st->leaf_val.ensure(T1 * 8));
-  ST_TRY(st->seg_rec.ensure(A1 * 16)); ST_TRY(st->seg_cg.ensure(A1 * 8));
-  ST_TRY(st->wave_list.ensure(A1 * 4));
-  ST_TRY(st->crank_first.ensure(((size_t)N + 1) * 4));
-  ST_TRY(st->seg_cnt.ensure(((size_t)N + 1) * 4));
-  ST_TRY(st->lmax.ensure((size_t)std::max<int64_t>(NL, 1) * 8));
-  ST_TRY(st->c_gu.ensure((size_t)N * 4)); ST_TRY(st->c_umask.ensure((size_t)N * 8));
-  ST_TRY(st->c_best.ensure((size_t)N * 8)); ST_TRY(st->c_bestcl.ensure((size_t)N * 4));
-  ST_TRY(st->c_nopt.ensure((size_t)N * 4));
-  ST_TRY(st->run_crit.ensure(A1 * 8)); ST_TRY(st->run_rank.ensure(A1 * 8));
-  ST_TRY(st->satt_lohi.ensure(A1 * 8)); ST_TRY(st->satt_sc.ensure(A1 * 8));
-  ST_TRY(st->act0.ensure((size_t)N * 4)); ST_TRY(st->act1.ensure((size_t)N * 4));
-  ST_TRY(st->base0.ensure((size_t)N * 8)); ST_TRY(st->base1.ensure((size_t)N * 8));
-  ST_TRY(st->big_list.ensure((size_t)N * 8));
-  ST_TRY(st->two_list.ensure((size_t)N * 8));
-  ST_TRY(st->one_list.ensure((size_t)N * 8));
+  ST_TRY(st->att_lo.ensure(s, A1 * 4)); ST_TRY(st->att_hi.ensure(s, A1 * 4));
+  ST_TRY(st->att_loc.ensure(s, A1 * 4)); ST_TRY(st->att_clade.ensure(s, A1 * 4));
+  ST_TRY(st->att_hit.ensure(s, A1 * 4)); ST_TRY(st->att_sc.ensure(s, A1 * 8));
+  ST_TRY(st->keys0.ensure(s, A1 * 8)); ST_TRY(st->keys1.ensure(s, A1 * 8));
+  ST_TRY(st->vals0.ensure(s, A1 * 4)); ST_TRY(st->vals1.ensure(s, A1 * 4));
+  ST_TRY(st->flags.ensure(s, A1 * 4)); ST_TRY(st->seg_id.ensure(s, A1 * 4));
+  ST_TRY(st->seg_start.ensure(s, (A1 + 1) * 4)); ST_TRY(st->seg_crank.ensure(s, A1 * 4));
+  ST_TRY(st->seg_mean.ensure(s, A1 * 8));
+  ST_TRY(st->seg_nleaf.ensure(s, (A1 + 1) * 4)); ST_TRY(st->leaf_off.ensure(s, (A1 + 1) * 4));
+  ST_TRY(st->leaf_seg.ensure(s, T1 * 4)); ST_TRY(st->leaf_val.ensure(s, T1 * 8));
+  ST_TRY(st->seg_rec.ensure(s, A1 * 16)); ST_TRY(st->seg_cg.ensure(s, A1 * 8));
+  ST_TRY(st->wave_list.ensure(s, A1 * 4));
+  ST_TRY(st->crank_first.ensure(s, ((size_t)N + 1) * 4));
+  ST_TRY(st->seg_cnt.ensure(s, ((size_t)N + 1) * 4));
+  ST_TRY(st->lmax.ensure(s, (size_t)std::max<int64_t>(NL, 1) * 8));
+  ST_TRY(st->c_gu.ensure(s, (size_t)N * 4)); ST_TRY(st->c_umask.ensure(s, (size_t)N * 8));
+  ST_TRY(st->c_best.ensure(s, (size_t)N * 8)); ST_TRY(st->c_bestcl.ensure(s, (size_t)N * 4));
+  ST_TRY(st->c_nopt.ensure(s, (size_t)N * 4));
+  ST_TRY(st->run_crit.ensure(s, A1 * 8)); ST_TRY(st->run_rank.ensure(s, A1 * 8));
+  ST_TRY(st->satt_lohi.ensure(s, A1 * 8)); ST_TRY(st->satt_sc.ensure(s, A1 * 8));
+  ST_TRY(st->act0.ensure(s, (size_t)N * 4)); ST_TRY(st->act1.ensure(s, (size_t)N * 4));
+  ST_TRY(st->base0.ensure(s, (size_t)N * 8)); ST_TRY(st->base1.ensure(s, (size_t)N * 8));
+  ST_TRY(st->big_list.ensure(s, (size_t)N * 8));
+  ST_TRY(st->two_list.ensure(s, (size_t)N * 8));
+  ST_TRY(st->one_list.ensure(s, (size_t)N * 8));
   const int64_t n_annot = NL * k.n_sys;
-  if (n_annot > 0) ST_TRY(st->annot_best.ensure((size_t)n_annot * 8));
+  if (n_annot > 0) ST_TRY(st->annot_best.ensure(s, (size_t)n_annot * 8));
   {
     // temp storage for every primitive of this call, sized once (no reallocation between
     // enqueued kernels)
@@ -1837,7 +1835,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     size_t t4 = 0;
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t4, st->seg_cnt.as<int32_t>(),
                                             st->crank_first.as<int32_t>(), N + 1, s));
-    ST_TRY(st->tmp.ensure(std::max(std::max(t1, t4), std::max(t2, t3))));
+    ST_TRY(st->tmp.ensure(s, std::max(std::max(t1, t4), std::max(t2, t3))));
   }
   sa.att_lo = st->att_lo.as<int32_t>(); sa.att_hi = st->att_hi.as<int32_t>();
   sa.att_loc = st->att_loc.as<int32_t>(); sa.att_clade = st->att_clade.as<int32_t>();
@@ -1851,7 +1849,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   sa.seg_cg = st->seg_cg.as<int2>();
   sa.crank_first = st->crank_first.as<int32_t>();
   sa.seg_cnt = st->seg_cnt.as<int32_t>();
-  ST_TRY(st->seg_len.ensure(A1 * 4));
+  ST_TRY(st->seg_len.ensure(s, A1 * 4));
   sa.seg_len = sa.sort_cap > 0 ? st->seg_len.as<int32_t>() : nullptr;   // set by k_seg_build
   sa.lmax = st->lmax.as<uint64_t>();
   sa.c_gu = st->c_gu.as<int32_t>(); sa.c_umask = st->c_umask.as<uint64_t>();
@@ -1899,7 +1897,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   // device, while the host waits for level L-1's count word -- the GPU never idles on a
   // host round trip, and one empty level is enqueued at the end.
   const int n_lv = kMaxIter + 2;
-  ST_TRY(st->lvl_ctr.ensure((size_t)n_lv * 8 * sizeof(unsigned long long)));
+  ST_TRY(st->lvl_ctr.ensure(s, (size_t)n_lv * 8 * sizeof(unsigned long long)));
   ST_TRY(hipMemsetAsync(st->lvl_ctr.p, 0, (size_t)n_lv * 8 * sizeof(unsigned long long), s));
   unsigned long long* lvl_ctr = st->lvl_ctr.as<unsigned long long>();
   // Measured on cfg2: the host round trips it removes (~0.1 ms per pass) are paid back by
@@ -1911,8 +1909,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   int64_t n_keys = A;
   if (det) {
     det->levels.clear();
-    ST_TRY(st->span_cnt.ensure(A1 * 4));
-    ST_TRY(st->spans.ensure(A1 * 8));
+    ST_TRY(st->span_cnt.ensure(s, A1 * 4));
+    ST_TRY(st->spans.ensure(s, A1 * 8));
   }
   for (int level = 0; n_act > 0 && level <= kMaxIter; ++level) {
     const bool async = pipelined && level >= 1;
@@ -2073,7 +2071,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     if (n_big > 0) {
       const int64_t slot = ((int64_t)st->host_counters[3] + 255) & ~int64_t(255);
       const int slots = std::min(n_big, st->cus * 2);
-      ST_TRY(st->big_ws.ensure((size_t)slot * slots));
+      ST_TRY(st->big_ws.ensure(s, (size_t)slot * slots));
       sa.k.big_ws = st->big_ws.as<char>();
       sa.k.slot_bytes = slot;
       hipLaunchKernelGGL(k_decide_big, dim3(slots), dim3(kBlock), 0, s, sa, level, n_keys, n_big);
@@ -2090,7 +2088,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
       // HBM decision slots for the pipelined levels, sized for the largest possible contig
       const int64_t slot = (arena_bound(max_att + 2, max_loci) + 255) & ~int64_t(255);
       st->big_slots = st->cus * 2;
-      ST_TRY(st->big_ws.ensure((size_t)slot * st->big_slots));
+      ST_TRY(st->big_ws.ensure(s, (size_t)slot * st->big_slots));
       sa.k.big_ws = st->big_ws.as<char>();
       sa.k.slot_bytes = slot;
     }

@@ -54,7 +54,8 @@ def score_ranked(batch, tax, params, score_shard, dist):
     if dist is None:
         return score_shard(batch)
     rank, world = dist.get_rank(), dist.get_world_size()
-    bounds = rank_bounds(contig_cost(batch), world)
+    k2 = float(params.get("two_clade_threshold", 0.8)) if isinstance(params, dict) else 0.8
+    bounds = rank_bounds(contig_cost(batch, k2), world)
     a, b = bounds[rank]
     try:
         local = score_shard(batch.slice(a, b))

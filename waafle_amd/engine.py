@@ -19,7 +19,7 @@ DIS_ONE = {"report-best": 0, "meld": 1}
 DIS_TWO = {"report-best": 0, "jump": 1, "meld": 2}
 LEVEL = {"off": 0, "lenient": 1, "strict": 2}
 WEAK = {"ignore": 0, "penalize": 1, "assign-unknown": 2}
-MODES = {"staged": L.MODE_STAGED, "fused": L.MODE_FUSED}
+MODES = {"staged": L.MODE_STAGED}
 
 
 def params_struct(p):
@@ -104,7 +104,7 @@ def taxonomy_struct(t):
 class GpuScorer:
     """One libwaafle_hip context on one device."""
 
-    def __init__(self, device=0, lds_bytes=None, threads=None, tier2_lds_bytes=None, mode=None):
+    def __init__(self, device=0, lds_bytes=None, mode=None):
         self.lib = L.load()
         h = C.c_void_p()
         rc = self.lib.wf_init(int(device), C.byref(h))
@@ -116,10 +116,6 @@ class GpuScorer:
             self._check(self.lib.wf_set_mode(self.h, MODES[mode] if isinstance(mode, str) else int(mode)))
         if lds_bytes:
             self._check(self.lib.wf_set_lds_bytes(self.h, int(lds_bytes)))
-        if threads:
-            self._check(self.lib.wf_set_workgroup(self.h, int(threads)))
-        if tier2_lds_bytes:
-            self._check(self.lib.wf_set_tier2_lds_bytes(self.h, int(tier2_lds_bytes)))
 
     def _check(self, rc):
         if rc != L.WF_OK:
@@ -185,10 +181,31 @@ class GpuScorer:
             pass
 
 
-def contig_cost(batch):
-    """Cost estimate per contig for balancing shards: hits x loci (attach + site work)."""
-    return np.diff(batch.hit_off).astype(np.float64) * np.maximum(
-        1, np.diff(batch.loc_off)).astype(np.float64) + 1.0
+def contig_cost(batch, k2=0.8):
+    """Estimated work per contig for balancing shards:
+    w = H + sum_loci len * P_c + G * P_pot^2, with P_c = distinct hit taxa of the contig and
+    P_pot = distinct taxa with a hit scoring >= k2 (an upper bound of the clades whose best
+    gene score reaches k2: a gene score is a mean of sites no higher than the best hit).
+    The k2 term is the explain_two all-pairs search; it dominates skewed batches (cfg5
+    stress contigs cost ~P_pot^2 * G where an ordinary contig costs ~H)."""
+    N = batch.n_contigs
+    H = np.diff(batch.hit_off).astype(np.float64)
+    G = np.diff(batch.loc_off).astype(np.float64)
+    if N == 0:
+        return H
+    lens = (np.abs(batch.loc_end.astype(np.int64) - batch.loc_start.astype(np.int64)) + 1).astype(np.float64)
+    loc_contig = np.repeat(np.arange(N), np.diff(batch.loc_off))
+    len_sum = np.bincount(loc_contig, weights=lens, minlength=N)
+    hit_contig = np.repeat(np.arange(N, dtype=np.int64), np.diff(batch.hit_off))
+    ntax = np.int64(max(int(batch.hit_taxon.max()) + 1, 1)) if batch.n_hits else np.int64(1)
+
+    def distinct(mask):
+        pairs = np.unique(hit_contig[mask] * ntax + batch.hit_taxon[mask].astype(np.int64))
+        return np.bincount(pairs // ntax, minlength=N).astype(np.float64)
+
+    p_c = distinct(np.ones(batch.n_hits, bool))
+    p_pot = distinct(batch.hit_score >= k2)
+    return H + len_sum * p_c + G * p_pot * p_pot + 1.0
 
 
 def shard_bounds(cost, parts):
@@ -206,22 +223,29 @@ def shard_bounds(cost, parts):
     return [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a] or [(0, n)]
 
 
-def score(batch, tax, params, gpus=1, lds_bytes=None):
+def score(batch, tax, params, gpus=1, lds_bytes=None, devices=None):
+    """Score a batch on `gpus` devices: contiguous shards balanced by contig_cost, one
+    context and host thread per shard.  `devices[k]` is shard k's device (default k); two
+    shards may share a device (each context has its own stream and scratch)."""
     gpus = max(1, int(gpus))
     if gpus == 1:
-        s = GpuScorer(0, lds_bytes)
+        s = GpuScorer(devices[0] if devices else 0, lds_bytes)
         try:
             s.set_taxonomy(tax)
             return s.score(batch, params)
         finally:
             s.close()
-    bounds = shard_bounds(contig_cost(batch), gpus)
+    k2 = float(params.get("two_clade_threshold", 0.8)) if isinstance(params, dict) else 0.8
+    bounds = shard_bounds(contig_cost(batch, k2), gpus)
+    devs = list(devices) if devices else list(range(len(bounds)))
+    if len(devs) < len(bounds):
+        raise ValueError("devices: {} entries for {} shards".format(len(devs), len(bounds)))
     parts = [None] * len(bounds)
     errors = []
 
     def work(k, a, b):
         try:
-            s = GpuScorer(k, lds_bytes)
+            s = GpuScorer(devs[k], lds_bytes)
             try:
                 s.set_taxonomy(tax)
                 parts[k] = s.score(batch.slice(a, b), params)

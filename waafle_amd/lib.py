@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(HERE, "libwaafle_hip.so")
 WF_OK, WF_E_BADINPUT, WF_E_HIP, WF_E_RUNAWAY, WF_E_NOMEM, WF_E_STATE, WF_E_EMPTYMASK = \
     0, -1, -2, -3, -4, -5, -6
 CALL_UNCLASSIFIED, CALL_NO_LGT, CALL_LGT = 0, 1, 2
-MODE_STAGED, MODE_FUSED = 0, 1
+MODE_STAGED = 0
 
 _P = C.c_void_p
 
@@ -50,8 +50,7 @@ class WfResult(C.Structure):
 
 
 class WfTiming(C.Structure):
-    _fields_ = [("lds_kernel_ms", C.c_double), ("big_kernel_ms", C.c_double),
-                ("launches", C.c_int64), ("overflow_contigs", C.c_int64)]
+    _fields_ = [("pass_ms", C.c_double), ("passes", C.c_int64)]
 
 
 class WfGcBatch(C.Structure):
@@ -85,8 +84,6 @@ SIGNATURES = {
     "wf_last_error": (C.c_char_p, [C.c_void_p]),
     "wf_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "wf_set_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
-    "wf_set_workgroup": (C.c_int, [C.c_void_p, C.c_int]),
-    "wf_set_tier2_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
     "wf_set_mode": (C.c_int, [C.c_void_p, C.c_int]),
     "wf_set_taxonomy": (C.c_int, [C.c_void_p, C.POINTER(WfTaxonomy)]),
     "wf_score": (C.c_int, [C.c_void_p, C.POINTER(WfBatch), C.POINTER(WfParams),
@@ -126,7 +123,7 @@ def load(path=LIB_PATH):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.wf_abi_version() != 1:
+    if lib.wf_abi_version() != 2:
         raise ImportError("libwaafle_hip ABI mismatch")
     _lib = lib
     return lib

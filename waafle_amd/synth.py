@@ -107,6 +107,14 @@ def generate(n, genes, clades, decoys=20, lgt_frac=0.10, seed=0, stress=False,
              short_frac=0.0, name_prefix="contig"):
     rng = np.random.default_rng(seed)
     tax = make_taxonomy(clades, rng)
+    return _generate_contigs(rng, tax, n, genes, clades, decoys, lgt_frac, stress, short_frac,
+                             name_prefix, 0)
+
+
+def _generate_contigs(rng, tax, n, genes, clades, decoys, lgt_frac, stress, short_frac,
+                      name_prefix, first):
+    """Contigs `first .. first + n - 1` drawn from `rng` (generate() draws the taxonomy
+    from the same generator first; generate_chunk draws each chunk from its own)."""
     N, G = int(n), int(genes)
 
     glen = rng.integers(250, 1500, size=(N, G))
@@ -179,7 +187,7 @@ def generate(n, genes, clades, decoys=20, lgt_frac=0.10, seed=0, stress=False,
     order = np.lexsort((cat["qstart"], cat["contig"]))
     cat = {k: v[order] for k, v in cat.items()}
 
-    names = ["{}{}".format(name_prefix, i) for i in range(N)]
+    names = ["{}{}".format(name_prefix, first + i) for i in range(N)]
     return SynthData(
         tax=tax, contig_names=names, contig_lengths=clen.astype(np.int64),
         loc_contig=np.repeat(np.arange(N), G), loc_start=gstart.ravel().astype(np.int64),
@@ -191,6 +199,102 @@ def generate(n, genes, clades, decoys=20, lgt_frac=0.10, seed=0, stress=False,
         qstart=cat["qstart"].astype(np.int64), qend=cat["qend"].astype(np.int64),
         sstart=cat["sstart"].astype(np.int64), send=cat["send"].astype(np.int64),
         pident_milli=cat["pid"].astype(np.int64), minus=cat["minus"].astype(bool))
+
+
+CHUNK = 10_000     # contigs per independently seeded chunk (generate_chunk)
+
+
+def chunk_taxonomy(name, seed=None):
+    """Taxonomy of a chunked synthetic set: drawn from default_rng(seed) alone."""
+    spec = CONFIGS[name]
+    seed = int(name[-1]) if seed is None else seed
+    return make_taxonomy(spec["clades"], np.random.default_rng(seed))
+
+
+def generate_chunk(name, k, seed=None, tax=None, chunk=CHUNK, n_total=None):
+    """Chunk k (contigs k*chunk .. ) of a BASELINE config drawn from its own generator
+    default_rng([seed, k]) -- so any contig range is reproducible without generating
+    the contigs before it, and chunks can be generated in parallel.  Same per-contig
+    distributions as generate(); the taxonomy comes from chunk_taxonomy."""
+    spec = dict(CONFIGS[name])
+    seed = int(name[-1]) if seed is None else seed
+    n_total = spec["n"] if n_total is None else n_total
+    tax = chunk_taxonomy(name, seed) if tax is None else tax
+    first = k * chunk
+    n = min(chunk, n_total - first)
+    rng = np.random.default_rng([seed, k])
+    return _generate_contigs(rng, tax, n, spec["genes"], spec["clades"], 20, 0.10,
+                             spec.get("stress", False), 0.0, "contig", first)
+
+
+def _pack_chunk(args):
+    """Worker: chunk k -> the device arrays of its contigs (no names, no annotation text)."""
+    name, k, seed, chunk, n_total = args
+    d = generate_chunk(name, k, seed, chunk=chunk, n_total=n_total)
+    from .inputs import derive_hit_values
+    scov, score = derive_hit_values(d.qlen, d.slen, d.qstart, d.qend, d.sstart, d.send,
+                                    d.pident_milli / 1000.0, d.minus)
+    keep = (np.abs(d.loc_end - d.loc_start) + 1) >= 200.0
+    return dict(
+        hit_cnt=np.bincount(d.hit_contig, minlength=d.n_contigs).astype(np.int64),
+        loc_cnt=np.bincount(d.loc_contig[keep], minlength=d.n_contigs).astype(np.int64),
+        hit_qlo=np.minimum(d.qstart, d.qend).astype(np.int32),
+        hit_qhi=np.maximum(d.qstart, d.qend).astype(np.int32),
+        hit_clade=d.hit_clade.astype(np.int32), hit_strand=d.minus.astype(np.int8),
+        hit_score=score, hit_scov=scov,
+        loc_start=d.loc_start[keep].astype(np.int32), loc_end=d.loc_end[keep].astype(np.int32),
+        loc_strand=np.where(d.loc_strand[keep] == ord("-"), 1, 0).astype(np.int8),
+        contig_lengths=d.contig_lengths)
+
+
+def generate_batch(name, lo=0, hi=None, seed=None, workers=None, chunk=CHUNK, n_total=None):
+    """Contigs [lo, hi) of a BASELINE config (whole chunks) packed straight into a device
+    batch, chunks generated in parallel worker processes.  Returns (HostBatch,
+    TaxonomyTables).  The batch carries no contig names or annotation values (the bench
+    never renders TSVs); every hit has annotation system 0 (sysmask 1), as to_batch."""
+    from .inputs import HostBatch
+    from .taxonomy import TaxonomyTables
+    spec = CONFIGS[name]
+    n_total = spec["n"] if n_total is None else n_total
+    hi = n_total if hi is None else hi
+    seed = int(name[-1]) if seed is None else seed
+    st = make_taxonomy(spec["clades"], np.random.default_rng(seed))
+    tax = TaxonomyTables(st.edges)
+    clade_to_id = np.array([tax.index[sp] for sp in st.species], dtype=np.int32)
+    ks = list(range(lo // chunk, (hi + chunk - 1) // chunk))
+    jobs = [(name, k, seed, chunk, n_total) for k in ks]
+    if workers is None:
+        workers = min(16, len(os.sched_getaffinity(0)), len(jobs))
+    if workers > 1:
+        import multiprocessing as mp
+        with mp.get_context("fork").Pool(workers) as pool:
+            parts = pool.map(_pack_chunk, jobs, chunksize=1)
+    else:
+        parts = [_pack_chunk(j) for j in jobs]
+    # trim to [lo, hi)
+    c0 = lo - ks[0] * chunk
+    n = hi - lo
+    cat = lambda f: np.concatenate([p[f] for p in parts])
+    hit_cnt, loc_cnt = cat("hit_cnt"), cat("loc_cnt")
+    hoff = np.concatenate([[0], np.cumsum(hit_cnt)])
+    loff = np.concatenate([[0], np.cumsum(loc_cnt)])
+    ha, hb = int(hoff[c0]), int(hoff[c0 + n])
+    la, lb = int(loff[c0]), int(loff[c0 + n])
+    hit_off = (hoff[c0:c0 + n + 1] - ha).astype(np.int64)
+    loc_off = (loff[c0:c0 + n + 1] - la).astype(np.int64)
+
+    def hits(f):
+        return np.concatenate([p[f] for p in parts])[ha:hb]
+
+    batch = HostBatch(
+        contig_names=[], contig_lengths=cat("contig_lengths")[c0:c0 + n],
+        hit_off=hit_off, hit_qlo=hits("hit_qlo"), hit_qhi=hits("hit_qhi"),
+        hit_taxon=clade_to_id[hits("hit_clade")], hit_strand=hits("hit_strand"),
+        hit_score=hits("hit_score"), hit_scov=hits("hit_scov"),
+        hit_sysmask=np.ones(hb - ha, dtype=np.uint32), loc_off=loc_off,
+        loc_start=cat("loc_start")[la:lb], loc_end=cat("loc_end")[la:lb],
+        loc_strand=cat("loc_strand")[la:lb], systems=["UniProt"])
+    return batch, tax
 
 
 def generate_config(name, seed=None, n=None, **kw):
