@@ -47,9 +47,9 @@ def parse_args():
     ap.add_argument("--config", default="cfg4")
     ap.add_argument("--contigs", type=int, default=None, help="override total contigs")
     ap.add_argument("--lds-bytes", type=int, default=None)
-    ap.add_argument("--cpu-sample", type=int, default=1500,
+    ap.add_argument("--cpu-sample", type=int, default=5000,
                     help="contigs timed on the CPU oracle, 1 core (rank 0, N=1); 0 disables")
-    ap.add_argument("--cpu-shard", type=int, default=300,
+    ap.add_argument("--cpu-shard", type=int, default=600,
                     help="contigs per process of the parallel CPU leg; 0 disables")
     ap.add_argument("--e2e", default="cfg2", help="CLI end-to-end config ('' disables)")
     ap.add_argument("--pcie", type=int, default=1, help="time the host-array scope")
@@ -106,8 +106,7 @@ def cpu_baseline(config, n_one, n_shard):
     from oracle import orgscorer_oracle as orc
     from waafle_amd import cli, synth
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    data = synth.generate_chunk(config, 0) if config in ("cfg4", "cfg3") else \
-        synth.generate_config(config, n=min(synth.CONFIGS[config]["n"], synth.CHUNK))
+    data = synth.generate_chunk(config, 0)
     batch, tax = synth.to_batch(data, with_codes=False)
     _CPU.update(batch=batch, tax=tax, otax=orc.Taxonomy(data.tax.edges),
                 params=orc.Params(**cli.param_dict(cli.parse_flags([]))))

@@ -173,6 +173,53 @@ typedef struct wf_gc_result { /* same residency as the batch */
 
 int wf_genecall(wf_ctx* ctx, const wf_gc_batch* batch, const wf_gc_params* params, wf_gc_result* out);
 
+/* ---- waafle_junctions (waafle_junctions.py:252-316, 414-451) ---------------------------
+ * Read-pair support of gene-gene junctions.  For every concordant pair (two consecutive
+ * aligned SAM records with the same QNAME and RNAME, concordant_hits :252-275) the pair's
+ * span [min(coords) - 1, max(coords) - 1] adds 1 to the contig's per-site coverage
+ * (:432-436), and every locus overlapping either mate by >= min_overlap_sites sites
+ * (find_hit_loci :277-286) is hit.  For each pair of start-adjacent loci (j, j+1) of a
+ * contig (evaluate_contig :292-316): junction_hits = pairs hitting both, coverage_gene1/2 =
+ * mean coverage over each locus, coverage_junction = mean over [end(j) - 1, start(j+1))
+ * (0 when the loci touch or overlap), ratio = junction / (mean of the two genes + 1e-6).
+ * Slices follow Python's rules on the contig's coverage array; an empty slice gives NaN
+ * (np.mean of nothing).  Replaces the SAM loop of the reference's main() and its
+ * evaluate_contig calls. */
+typedef struct wf_jn_batch {
+  int32_t n_contigs;
+  int32_t device_resident;    /* 1: device pointers (enqueue only); 0: host arrays */
+  int64_t n_pairs;
+  int64_t n_loci;
+  const int64_t* contig_length; /* [n_contigs] FASTA lengths (read_contig_lengths) */
+  const int64_t* loc_off;     /* [n_contigs + 1] loci of each contig, sorted by start (stable) */
+  const int64_t* loc_start;   /* [n_loci] GFF start */
+  const int64_t* loc_end;     /* [n_loci] GFF end */
+  const int32_t* pair_contig; /* [n_pairs] contig of both mates */
+  const int64_t* m1_start;    /* [n_pairs] mate 1: POS, POS + cigar_length - 1 (utils.py:524-539) */
+  const int64_t* m1_end;
+  const int64_t* m2_start;    /* mate 2 */
+  const int64_t* m2_end;
+} wf_jn_batch;
+
+typedef struct wf_jn_params {
+  int64_t min_overlap_sites;  /* --min-overlap-sites, default 25 */
+} wf_jn_params;
+
+typedef struct wf_jn_result {   /* same residency as the batch */
+  int32_t* junction_hits;     /* [n_loci] at j: junction (j, j+1) of j's contig */
+  double* coverage_gene1;     /* [n_loci] */
+  double* coverage_gene2;
+  double* coverage_junction;
+  double* ratio;
+  int32_t* locus_hits;        /* [n_loci] pairs hitting locus j, or NULL */
+  int64_t* coverage;          /* [sum(contig_length)] per-site coverage, contig-major, or NULL */
+  int64_t* pair_first;        /* [n_pairs] first hit locus of each pair (-1: none), or NULL */
+  uint64_t* pair_mask;        /* [n_pairs] bit i: locus pair_first + i hit (the pair's code
+                                 set, :277-286; WF_E_NOMEM if hits span more than 64 loci) */
+} wf_jn_result;
+
+int wf_junctions(wf_ctx* ctx, const wf_jn_batch* batch, const wf_jn_params* params, wf_jn_result* out);
+
 /* ---- --write-details (orgscorer.py:766-812, 931-937) --------------------------------
  * With details on, the next wf_score (staged mode) also records, for every roll-up level,
  * the contigs it evaluated and each (contig, clade, locus) segment of that level: its gene

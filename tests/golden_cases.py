@@ -112,3 +112,31 @@ def compare_tsv(fixture, texts):
         if order_w != order_g:
             bad.append(("row order", kind))
     return bad
+
+
+def junction_names():
+    """waafle_junctions / waafle_qc fixtures (make_junctions.py)."""
+    return sorted(os.path.basename(p)[:-len(".junc.json.gz")]
+                  for p in glob.glob(os.path.join(GOLDEN, "*.junc.json.gz")))
+
+
+def load_junction(name):
+    with gzip.open(os.path.join(GOLDEN, name + ".junc.json.gz"), "rt") as fh:
+        return json.load(fh)
+
+
+def materialize_junction(fixture, tmpdir):
+    """(fna, gff, sam, lgt.tsv) paths for a junction fixture, rebuilt from its recipe."""
+    from waafle_amd import synth, synth_reads
+    r = fixture["recipe"]
+    sub = os.path.join(str(tmpdir), "junc_" + "_".join(
+        "{}{}".format(k, v) for k, v in sorted(r["generate"].items())))
+    fna, gff = os.path.join(sub, "synth.fna"), os.path.join(sub, "synth.gff")
+    sam, lgt = os.path.join(sub, "reads.sam"), os.path.join(sub, "synth.lgt.tsv")
+    if not os.path.exists(lgt):
+        data = synth.generate(**r["generate"])
+        synth.write_text(data, sub, "synth")
+        synth_reads.write_sam(data, sam, **r["reads"])
+        with open(lgt, "w") as fh:
+            fh.write(load(r["lgt_golden"])["tsv"]["lgt"])
+    return fna, gff, sam, lgt

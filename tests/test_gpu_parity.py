@@ -132,8 +132,9 @@ def test_gpu_deep_taxonomy_and_runaway(name, scorer, tmp_path):
     run = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert run.returncode == fx["returncode"]
-    want = fx["stderr"].strip().splitlines()
-    assert run.stderr.strip().splitlines()[-len(want):] == want
+    want = fx["stderr"].strip().splitlines()[-2:]        # the die: LETHAL ERROR + EXITING.
+    assert want[0].startswith("LETHAL ERROR:")
+    assert run.stderr.strip().splitlines()[-2:] == want
 
 
 def synth_case(tmp_path, flags=(), **kw):

@@ -28,6 +28,10 @@ struct wf_ctx {
   DevBuf parent, depth, sibp, leaves, lin;
   // genecaller staging (host-resident calls)
   DevBuf gc_off, gc_qlo, gc_qhi, gc_strand, gc_scov, gc_ngenes, gc_gstart, gc_gstop, gc_gstrand, gc_status;
+  // waafle_junctions staging and scratch
+  DevBuf jn_site_off, jn_loc_off, jn_loc_contig, jn_lstart, jn_lend, jn_pc, jn_m1s, jn_m1e, jn_m2s, jn_m2e;
+  DevBuf jn_diff, jn_cov, jn_prefix, jn_hits, jn_lhits, jn_c1, jn_c2, jn_cj, jn_ratio, jn_tmp;
+  DevBuf jn_pfirst, jn_pmask, jn_ovf;
   bool have_lin = false;
   int64_t lds_bytes = 24 * 1024;   // decision arena per workgroup (wf_set_lds_bytes)
   // staging for host-resident batches
@@ -203,6 +207,11 @@ void wf_free(wf_ctx* ctx) {
   DevBuf* bufs[] = {&ctx->parent, &ctx->depth, &ctx->sibp, &ctx->leaves, &ctx->lin, &ctx->gc_off,
                     &ctx->gc_qlo, &ctx->gc_qhi, &ctx->gc_strand, &ctx->gc_scov, &ctx->gc_ngenes,
                     &ctx->gc_gstart, &ctx->gc_gstop, &ctx->gc_gstrand, &ctx->gc_status,
+                    &ctx->jn_site_off, &ctx->jn_loc_off, &ctx->jn_loc_contig, &ctx->jn_lstart,
+                    &ctx->jn_lend, &ctx->jn_pc, &ctx->jn_m1s, &ctx->jn_m1e, &ctx->jn_m2s,
+                    &ctx->jn_m2e, &ctx->jn_diff, &ctx->jn_cov, &ctx->jn_prefix, &ctx->jn_hits,
+                    &ctx->jn_lhits, &ctx->jn_c1, &ctx->jn_c2, &ctx->jn_cj, &ctx->jn_ratio,
+                    &ctx->jn_tmp, &ctx->jn_pfirst, &ctx->jn_pmask, &ctx->jn_ovf,
                     &ctx->b_hit_off, &ctx->b_qlo, &ctx->b_qhi, &ctx->b_taxon, &ctx->b_hstrand,
                     &ctx->b_score, &ctx->b_scov, &ctx->b_sysmask, &ctx->b_loc_off,
                     &ctx->b_lstart, &ctx->b_lend, &ctx->b_lstrand, &ctx->r_call, &ctx->r_crit,
@@ -503,6 +512,108 @@ int wf_genecall(wf_ctx* ctx, const wf_gc_batch* b, const wf_gc_params* p, wf_gc_
     if (status[g] != 0)
       return fail(ctx, WF_E_NOMEM, "contig group %lld has more than %lld intervals", (long long)g,
                   (long long)kCapMax);
+  return WF_OK;
+}
+
+int wf_junctions(wf_ctx* ctx, const wf_jn_batch* b, const wf_jn_params* p, wf_jn_result* r) {
+  if (!ctx) return WF_E_BADINPUT;
+  if (!b || !p || !r) return fail(ctx, WF_E_BADINPUT, "null batch/params/result");
+  if (b->n_contigs < 0 || b->n_pairs < 0 || b->n_loci < 0) return fail(ctx, WF_E_BADINPUT, "negative sizes");
+  if (b->device_resident) return fail(ctx, WF_E_BADINPUT, "wf_junctions takes host arrays");
+  if (b->n_contigs > 0 && (!b->contig_length || !b->loc_off))
+    return fail(ctx, WF_E_BADINPUT, "null contig arrays");
+  if (b->n_loci > 0 && (!b->loc_start || !b->loc_end)) return fail(ctx, WF_E_BADINPUT, "null locus arrays");
+  if (b->n_pairs > 0 && (!b->pair_contig || !b->m1_start || !b->m1_end || !b->m2_start || !b->m2_end))
+    return fail(ctx, WF_E_BADINPUT, "null pair arrays");
+  if (!r->junction_hits || !r->coverage_gene1 || !r->coverage_gene2 || !r->coverage_junction || !r->ratio)
+    return fail(ctx, WF_E_BADINPUT, "null result arrays");
+  HIP_TRY(ctx, hipSetDevice(ctx->device));
+  const int64_t N = b->n_contigs, NL = b->n_loci, NP = b->n_pairs;
+  if (N == 0) return WF_OK;
+  // host-side layout: site offsets (len + 1 slots per contig), locus -> contig, validation
+  std::vector<int64_t> site_off(N + 1, 0);
+  std::vector<int32_t> loc_contig((size_t)std::max<int64_t>(NL, 1), 0);
+  if (b->loc_off[0] != 0 || b->loc_off[N] != NL) return fail(ctx, WF_E_BADINPUT, "loc_off must span [0, n_loci]");
+  int forward = 1;
+  for (int64_t c = 0; c < N; ++c) {
+    if (b->contig_length[c] < 0) return fail(ctx, WF_E_BADINPUT, "negative contig length");
+    site_off[c + 1] = site_off[c] + b->contig_length[c] + 1;
+    if (b->loc_off[c + 1] < b->loc_off[c]) return fail(ctx, WF_E_BADINPUT, "loc_off decreases");
+    for (int64_t l = b->loc_off[c]; l < b->loc_off[c + 1]; ++l) {
+      loc_contig[l] = (int32_t)c;
+      if (b->loc_start[l] > b->loc_end[l]) forward = 0;
+      if (l > b->loc_off[c] && b->loc_start[l] < b->loc_start[l - 1])
+        return fail(ctx, WF_E_BADINPUT, "loci of contig %lld are not sorted by start", (long long)c);
+    }
+  }
+  const int64_t S = site_off[N];
+  if (S >= ((int64_t)1 << 31) - 1) return fail(ctx, WF_E_BADINPUT, "contigs longer than 2^31 sites in total");
+  for (int64_t i = 0; i < NP; ++i)
+    if (b->pair_contig[i] < 0 || b->pair_contig[i] >= N)
+      return fail(ctx, WF_E_BADINPUT, "pair %lld contig out of range", (long long)i);
+  wf::JnArgs a{};
+  a.n_contigs = (int)N;
+  a.loc_forward = forward;
+  a.n_pairs = NP;
+  a.n_loci = NL;
+  a.n_sites = S;
+  a.min_sites = p->min_overlap_sites;
+  int rc;
+  const int64_t* d_site_off;
+  const int32_t* d_loc_contig;
+  if ((rc = upload(ctx, ctx->jn_site_off, site_off.data(), N + 1, &d_site_off)) ||
+      (rc = upload(ctx, ctx->jn_loc_off, b->loc_off, N + 1, &a.loc_off)) ||
+      (rc = upload(ctx, ctx->jn_loc_contig, loc_contig.data(), NL, &d_loc_contig)) ||
+      (rc = upload(ctx, ctx->jn_lstart, b->loc_start, NL, &a.loc_start)) ||
+      (rc = upload(ctx, ctx->jn_lend, b->loc_end, NL, &a.loc_end)) ||
+      (rc = upload(ctx, ctx->jn_pc, b->pair_contig, NP, &a.pair_contig)) ||
+      (rc = upload(ctx, ctx->jn_m1s, b->m1_start, NP, &a.m1_start)) ||
+      (rc = upload(ctx, ctx->jn_m1e, b->m1_end, NP, &a.m1_end)) ||
+      (rc = upload(ctx, ctx->jn_m2s, b->m2_start, NP, &a.m2_start)) ||
+      (rc = upload(ctx, ctx->jn_m2e, b->m2_end, NP, &a.m2_end)) ||
+      (rc = alloc_out(ctx, ctx->jn_diff, S, &a.diff)) ||
+      (rc = alloc_out(ctx, ctx->jn_cov, S, &a.coverage)) ||
+      (rc = alloc_out(ctx, ctx->jn_prefix, S, &a.prefix)) ||
+      (rc = alloc_out(ctx, ctx->jn_hits, NL, &a.junction_hits)) ||
+      (rc = alloc_out(ctx, ctx->jn_c1, NL, &a.cov1)) || (rc = alloc_out(ctx, ctx->jn_c2, NL, &a.cov2)) ||
+      (rc = alloc_out(ctx, ctx->jn_cj, NL, &a.covj)) || (rc = alloc_out(ctx, ctx->jn_ratio, NL, &a.ratio)))
+    return rc;
+  a.site_off = d_site_off;
+  a.loc_contig = d_loc_contig;
+  if (r->locus_hits && (rc = alloc_out(ctx, ctx->jn_lhits, NL, &a.locus_hits))) return rc;
+  if (r->pair_first || r->pair_mask) {
+    if (!r->pair_first || !r->pair_mask) return fail(ctx, WF_E_BADINPUT, "pair_first and pair_mask go together");
+    if ((rc = alloc_out(ctx, ctx->jn_pfirst, NP, &a.pair_first)) ||
+        (rc = alloc_out(ctx, ctx->jn_pmask, NP, &a.pair_mask)) ||
+        (rc = alloc_out(ctx, ctx->jn_ovf, 1, &a.overflow)))
+      return rc;
+  }
+  const size_t tb = wf::junctions_tmp_bytes(S);
+  if ((rc = ensure(ctx, ctx->jn_tmp, tb))) return rc;
+  std::string err;
+  if (wf::junctions_run(a, ctx->jn_tmp.p, ctx->jn_tmp.bytes, ctx->stream, &err))
+    return fail(ctx, WF_E_HIP, "%s", err.c_str());
+  if ((rc = download(ctx, r->junction_hits, a.junction_hits, NL)) ||
+      (rc = download(ctx, r->coverage_gene1, a.cov1, NL)) ||
+      (rc = download(ctx, r->coverage_gene2, a.cov2, NL)) ||
+      (rc = download(ctx, r->coverage_junction, a.covj, NL)) ||
+      (rc = download(ctx, r->ratio, a.ratio, NL)))
+    return rc;
+  if (r->locus_hits && (rc = download(ctx, r->locus_hits, a.locus_hits, NL))) return rc;
+  unsigned overflow = 0;
+  if (a.pair_first && ((rc = download(ctx, r->pair_first, a.pair_first, NP)) ||
+                       (rc = download(ctx, r->pair_mask, a.pair_mask, NP)) ||
+                       (rc = download(ctx, &overflow, a.overflow, 1))))
+    return rc;
+  if (r->coverage) {   // drop the sentinel slot of each contig
+    for (int64_t c = 0; c < N; ++c) {
+      const int64_t n = b->contig_length[c];
+      if (n > 0 && (rc = download(ctx, r->coverage + (site_off[c] - c), a.coverage + site_off[c], n))) return rc;
+    }
+  }
+  HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+  if (overflow)
+    return fail(ctx, WF_E_NOMEM, "%u read pairs hit loci more than 64 apart (pair_mask holds 64)", overflow);
   return WF_OK;
 }
 

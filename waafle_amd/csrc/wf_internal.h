@@ -108,6 +108,31 @@ struct GcArgs {
 };
 hipError_t launch_genecall(const GcArgs& a, int cus, hipStream_t s);
 
+// waafle_junctions (wf_junctions.hip): read-pair coverage and junction support
+struct JnArgs {
+  int n_contigs;
+  int loc_forward;                         // every locus has start <= end (early exit ok)
+  int64_t n_pairs, n_loci, n_sites;        // n_sites = sum of (contig length + 1)
+  int64_t min_sites;                       // --min-overlap-sites
+  const int64_t* site_off;                 // [n_contigs + 1]
+  const int64_t* loc_off;                  // [n_contigs + 1] loci sorted by start per contig
+  const int32_t* loc_contig;               // [n_loci]
+  const int64_t* loc_start; const int64_t* loc_end;
+  const int32_t* pair_contig;              // [n_pairs]
+  const int64_t* m1_start; const int64_t* m1_end; const int64_t* m2_start; const int64_t* m2_end;
+  int32_t* diff;                           // [n_sites] scratch
+  int64_t* coverage;                       // [n_sites] per-site coverage (sentinels 0)
+  int64_t* prefix;                         // [n_sites] inclusive prefix of coverage
+  int32_t* junction_hits;                  // [n_loci] pairs supporting (j, j+1)
+  int32_t* locus_hits;                     // [n_loci] pairs hitting locus j, or null
+  int64_t* pair_first;                     // [n_pairs] first hit locus (-1: none), or null
+  uint64_t* pair_mask;                     // [n_pairs] hit loci first .. first + 63
+  unsigned* overflow;                      // pairs with a hit 64+ loci after their first
+  double* cov1; double* cov2; double* covj; double* ratio;   // [n_loci] per junction j
+};
+int junctions_run(const JnArgs& a, void* tmp, size_t tmp_bytes, hipStream_t s, std::string* err);
+size_t junctions_tmp_bytes(int64_t n_sites);
+
 // --write-details: per roll-up level, the evaluated (active) contigs and the segment
 // records of the level, copied to the host (wf_staged.hip details_level)
 struct DetailsLevel {

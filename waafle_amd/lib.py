@@ -68,6 +68,23 @@ class WfGcResult(C.Structure):
     _fields_ = [("n_genes", _P), ("gene_start", _P), ("gene_stop", _P), ("gene_strand", _P)]
 
 
+class WfJnBatch(C.Structure):
+    _fields_ = [("n_contigs", C.c_int32), ("device_resident", C.c_int32), ("n_pairs", C.c_int64),
+                ("n_loci", C.c_int64), ("contig_length", _P), ("loc_off", _P), ("loc_start", _P),
+                ("loc_end", _P), ("pair_contig", _P), ("m1_start", _P), ("m1_end", _P),
+                ("m2_start", _P), ("m2_end", _P)]
+
+
+class WfJnParams(C.Structure):
+    _fields_ = [("min_overlap_sites", C.c_int64)]
+
+
+class WfJnResult(C.Structure):
+    _fields_ = [("junction_hits", _P), ("coverage_gene1", _P), ("coverage_gene2", _P),
+                ("coverage_junction", _P), ("ratio", _P), ("locus_hits", _P), ("coverage", _P),
+                ("pair_first", _P), ("pair_mask", _P)]
+
+
 class WfDetails(C.Structure):
     _fields_ = [("n_evals", C.c_int64), ("eval_contig", _P), ("eval_level", _P),
                 ("n_segs", C.c_int64), ("seg_level", _P), ("seg_contig", _P), ("seg_clade", _P),
@@ -93,6 +110,8 @@ SIGNATURES = {
     "wf_timing_read": (C.c_int, [C.c_void_p, C.POINTER(WfTiming)]),
     "wf_genecall": (C.c_int, [C.c_void_p, C.POINTER(WfGcBatch), C.POINTER(WfGcParams),
                               C.POINTER(WfGcResult)]),
+    "wf_junctions": (C.c_int, [C.c_void_p, C.POINTER(WfJnBatch), C.POINTER(WfJnParams),
+                               C.POINTER(WfJnResult)]),
     "wf_details_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "wf_details_read": (C.c_int, [C.c_void_p, C.POINTER(WfDetails)]),
 }

@@ -202,6 +202,11 @@ def _generate_contigs(rng, tax, n, genes, clades, decoys, lgt_frac, stress, shor
 
 
 CHUNK = 10_000     # contigs per independently seeded chunk (generate_chunk)
+CHUNKS = {"cfg5": 500}   # stress contigs carry ~5000 hits each: smaller chunks
+
+
+def chunk_size(name):
+    return CHUNKS.get(name, CHUNK)
 
 
 def chunk_taxonomy(name, seed=None):
@@ -211,7 +216,7 @@ def chunk_taxonomy(name, seed=None):
     return make_taxonomy(spec["clades"], np.random.default_rng(seed))
 
 
-def generate_chunk(name, k, seed=None, tax=None, chunk=CHUNK, n_total=None):
+def generate_chunk(name, k, seed=None, tax=None, chunk=None, n_total=None):
     """Chunk k (contigs k*chunk .. ) of a BASELINE config drawn from its own generator
     default_rng([seed, k]) -- so any contig range is reproducible without generating
     the contigs before it, and chunks can be generated in parallel.  Same per-contig
@@ -219,6 +224,7 @@ def generate_chunk(name, k, seed=None, tax=None, chunk=CHUNK, n_total=None):
     spec = dict(CONFIGS[name])
     seed = int(name[-1]) if seed is None else seed
     n_total = spec["n"] if n_total is None else n_total
+    chunk = chunk_size(name) if chunk is None else chunk
     tax = chunk_taxonomy(name, seed) if tax is None else tax
     first = k * chunk
     n = min(chunk, n_total - first)
@@ -247,7 +253,7 @@ def _pack_chunk(args):
         contig_lengths=d.contig_lengths)
 
 
-def generate_batch(name, lo=0, hi=None, seed=None, workers=None, chunk=CHUNK, n_total=None):
+def generate_batch(name, lo=0, hi=None, seed=None, workers=None, chunk=None, n_total=None):
     """Contigs [lo, hi) of a BASELINE config (whole chunks) packed straight into a device
     batch, chunks generated in parallel worker processes.  Returns (HostBatch,
     TaxonomyTables).  The batch carries no contig names or annotation values (the bench
@@ -256,6 +262,7 @@ def generate_batch(name, lo=0, hi=None, seed=None, workers=None, chunk=CHUNK, n_
     from .taxonomy import TaxonomyTables
     spec = CONFIGS[name]
     n_total = spec["n"] if n_total is None else n_total
+    chunk = chunk_size(name) if chunk is None else chunk
     hi = n_total if hi is None else hi
     seed = int(name[-1]) if seed is None else seed
     st = make_taxonomy(spec["clades"], np.random.default_rng(seed))
