@@ -18,7 +18,8 @@ def case_names():
     return sorted(os.path.basename(p)[:-len(".json.gz")]
                   for p in glob.glob(os.path.join(GOLDEN, "*.json.gz"))
                   if not os.path.basename(p).startswith("details_")
-                  and ".runaway." not in os.path.basename(p))
+                  and ".runaway." not in os.path.basename(p)
+                  and ".junc." not in os.path.basename(p))
 
 
 # fixtures whose explain_two is too large for the scalar oracle (cfg5 stress contigs:
