@@ -64,6 +64,19 @@ def algorithmic_bytes(batch):
     return 24 * batch.n_hits + 12 * batch.n_loci + 16 * (N + 1) + 80 * N
 
 
+def k2_algorithmic(pair_evals, batch):
+    """SURVEY §8(d) counts for the isolated explain_two kernel, from the per-contig
+    reference-equivalent pair counts P_pot(P_pot-1)/2: B_k2 = sum P_pot*G*8 (the S rows
+    of the potential clades) and OPS_pair = sum pairs*G (this rank only)."""
+    sel = pair_evals > 0
+    p = pair_evals[sel].astype(np.float64)
+    ppot = np.rint((1.0 + np.sqrt(1.0 + 8.0 * p)) / 2.0)
+    g = np.diff(batch.loc_off)[sel].astype(np.float64)
+    return {"contigs_explain_two": int(sel.sum()), "p_pot_max": int(ppot.max()) if p.size else 0,
+            "b_k2_bytes": float((ppot * g * 8.0).sum()), "ops_pair": float((p * g).sum()),
+            "pairs": float(p.sum())}
+
+
 def host_cpus():
     """(threads usable by this job, CPU model string)."""
     n = len(os.sched_getaffinity(0))
@@ -257,7 +270,9 @@ def main():
     elapsed = wdist.max_over_ranks(t1 - t0, dist, dev)
 
     calls = out["call"].cpu().numpy()
-    pairs = float(out["pair_evals"].cpu().numpy().sum())
+    pe = out["pair_evals"].cpu().numpy()
+    pairs = float(pe.sum())
+    k2_counts = k2_algorithmic(pe, batch)
     iters = out["iterations"].cpu().numpy()
     if dist:          # whole-job counts
         import torch as T
@@ -281,8 +296,9 @@ def main():
             tj = json.load(fh)
         if tj.get("config") == args.config and tj.get("contigs") == N:
             traffic = tj.get("hbm_bytes_per_launch")
-            tsrc = {k: tj.get(k) for k in ("fetch_size_kb_raw", "fetch_bytes_x2", "write_bytes",
-                                           "hbm_bytes_raw", "valu_insts_per_pass", "source")}
+            tsrc = {k: tj.get(k) for k in ("fetch_bytes_raw", "fetch_bytes_x2", "write_bytes",
+                                           "hbm_bytes_raw", "hbm_bytes_x2",
+                                           "dispatches_per_pass", "source")}
     spec = synth.CONFIGS[args.config]
     result = {
         "metric": "contigs scored/sec + k2 clade-pair evals/sec at 1/2/4/8 MI355X vs CPU ref",
@@ -299,6 +315,7 @@ def main():
         "k2_pair_evals_note": "reference-equivalent count: sum of P_pot(P_pot-1)/2 over "
                               "explain_two calls (orgscorer.py:606-608 score(c1,c2) calls), "
                               "not pairs the mask-class search evaluates",
+        "k2_counts": k2_counts,
         "calls": {"lgt": int(n_lgt), "no_lgt": int(n_no), "unclassified": int(n_un),
                   "rolled_up": int(n_up)},
         "kernel_ms": {"wf_score_pass": pass_ms},

@@ -25,9 +25,11 @@ FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n
           "n_meld2", "annot_hit", "pair_evals", "iterations", "status")
 
 
-@pytest.fixture(scope="module")
-def scorer():
-    s = engine.GpuScorer(0)
+@pytest.fixture(scope="module", params=["level0", "staged"])
+def scorer(request):
+    """Both execution forms: the fused level-0 kernel with the staged kernels behind it
+    (default), and every contig through the staged kernels."""
+    s = engine.GpuScorer(0, mode=request.param)
     yield s
     s.close()
 
@@ -218,6 +220,7 @@ def test_full_size_cfg2_properties(scorer):
     assert_same_results(a, b, batch)
     for kw in (dict(lds_bytes=8192),          # small decision arena: HBM decision slots
                dict(lds_bytes=65536),         # large arena: every contig in LDS
+               dict(mode="staged"), dict(mode="level0"),
                dict()):
         small = engine.GpuScorer(0, **kw)
         small.set_taxonomy(tax)
@@ -280,7 +283,7 @@ def test_many_contigs_device_scan_branch():
     data = synth.generate(n=40000, genes=2, clades=30, seed=71, decoys=1, lgt_frac=0.2)
     batch, tax = synth.to_batch(data)
     params = cli.param_dict(cli.parse_flags([]))
-    s = engine.GpuScorer(0)
+    s = engine.GpuScorer(0, mode="staged")    # every contig reaches the staged level 0
     s.set_taxonomy(tax)
     whole = s.score(batch, params)
     parts = [s.score(batch.slice(x, x + 20000), params) for x in (0, 20000)]

@@ -45,6 +45,7 @@ struct wf_ctx {
   std::vector<std::pair<int, int>> ev_lds;   // indices into ev_pool (one pair per pass)
   int64_t launches = 0;
   bool lds_set = false;            // wf_set_lds_bytes called: also the staged decision arena
+  int mode = WF_MODE_LEVEL0;       // wf_set_mode
   wf::StagedState* staged = nullptr;
   // --write-details
   bool details_on = false;
@@ -244,8 +245,9 @@ int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes) {
 
 int wf_set_mode(wf_ctx* ctx, int mode) {
   if (!ctx) return WF_E_BADINPUT;
-  if (mode != WF_MODE_STAGED)
-    return fail(ctx, WF_E_BADINPUT, "mode must be WF_MODE_STAGED (0): the fused form is retired");
+  if (mode != WF_MODE_STAGED && mode != WF_MODE_LEVEL0)
+    return fail(ctx, WF_E_BADINPUT, "mode must be WF_MODE_LEVEL0 (2) or WF_MODE_STAGED (0)");
+  ctx->mode = mode;
   return WF_OK;
 }
 
@@ -346,6 +348,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   K.unknown = ctx->unknown;
   if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
   if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
+  wf::staged_set_level0(ctx->staged, ctx->mode == WF_MODE_LEVEL0);
   std::pair<int, int> el{-1, -1};
   if (ctx->timing) {
     if (take_event_pair(ctx, ctx->ev_lds) < 0) return fail(ctx, WF_E_HIP, "hipEventCreate failed");

@@ -457,6 +457,220 @@ __device__ __forceinline__ int below(int base, int bound, int m) {
   return d <= 0 ? 0 : min(m, (d + 7) >> 3);
 }
 
+// --------------------------------------------------------------------------
+// segment means shared by the staged kernels and the fused level-0 kernel (wf_fast.hip)
+// --------------------------------------------------------------------------
+constexpr int kThreadLeaves = 32;
+constexpr int kPruneMax = 64;      // attachments scanned for whole-locus domination
+
+__device__ __forceinline__ bool attaches(const DevParams& P, int qlo, int qhi, int hs, int l1,
+                                         int len, int lst) {
+  if (P.stranded && hs != lst) return false;
+  const int l2 = l1 + len - 1;
+  if (l1 > qhi || qlo > l2) return 0.0 >= P.min_overlap;   // calc_overlap -> int 0
+  const int ov = min(qhi, l2) - max(qlo, l1) + 1;
+  const int den = min(qhi - qlo + 1, l2 - l1 + 1);
+  return (double)ov / (double)den >= P.min_overlap;
+}
+
+// numpy's leaf [st, st+ln) over sites holding v on [lo, hi) and 0 elsewhere: accumulator c
+// adds v k_c times from 0.0 (k_c in {kmin, kmin+1, kmin+2}: seqsum closed form, see
+// SegAttT::closed_body), tree of the 8, then the tail sites in order.
+__device__ __forceinline__ double run_leaf(int lo, int hi, double v, int st, int ln) {
+  const int m = ln >> 3, be = st + (m << 3);
+  hi = max(hi, lo);                                  // empty slice (--min-overlap 0 wrap)
+  double res = 0.0;
+  if (m > 0) {
+    int k[8], kmin = m;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      k[c] = below(st + c, hi, m) - below(st + c, lo, m);
+      kmin = min(kmin, k[c]);
+    }
+    double s0 = 0.0;
+    for (int i = 0; i < kmin; ++i) s0 += v;
+    const double s1 = s0 + v, s2 = s1 + v;
+    double r[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r[c] = k[c] == kmin ? s0 : (k[c] == kmin + 1 ? s1 : s2);
+    res = leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+  }
+  for (int x = be; x < st + ln; ++x) res += (x >= lo && x < hi) ? v : 0.0;
+  return res;
+}
+
+// numpy add.reduce of n <= 128 values produced in order by next() (pairwise_sum's leaf:
+// n < 8 sequential, else eight strided accumulators combined as a tree, then the tail)
+template <class F>
+__device__ __forceinline__ double np_sum_seq(int n, F next) {
+  if (n < 8) {
+    double r = 0.0;
+    for (int i = 0; i < n; ++i) r += next();
+    return r;
+  }
+  double r0 = next(), r1 = next(), r2 = next(), r3 = next();
+  double r4 = next(), r5 = next(), r6 = next(), r7 = next();
+  int i = 8;
+  const int m = n - (n & 7);
+  for (; i < m; i += 8) {
+    r0 += next(); r1 += next(); r2 += next(); r3 += next();
+    r4 += next(); r5 += next(); r6 += next(); r7 += next();
+  }
+  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+  for (; i < n; ++i) res += next();
+  return res;
+}
+
+// Mean of a segment whose site array is ONE run of value v on [lo, hi) over a zero
+// background (len < kNpyBuf: one numpy buffer; lt/nl: its leaf table).  Three uniform
+// phases instead of one leaf formula per loop trip (the lanes of a wave would otherwise run
+// every leaf kind on every trip):
+//  A. classify the leaves against the run: at most two straddle a run boundary, the ones
+//     inside have at most 4 distinct lengths (numpy's split of one buffer);
+//  B. the <= 2 boundary leaves by run_leaf, each inside length once (8 equal accumulators:
+//     8 * seqsum, exact doubling, then the tail in order);
+//  C. the tree, picking each leaf's value (outside leaves are 0).
+__device__ __forceinline__ double one_run_mean(const int4* lt, int nl, int len, int lo, int hi, double v) {
+  hi = max(hi, lo);
+  int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
+  int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
+#pragma unroll 4
+  for (int q = 0; q < nl; ++q) {
+    const int4 e = lt[q];
+    const int le = e.x + e.y;
+    const bool in = lo <= e.x && le <= hi && lo < hi;
+    const bool out = le <= lo || e.x >= hi || lo >= hi;
+    if (!in && !out) {
+      if (pst0 < 0) { pst0 = e.x; pln0 = e.y; } else { pst1 = e.x; pln1 = e.y; }
+    } else if (in && e.y != L0 && e.y != L1 && e.y != L2 && e.y != L3) {
+      if (L0 < 0) L0 = e.y; else if (L1 < 0) L1 = e.y; else if (L2 < 0) L2 = e.y; else L3 = e.y;
+    }
+  }
+  const double vp0 = pst0 >= 0 ? run_leaf(lo, hi, v, pst0, pln0) : 0.0;
+  const double vp1 = pst1 >= 0 ? run_leaf(lo, hi, v, pst1, pln1) : 0.0;
+  auto inside = [&](int ln) -> double {
+    if (ln < 0) return 0.0;
+    double b = 0.0;
+    for (int i = 0; i < (ln >> 3); ++i) b += v;
+    double res = 8.0 * b;
+    for (int x = ln & ~7; x < ln; ++x) res += v;
+    return res;
+  };
+  const double V0 = inside(L0), V1 = inside(L1), V2 = inside(L2), V3 = inside(L3);
+  SumStack stk;
+#pragma unroll 4
+  for (int q = 0; q < nl; ++q) {
+    const int4 e = lt[q];
+    const int le = e.x + e.y;
+    const bool in = lo <= e.x && le <= hi && lo < hi;
+    const bool out = le <= lo || e.x >= hi || lo >= hi;
+    double x = 0.0;
+    if (in) x = e.y == L0 ? V0 : e.y == L1 ? V1 : e.y == L2 ? V2 : V3;
+    else if (!out) x = e.x == pst0 ? vp0 : vp1;
+    stk.push(x);
+    for (int a = 0; a < e.z; ++a) stk.add_top();
+  }
+  return (0.0 + stk.s0) / (double)len;
+}
+
+// Orders this wave's LDS accesses (one wave of a multi-wave workgroup working alone).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Segments with up to 64 attachments, one wave each: the max-envelope is swept once into
+// runs (lane i holds attachment i; run value = wave max over the covering ones, run end =
+// wave min over the next boundaries), then lane q evaluates leaf q (nl <= 64) from the runs
+// -- each of the eight stride accumulators adds its sites in site order, a run of value v
+// contributing v k_c times (zero runs add nothing: x + 0.0 = x for x >= 0) -- and lane 0
+// folds the leaves in tree order.  Same sums as k_leaf's per-leaf stride walks.  A lane
+// without an attachment passes lo = hi = 0.  Returns the mean on every lane.
+// R bounds the positive runs: 2 * attachments - 1.
+constexpr int kWaveRuns = 2 * 64 + 2;
+template <int R>
+struct WaveRunsT {
+  int r_lo[R], r_hi[R];
+  double r_v[R];
+  double lv[64];
+  int z[64];
+};
+using WaveRuns = WaveRunsT<kWaveRuns>;
+
+template <int R>
+__device__ __forceinline__ double wave_seg_mean(const int4* lt, int nl, int len, int lo, int hi, double sc,
+                                                WaveRunsT<R>& W) {
+  const int lane = lane_id();
+  int nr = 0;
+  for (int x = 0; x < len;) {                       // wave-uniform sweep
+    double v = (lo <= x && x < hi) ? sc : 0.0;
+    int nb = len;
+    if (lo < hi) {
+      if (lo > x) nb = lo;
+      else if (hi > x) nb = hi;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double v2 = __shfl_xor(v, off, 64);
+      const int n2 = __shfl_xor(nb, off, 64);
+      v = v2 > v ? v2 : v;
+      nb = n2 < nb ? n2 : nb;
+    }
+    if (v > 0.0) {
+      if (lane == 0) { W.r_lo[nr] = x; W.r_hi[nr] = nb; W.r_v[nr] = v; }
+      ++nr;
+    }
+    x = nb;
+  }
+  wave_sync();
+  if (lane < nl) {
+    const int4 e = lt[lane];
+    const int st = e.x, ln = e.y, m = ln >> 3, be = st + (m << 3);
+    int j = 0;
+    while (j < nr && W.r_hi[j] <= st) ++j;
+    double r[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r[c] = 0.0;
+    for (int jj = j; jj < nr && W.r_lo[jj] < be; ++jj) {
+      const int a = max(W.r_lo[jj], st), b = min(W.r_hi[jj], be);
+      const double v = W.r_v[jj];
+      int k[8], kmin = m;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        k[c] = below(st + c, b, m) - below(st + c, a, m);
+        kmin = min(kmin, k[c]);
+      }
+      for (int q = 0; q < kmin; ++q) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) r[c] += v;
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (k[c] > kmin) r[c] += v;
+    }
+    double res = m > 0 ? leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]) : 0.0;
+    for (int x = be; x < st + ln; ++x) {            // tail sites, in order
+      while (j < nr && W.r_hi[j] <= x) ++j;
+      res += (j < nr && W.r_lo[j] <= x) ? W.r_v[j] : 0.0;
+    }
+    W.lv[lane] = res;
+    W.z[lane] = e.z;
+  }
+  wave_sync();
+  double mean = 0.0;
+  if (lane == 0) {
+    SumStack stk;
+    for (int q = 0; q < nl; ++q) {
+      stk.push(W.lv[q]);
+      for (int a = 0; a < W.z[q]; ++a) stk.add_top();
+    }
+    mean = (0.0 + stk.s0) / (double)len;
+  }
+  wave_sync();                                      // W is reused by the next segment
+  return __shfl(mean, 0, 64);
+}
+
 constexpr int kRegAtt = 4;   // attachments of a segment held in registers
 
 // The attachments of one (clade, locus) segment -- sorted keys [kb, ke) -- and the exact

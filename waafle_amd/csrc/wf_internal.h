@@ -16,6 +16,7 @@ constexpr int kNpyBuf = 8192;           // numpy reduction buffer (NPY_BUFSIZE)
 constexpr int kLeafSlots = 160;         // >= leaves of one 8192-element buffer
 constexpr int kMaxIter = 100;           // orgscorer.py:580
 constexpr int kLin = 16;                // lineage row: ancestors at depths 0..15 (64 B)
+constexpr int kAnnSlots = 256;          // (locus, system) annotation slots in LDS
 
 // Parameters with the derived thresholds precomputed on the host
 // (orgscorer.py:338-346, :515-516, :720-721).
@@ -150,9 +151,15 @@ struct DetailsSink {
 };
 
 struct StagedState;
+// Fused level 0 (wf_fast.hip): per contig, 0 = finished here, 1 = handed to the staged
+// path with its attachment and leaf counts in ccnt / cleaves.
+hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, unsigned grid,
+                       hipStream_t s);
+int fast_blocks_per_cu();
 StagedState* staged_create(int device);
 void staged_destroy(StagedState* st);
 void staged_set_lds(StagedState* st, int64_t bytes);
+void staged_set_level0(StagedState* st, bool on);   // fused level 0 (wf_fast.hip) first
 // Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2 with
 // the message in *err (-1 bad input, -2 HIP failure).
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t n_hits,

@@ -71,15 +71,6 @@ __device__ __forceinline__ int seg_count(const SArgs& S, int64_t n_keys) {
   return n_keys > 0 ? S.seg_id[n_keys - 1] : 0;
 }
 
-__device__ __forceinline__ bool attaches(const DevParams& P, int qlo, int qhi, int hs, int l1,
-                                         int len, int lst) {
-  if (P.stranded && hs != lst) return false;
-  const int l2 = l1 + len - 1;
-  if (l1 > qhi || qlo > l2) return 0.0 >= P.min_overlap;   // calc_overlap -> int 0
-  const int ov = min(qhi, l2) - max(qlo, l1) + 1;
-  const int den = min(qhi - qlo + 1, l2 - l1 + 1);
-  return (double)ov / (double)den >= P.min_overlap;
-}
 
 // ---- numpy leaf tables by buffer length ------------------------------------------------
 __global__ void k_lut_count(int32_t* cnt) {
@@ -111,7 +102,6 @@ __global__ void k_init(const KArgs K) {
 // annotation transfer (orgscorer.py:383-392) for the contig's loci in LDS.
 constexpr int kAttNT = 64;       // one wave per contig: many contigs in flight
 constexpr int kAttLoc = 128;      // loci staged in LDS (more: read from HBM)
-constexpr int kAnnSlots = 256;    // (locus, system) annotation slots in LDS
 
 struct LocView {
   int lo, len, st;
@@ -119,7 +109,8 @@ struct LocView {
 
 template <int PASS>
 __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* ccnt,
-                                                       int64_t* cleaves, unsigned long long* cmax) {
+                                                       int64_t* cleaves, unsigned long long* cmax,
+                                                       const int32_t* list, int n_list) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   __shared__ int s_lo[kAttLoc], s_len[kAttLoc], s_nl[kAttLoc];
@@ -129,7 +120,8 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* c
   __shared__ int s_scan[kAttNT / 64];
   __shared__ long long s_red[2][kAttNT / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
+  for (int i = blockIdx.x; i < n_list; i += gridDim.x) {
+    const int c = list ? list[i] : i;               // list: the contigs k_fast handed over
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     const int64_t l0 = K.loc_off[c];
     const int G = (int)(K.loc_off[c + 1] - l0);
@@ -287,7 +279,7 @@ __global__ void k_keys_active(const SArgs S, int n_act, uint64_t* keys, int32_t*
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const int c = S.act ? S.act[cr] : cr;
     const int64_t a0 = S.catt_off[c], a1 = S.catt_off[c + 1];
-    const int64_t base = S.act ? S.act_base[cr] : a0;
+    const int64_t base = S.act_base ? S.act_base[cr] : a0;   // level 0: own offsets
     for (int64_t i = threadIdx.x; i < a1 - a0; i += blockDim.x) {
       keys[base + i] = make_key(S, cr, (int)(a0 + i));
       vals[base + i] = (int)(a0 + i);
@@ -501,34 +493,7 @@ __device__ __forceinline__ int lut_count(const SArgs& S, int m) { return S.lut_o
 // one code path; the leaves go in tree order onto a register stack, exactly as k_leaf +
 // k_seg_combine do, without the leaf list, the leaf values or the leaf -> segment map ever
 // touching HBM.  Their leaf count is reported as 0, so the leaf kernels skip them.
-constexpr int kThreadLeaves = 32;
-constexpr int kPruneMax = 64;      // attachments scanned for whole-locus domination
 
-// numpy's leaf [st, st+ln) over sites holding v on [lo, hi) and 0 elsewhere: accumulator c
-// adds v k_c times from 0.0 (k_c in {kmin, kmin+1, kmin+2}: seqsum closed form, see
-// SegAttT::closed_body), tree of the 8, then the tail sites in order.
-__device__ __forceinline__ double run_leaf(int lo, int hi, double v, int st, int ln) {
-  const int m = ln >> 3, be = st + (m << 3);
-  hi = max(hi, lo);                                  // empty slice (--min-overlap 0 wrap)
-  double res = 0.0;
-  if (m > 0) {
-    int k[8], kmin = m;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      k[c] = below(st + c, hi, m) - below(st + c, lo, m);
-      kmin = min(kmin, k[c]);
-    }
-    double s0 = 0.0;
-    for (int i = 0; i < kmin; ++i) s0 += v;
-    const double s1 = s0 + v, s2 = s1 + v;
-    double r[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) r[c] = k[c] == kmin ? s0 : (k[c] == kmin + 1 ? s1 : s2);
-    res = leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
-  }
-  for (int x = be; x < st + ln; ++x) res += (x >= lo && x < hi) ? v : 0.0;
-  return res;
-}
 
 
 // --write-details gene spans (make_gene_spans_field, orgscorer.py:770-789), thread per
@@ -635,54 +600,7 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
       }
     }
     if (one_run) {
-      // Three uniform phases instead of one leaf formula per loop trip (the lanes of a wave
-      // would otherwise run every leaf kind on every trip):
-      //  A. classify the leaves against the run: at most two straddle a run boundary, the
-      //     ones inside have at most 4 distinct lengths (numpy's split of one buffer);
-      //  B. the <= 2 boundary leaves by run_leaf, each inside length once (8 equal
-      //     accumulators: 8 * seqsum, exact doubling, then the tail in order);
-      //  C. the tree, picking each leaf's value (outside leaves are 0).
-      const int4* lt = S.lut + S.lut_off[si.len];
-      hi = max(hi, lo);
-      int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
-      int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
-#pragma unroll 4
-      for (int q = 0; q < nl; ++q) {
-        const int4 e = lt[q];
-        const int le = e.x + e.y;
-        const bool in = lo <= e.x && le <= hi && lo < hi;
-        const bool out = le <= lo || e.x >= hi || lo >= hi;
-        if (!in && !out) {
-          if (pst0 < 0) { pst0 = e.x; pln0 = e.y; } else { pst1 = e.x; pln1 = e.y; }
-        } else if (in && e.y != L0 && e.y != L1 && e.y != L2 && e.y != L3) {
-          if (L0 < 0) L0 = e.y; else if (L1 < 0) L1 = e.y; else if (L2 < 0) L2 = e.y; else L3 = e.y;
-        }
-      }
-      const double vp0 = pst0 >= 0 ? run_leaf(lo, hi, v, pst0, pln0) : 0.0;
-      const double vp1 = pst1 >= 0 ? run_leaf(lo, hi, v, pst1, pln1) : 0.0;
-      auto inside = [&](int ln) -> double {
-        if (ln < 0) return 0.0;
-        double b = 0.0;
-        for (int i = 0; i < (ln >> 3); ++i) b += v;
-        double res = 8.0 * b;
-        for (int x = ln & ~7; x < ln; ++x) res += v;
-        return res;
-      };
-      const double V0 = inside(L0), V1 = inside(L1), V2 = inside(L2), V3 = inside(L3);
-      SumStack stk;
-#pragma unroll 4
-      for (int q = 0; q < nl; ++q) {
-        const int4 e = lt[q];
-        const int le = e.x + e.y;
-        const bool in = lo <= e.x && le <= hi && lo < hi;
-        const bool out = le <= lo || e.x >= hi || lo >= hi;
-        double x = 0.0;
-        if (in) x = e.y == L0 ? V0 : e.y == L1 ? V1 : e.y == L2 ? V2 : V3;
-        else if (!out) x = e.x == pst0 ? vp0 : vp1;
-        stk.push(x);
-        for (int a = 0; a < e.z; ++a) stk.add_top();
-      }
-      S.seg_mean[s] = (0.0 + stk.s0) / (double)si.len;
+      S.seg_mean[s] = one_run_mean(S.lut + S.lut_off[si.len], nl, si.len, lo, hi, v);
       nl = 0;
     } else {
       S.seg_rec[s] = make_int4(si.kb, na, si.len, nl);
@@ -709,92 +627,21 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
 // k_c times (zero runs add nothing: x + 0.0 = x for x >= 0) -- and lane 0 folds the leaves
 // in tree order.  Same sums as k_leaf's per-leaf stride walks, without rescanning the
 // attachments for every run of every leaf.
-constexpr int kWaveRuns = 2 * 64 + 2;
-
 __global__ __launch_bounds__(64) void k_seg_wave(const SArgs S) {
-  __shared__ int r_lo[kWaveRuns], r_hi[kWaveRuns];
-  __shared__ double r_v[kWaveRuns];
-  __shared__ double s_lv[64];
-  __shared__ int s_z[64];
+  __shared__ WaveRuns W;
   const int lane = threadIdx.x;
   const int count = (int)S.counters[7];
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const int s = S.wave_list[i];
     const int4 rec = S.seg_rec[s];                  // (kb, attachments, length, leaves)
-    const int len = rec.z, nl = rec.w;
     int lo = 0, hi = 0;
     double sc = 0.0;
     if (lane < rec.y) {
       const int2 x = S.satt_lohi[rec.x + lane];
       if (x.x < x.y) { lo = x.x; hi = x.y; sc = S.satt_sc[rec.x + lane]; }
     }
-    int nr = 0;
-    for (int x = 0; x < len;) {                     // wave-uniform sweep
-      double v = (lo <= x && x < hi) ? sc : 0.0;
-      int nb = len;
-      if (lo < hi) {
-        if (lo > x) nb = lo;
-        else if (hi > x) nb = hi;
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const double v2 = __shfl_xor(v, off, 64);
-        const int n2 = __shfl_xor(nb, off, 64);
-        v = v2 > v ? v2 : v;
-        nb = n2 < nb ? n2 : nb;
-      }
-      if (v > 0.0) {
-        if (lane == 0) { r_lo[nr] = x; r_hi[nr] = nb; r_v[nr] = v; }
-        ++nr;
-      }
-      x = nb;
-    }
-    __syncthreads();
-    const int4* lt = S.lut + S.lut_off[len];
-    int4 e = make_int4(0, 0, 0, 0);
-    if (lane < nl) {
-      e = lt[lane];
-      const int st = e.x, ln = e.y, m = ln >> 3, be = st + (m << 3);
-      int j = 0;
-      while (j < nr && r_hi[j] <= st) ++j;
-      double r[8];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) r[c] = 0.0;
-      for (int jj = j; jj < nr && r_lo[jj] < be; ++jj) {
-        const int a = max(r_lo[jj], st), b = min(r_hi[jj], be);
-        const double v = r_v[jj];
-        int k[8], kmin = m;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          k[c] = below(st + c, b, m) - below(st + c, a, m);
-          kmin = min(kmin, k[c]);
-        }
-        for (int q = 0; q < kmin; ++q) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) r[c] += v;
-        }
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-          if (k[c] > kmin) r[c] += v;
-      }
-      double res = m > 0 ? leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]) : 0.0;
-      for (int x = be; x < st + ln; ++x) {          // tail sites, in order
-        while (j < nr && r_hi[j] <= x) ++j;
-        res += (j < nr && r_lo[j] <= x) ? r_v[j] : 0.0;
-      }
-      s_lv[lane] = res;
-      s_z[lane] = e.z;
-    }
-    __syncthreads();
-    if (lane == 0) {
-      SumStack stk;
-      for (int q = 0; q < nl; ++q) {
-        stk.push(s_lv[q]);
-        for (int a = 0; a < s_z[q]; ++a) stk.add_top();
-      }
-      S.seg_mean[s] = (0.0 + stk.s0) / (double)len;
-    }
-    __syncthreads();
+    const double m = wave_seg_mean(S.lut + S.lut_off[rec.z], rec.w, rec.z, lo, hi, sc, W);
+    if (lane == 0) S.seg_mean[s] = m;
   }
 }
 
@@ -955,27 +802,6 @@ __global__ void k_flat_prep(const SArgs S, int n_act, int level) {
   S.c_gu[cr] = Gu;
 }
 
-// numpy add.reduce of n <= 128 values produced in order by next() (pairwise_sum's leaf:
-// n < 8 sequential, else eight strided accumulators combined as a tree, then the tail)
-template <class F>
-__device__ __forceinline__ double np_sum_seq(int n, F next) {
-  if (n < 8) {
-    double r = 0.0;
-    for (int i = 0; i < n; ++i) r += next();
-    return r;
-  }
-  double r0 = next(), r1 = next(), r2 = next(), r3 = next();
-  double r4 = next(), r5 = next(), r6 = next(), r7 = next();
-  int i = 8;
-  const int m = n - (n & 7);
-  for (; i < m; i += 8) {
-    r0 += next(); r1 += next(); r2 += next(); r3 += next();
-    r4 += next(); r5 += next(); r6 += next(); r7 += next();
-  }
-  double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-  for (; i < n; ++i) res += next();
-  return res;
-}
 
 __device__ __forceinline__ bool run_start(const SArgs& S, int s) {
   return s == 0 || S.seg_crank[s] != S.seg_crank[s - 1] || S.seg_cg[s].x != S.seg_cg[s - 1].x;
@@ -1513,7 +1339,8 @@ struct StagedState {
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
   int big_slots = 512;
   Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
-  Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp;
+  Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp, pend;
+  bool level0 = true;               // fused level 0 (k_fast) before the staged kernels
   bool lut_ready = false;
   int64_t dec_lds = 24 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
@@ -1554,6 +1381,8 @@ StagedState* staged_create(int device) {
 }
 
 void staged_destroy(StagedState* st) { delete st; }
+
+void staged_set_level0(StagedState* st, bool on) { st->level0 = on; }
 
 void staged_set_lds(StagedState* st, int64_t bytes) {
   st->dec_lds = bytes;
@@ -1737,17 +1566,30 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   ST_TRY(st->cnt.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
   ST_TRY(st->cnt_leaves.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
   ST_TRY(st->att_off.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
-  ST_TRY(st->red.ensure(s, 2 * sizeof(int64_t)));
+  ST_TRY(st->red.ensure(s, 4 * sizeof(int64_t)));
   sa.catt_off = st->att_off.as<int64_t>();
   static const char* ag_env = getenv("WF_ATT_GRID");        // blocks per CU (measurement aid)
   const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * (ag_env ? atoi(ag_env) : 32));
-  ST_TRY(hipMemsetAsync(st->red.p, 0, 2 * sizeof(int64_t), s));
+  ST_TRY(hipMemsetAsync(st->red.p, 0, 4 * sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt.as<int64_t>() + N, 0, sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt_leaves.as<int64_t>() + N, 0, sizeof(int64_t), s));
+  // Fused level 0 (wf_fast.hip) unless --write-details (per-level records of every contig),
+  // --weak-loci assign-unknown (virtual "Unknown" row) or HBM annotation slots are needed.
+  static const char* l0_env = getenv("WF_LEVEL0");          // 0: staged only (measurement aid)
+  const bool level0 = st->level0 && !det && k.p.weak != 2 && (int64_t)max_loci * k.n_sys <= kAnnSlots &&
+                      !(l0_env && l0_env[0] == '0');
   hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, sa.k);
-  hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
-                     st->cnt_leaves.as<int64_t>(),
-                     reinterpret_cast<unsigned long long*>(st->red.as<int64_t>() + 1));
+  if (level0) {
+    ST_TRY(st->pend.ensure(s, (size_t)N * 4));
+    ST_TRY(st->act0.ensure(s, (size_t)N * 4));
+    const unsigned fgrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * fast_blocks_per_cu());
+    ST_TRY(launch_fast(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), fgrid,
+                       s));
+  } else {
+    hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
+                       st->cnt_leaves.as<int64_t>(),
+                       reinterpret_cast<unsigned long long*>(st->red.as<int64_t>() + 1), nullptr, N);
+  }
   ST_TRY(hipGetLastError());
   {
     size_t t1 = 0, t2 = 0;
@@ -1755,10 +1597,14 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
                                             st->att_off.as<int64_t>(), (int)(N + 1), s));
     ST_TRY(hipcub::DeviceReduce::Sum(nullptr, t2, st->cnt_leaves.as<int64_t>(),
                                      st->red.as<int64_t>(), (int)(N + 1), s));
-    size_t t3 = 0;
+    size_t t3 = 0, t4 = 0;
     ST_TRY(hipcub::DeviceReduce::Max(nullptr, t3, st->cnt.as<int64_t>(), st->red.as<int64_t>() + 1,
                                      (int)(N + 1), s));
-    ST_TRY(st->tmp.ensure(s, std::max(t1, std::max(t2, t3))));
+    if (level0)
+      ST_TRY(hipcub::DeviceSelect::Flagged(nullptr, t4, hipcub::CountingInputIterator<int32_t>(0),
+                                           st->pend.as<int32_t>(), st->act0.as<int32_t>(),
+                                           st->red.as<int64_t>() + 2, N, s));
+    ST_TRY(st->tmp.ensure(s, std::max(std::max(t1, t4), std::max(t2, t3))));
     size_t tb = st->tmp.n;
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, tb, st->cnt.as<int64_t>(),
                                             st->att_off.as<int64_t>(), (int)(N + 1), s));
@@ -1769,18 +1615,26 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     tb = st->tmp.n;
     ST_TRY(hipcub::DeviceReduce::Max(st->tmp.p, tb, st->cnt.as<int64_t>(), st->red.as<int64_t>() + 1,
                                      (int)(N + 1), s));
+    if (level0) {                     // the contigs k_fast handed over, in contig order
+      tb = st->tmp.n;
+      ST_TRY(hipcub::DeviceSelect::Flagged(st->tmp.p, tb, hipcub::CountingInputIterator<int32_t>(0),
+                                           st->pend.as<int32_t>(), st->act0.as<int32_t>(),
+                                           st->red.as<int64_t>() + 2, N, s));
+    }
   }
   static const char* mb_env = getenv("WF_MAILBOX");         // 0: copy + event (measurement aid)
   const bool mailbox = st->mbox && !(mb_env && mb_env[0] == '0');
   if (mailbox) {
-    ST_TRY(publish_sync(st, s, st->att_off.as<int64_t>() + N, 1, st->red.p, 2,
+    ST_TRY(publish_sync(st, s, st->att_off.as<int64_t>() + N, 1, st->red.p, 3,
                         reinterpret_cast<unsigned long long*>(&hc[2])));
   } else {
     ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     ST_TRY(spin_sync(s, st->lvl_ev[0]));
   }
   const int64_t A = hc[2], TLB = hc[3], max_att = hc[4];
+  const int n_first = level0 ? (int)hc[5] : N;     // contigs of the staged level 0
+  if (n_first == 0) return 0;                       // k_fast finished every contig
   // per-contig LDS sort when every contig's attachments fit one workgroup's LDS
   // (WF_LDS_SORT=0: device radix sort of the whole level; measurement aid)
   static const char* ls_env = getenv("WF_LDS_SORT");
@@ -1865,7 +1719,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     ST_TRY(hipMemsetAsync(st->annot_best.p, 0, (size_t)n_annot * 8, s));
     ST_TRY(hipMemsetAsync(k.annot, 0xFF, (size_t)n_annot * 4, s));     // -1: no winner
   }
-  hipLaunchKernelGGL(k_att_contig<1>, dim3(agrid), dim3(kAttNT), 0, s, sa, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL(k_att_contig<1>, dim3(std::min<unsigned>(agrid, (unsigned)n_first)), dim3(kAttNT), 0, s, sa,
+                     nullptr, nullptr, nullptr, level0 ? st->act0.as<int32_t>() : nullptr, n_first);
   ST_TRY(hipGetLastError());
 
   // flat explain_one applies to --weak-loci ignore/penalize and <= 64 loci per contig
@@ -1905,7 +1760,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   // (WF_PIPELINE=1) until a level has fewer launches.
   static const char* pipe_env = getenv("WF_PIPELINE");
   const bool pipelined = sa.sort_cap > 0 && !flat_one && !det && pipe_env && pipe_env[0] == '1';
-  int n_act = N;
+  int n_act = n_first;
   int64_t n_keys = A;
   if (det) {
     det->levels.clear();
@@ -1917,7 +1772,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
     sa.counters = lvl_ctr + 8 * level;
     sa.in_counts = async ? lvl_ctr + 8 * (level - 1) : nullptr;
     const int cur = level & 1;
-    sa.act = level == 0 ? nullptr : act[cur]->as<int32_t>();
+    sa.act = level == 0 ? (level0 ? st->act0.as<int32_t>() : nullptr) : act[cur]->as<int32_t>();
     sa.act_base = level == 0 ? nullptr : base[cur]->as<int64_t>();
     sa.act_next = act[cur ^ 1]->as<int32_t>();
     sa.act_base_next = base[cur ^ 1]->as<int64_t>();
