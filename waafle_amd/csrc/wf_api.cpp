@@ -356,7 +356,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
     HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.first], ctx->stream));
   }
   std::string err;
-  const int rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->n_hits, b->n_loci, ctx->stream,
+  const int rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->max_hits, b->n_hits, b->n_loci, ctx->stream,
                                   &err, ctx->details_on ? &ctx->det : nullptr);
   if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : WF_E_HIP, "%s", err.c_str());
   if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));

@@ -530,13 +530,29 @@ __device__ __forceinline__ double np_sum_seq(int n, F next) {
 //  B. the <= 2 boundary leaves by run_leaf, each inside length once (8 equal accumulators:
 //     8 * seqsum, exact doubling, then the tail in order);
 //  C. the tree, picking each leaf's value (outside leaves are 0).
-__device__ __forceinline__ double one_run_mean(const int4* lt, int nl, int len, int lo, int hi, double v) {
+// Leaf tables are read through a getter: q -> (start, length, parent adds) of leaf q.
+struct PtrLut {                       // the device table (int4 per leaf)
+  const int4* p;
+  __device__ __forceinline__ int4 operator()(int q) const { return p[q]; }
+};
+// Packed leaf entry (LDS copies): start | length << 13 | parent adds << 21.
+__device__ __forceinline__ uint32_t pack_leaf(int4 e) { return (uint32_t)e.x | ((uint32_t)e.y << 13) | ((uint32_t)e.z << 21); }
+struct PackedLut {
+  const uint32_t* p;
+  __device__ __forceinline__ int4 operator()(int q) const {
+    const uint32_t u = p[q];
+    return make_int4((int)(u & 8191u), (int)((u >> 13) & 255u), (int)(u >> 21), 0);
+  }
+};
+
+template <class LT>
+__device__ __forceinline__ double one_run_mean(LT lt, int nl, int len, int lo, int hi, double v) {
   hi = max(hi, lo);
   int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
   int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
 #pragma unroll 4
   for (int q = 0; q < nl; ++q) {
-    const int4 e = lt[q];
+    const int4 e = lt(q);
     const int le = e.x + e.y;
     const bool in = lo <= e.x && le <= hi && lo < hi;
     const bool out = le <= lo || e.x >= hi || lo >= hi;
@@ -560,7 +576,7 @@ __device__ __forceinline__ double one_run_mean(const int4* lt, int nl, int len, 
   SumStack stk;
 #pragma unroll 4
   for (int q = 0; q < nl; ++q) {
-    const int4 e = lt[q];
+    const int4 e = lt(q);
     const int le = e.x + e.y;
     const bool in = lo <= e.x && le <= hi && lo < hi;
     const bool out = le <= lo || e.x >= hi || lo >= hi;
@@ -598,8 +614,8 @@ struct WaveRunsT {
 };
 using WaveRuns = WaveRunsT<kWaveRuns>;
 
-template <int R>
-__device__ __forceinline__ double wave_seg_mean(const int4* lt, int nl, int len, int lo, int hi, double sc,
+template <int R, class LT>
+__device__ __forceinline__ double wave_seg_mean(LT lt, int nl, int len, int lo, int hi, double sc,
                                                 WaveRunsT<R>& W) {
   const int lane = lane_id();
   int nr = 0;
@@ -625,7 +641,7 @@ __device__ __forceinline__ double wave_seg_mean(const int4* lt, int nl, int len,
   }
   wave_sync();
   if (lane < nl) {
-    const int4 e = lt[lane];
+    const int4 e = lt(lane);
     const int st = e.x, ln = e.y, m = ln >> 3, be = st + (m << 3);
     int j = 0;
     while (j < nr && W.r_hi[j] <= st) ++j;

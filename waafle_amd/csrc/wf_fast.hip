@@ -1,154 +1,479 @@
-// Fused level 0 of the contig-scoring path (gfx950 / MI355X).
+// Per-contig wave kernels of the contig-scoring path (gfx950 / MI355X).
 //
-// One 256-thread workgroup carries one contig from its hits to its explain_one decision
-// with every intermediate in LDS: attachments (orgscorer.py:359-392), the (clade, locus)
-// sort and segments (:394-406), the exact numpy segment means (:399-406), per-locus maxes
-// and the weak-locus mask (:407-429), Contig.score of every clade (:447-461), explain_one
-// and meld_one (:585-597, :621-631).  A contig it cannot finish -- no one-clade option
-// (explain_two), more attachments than the LDS holds, more than 64 loci, a segment no
-// LDS-resident mean covers -- is handed to the staged path (wf_staged.hip) through a
-// per-contig flag with its attachment and leaf counts; the staged level 0 then runs on
+// One wave64 carries one contig through the whole path, alone: each workgroup is a single
+// wave with its own LDS slice, so no wave ever waits on another (no workgroup barrier) and
+// a CU holds as many independent contigs as the slices allow.  Per contig:
+//   attachments (orgscorer.py:359-392)        lane per hit, loci in LDS, wave scan for slots
+//   (clade, locus) sort (:394-406)            bitonic in registers: R keys per lane, strides
+//                                             < 64 by shuffles, >= 64 inside the lane
+//   segment means (:399-406)                  lane per segment (numpy closed forms), the wave
+//                                             together for multi-run segments
+//   maxes, weak loci, Contig.score, explain_one, meld_one (:407-429, :447-461, :585-597,
+//                                             :621-631)   lane per clade run
+// Two forms of the same kernel:
+//   k_wave<CAP, false>  every contig, level 0, explain_one only (small slice, high occupancy)
+//   k_wave<CAP, true>   the contigs the first one handed over: explain_two (:599-619), the
+//                       LGT checks and meld_two (:633-744, eval_two of wf_device.h), and the
+//                       roll-up loop (:431-445, :566-583) -- attachments re-keyed to the parent
+//                       clade in LDS, level after level
+// A contig neither can finish (more attachments than a slice holds, more than 64 loci, a
+// leaf table, segment or explain_two state the slice cannot hold) is handed to the staged
+// path (wf_staged.hip) with its attachment and leaf counts; the staged level 0 then runs on
 // those contigs only.  Contigs finished here never write attachments, keys or segment
 // records to HBM: their traffic is the hits and loci read once plus the result record.
+#include <algorithm>
+
 #include "wf_device.h"
+
+// WF_SKIP (diagnostic variants only, never the product build): 1 skips the segment means,
+// 2 the sort, 4 explain_one, 8 everything after the attachments -- per-phase cost by
+// difference of kernel times (no contig is handed on, the results are not meaningful).
+#ifndef WF_SKIP
+#define WF_SKIP 0
+#endif
 
 namespace wf {
 
 namespace {
 
-constexpr int kFastNT = 256;
-constexpr int kFastW = kFastNT / 64;
-constexpr int kFastCap = 512;        // attachments held in LDS (the sort width)
 constexpr int kSlotBits = 9;         // key = clade << 15 | locus << 9 | attachment slot
 constexpr int kCladeShift = 15;
-constexpr int kFastLoc = 64;         // loci per contig (locus bitmasks are 64-bit)
-constexpr int kFastRuns = 64;        // envelope runs of a multi-attachment segment
-constexpr int kFastMultiAtt = 32;    // ... so at most 32 attachments (2 * 32 - 1 runs)
+constexpr uint64_t kSlotMask = (1u << kSlotBits) - 1;
+constexpr int kLoc0 = 64;            // loci per contig (locus bitmasks are 64-bit)
+constexpr int kLut0 = 256;           // packed leaf-table entries of the contig's loci
+constexpr int kAnn0 = 64;            // (locus, system) annotation slots
+constexpr int kRuns0 = 64;           // envelope runs of a multi-attachment segment ...
+constexpr int kMultiAtt0 = 32;       // ... so at most 32 attachments (2 * 32 - 1 runs)
+constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two
 
-struct FastSmem {
-  uint64_t key[kFastCap];            // sort keys (slot order until the sort)
-  int2 lohi[kFastCap];               // by slot: site range [lo, hi); after the means: (clade, locus) by segment
-  double sc[kFastCap];               // by slot: score; after the means: option rank by segment
-  int hit[kFastCap];                 // by slot: hit index; then the multi-run list, then meld members
-  int seg[kFastCap + 1];             // segment starts (sorted positions)
-  double v[kFastCap];                // segment means
-  int lo[kFastLoc], len[kFastLoc], nl[kFastLoc];
-  int8_t st[kFastLoc];
-  unsigned long long mx[kFastLoc];   // per-locus max score bits over known clades
-  unsigned long long abest[kAnnSlots];
-  int ahit[kAnnSlots];
-  WaveRunsT<kFastRuns> runs[kFastW];
-  int red_i[kFastW];
-  long long red_l[kFastW];
-  double red_r[kFastW], red_c[kFastW];
-  long long red_k[kFastW];
-  int n_multi, n_mem, flag, lca;
-  unsigned long long um;
+// One wave's LDS slice.  `scr` is reused phase by phase (offsets in the accessors):
+//   attachments:  hit[CAP] | sm[CAP]                         (annotation pass 2)
+//   means:        v[CAP] | runs                              (multi-run segments)
+//   explain_one:  v | rank[CAP] (FULL; else in sc) | mem[CAP]
+//   explain_two:  v | cl[CAP] | sib[CAP] | hm[CAP] | S[CAP] | masks, loci lists (FULL only)
+// key, lohi and sc (by slot) live across roll-up levels.
+template <int CAP, bool FULL>
+struct WaveSmem {
+  static constexpr int kScr = FULL ? 32 * CAP + 2048 : 8 * CAP + (4 * CAP > 1792 ? 4 * CAP : 1792);
+  uint64_t key[CAP];                 // keys by slot, then in sorted order
+  int2 lohi[CAP];                    // by slot: site range [lo, hi)
+  double sc[CAP];                    // by slot: score
+  uint16_t seg[CAP + 2];             // segment starts (sorted positions)
+  uint32_t lut[kLut0];               // packed leaf tables, locus g at lbase[g]
+  int lo[kLoc0], len[kLoc0];
+  int16_t lbase[kLoc0], nl1[kLoc0];
+  int8_t st[kLoc0];
+  unsigned long long mx[kLoc0];      // per-locus max score bits over known clades
+  unsigned long long abest[kAnn0];
+  int ahit[kAnn0];
+  alignas(16) char scr[kScr];
+  __device__ int* hit() { return reinterpret_cast<int*>(scr); }
+  __device__ int* sm() { return reinterpret_cast<int*>(scr) + CAP; }
+  __device__ double* v() { return reinterpret_cast<double*>(scr); }
+  __device__ WaveRunsT<kRuns0>& runs() { return *reinterpret_cast<WaveRunsT<kRuns0>*>(scr + 8 * CAP); }
+  __device__ double* rank() { return FULL ? reinterpret_cast<double*>(scr + 8 * CAP) : sc; }
+  __device__ int* mem() { return reinterpret_cast<int*>(scr + (FULL ? 16 : 8) * CAP); }
+  __device__ int* cl() { return reinterpret_cast<int*>(scr + 8 * CAP); }
+  __device__ int* sib() { return reinterpret_cast<int*>(scr + 12 * CAP); }
+  __device__ uint64_t* hm() { return reinterpret_cast<uint64_t*>(scr + 16 * CAP); }
+  __device__ double* S() { return reinterpret_cast<double*>(scr + 24 * CAP); }
+  __device__ uint64_t* pmask() { return reinterpret_cast<uint64_t*>(scr + 32 * CAP); }   // [kPot0]
+  __device__ int* ign() { return reinterpret_cast<int*>(scr + 32 * CAP + 8 * kPot0); }  // [64]
+  __device__ int* um() { return ign() + 64; }
+  __device__ int* loc_len() { return ign() + 128; }
+  __device__ uint8_t* best_syn() { return reinterpret_cast<uint8_t*>(ign() + 192); }    // [64]
 };
-
-// Exclusive block prefix sum (two barriers); *total = block sum.
-__device__ __forceinline__ int fast_scan(int v, int* total, FastSmem& F) {
-  const int lane = lane_id(), w = wave_id();
-  int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) F.red_i[w] = x;
-  __syncthreads();
-  int base = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < kFastW; ++i) {
-    const int t = F.red_i[i];
-    base += i < w ? t : 0;
-    tot += t;
-  }
-  __syncthreads();
-  *total = tot;
-  return base + x - v;
-}
-
-__device__ __forceinline__ long long fast_sum(long long v, FastSmem& F) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  if (lane_id() == 0) F.red_l[wave_id()] = v;
-  __syncthreads();
-  long long t = 0;
-#pragma unroll
-  for (int i = 0; i < kFastW; ++i) t += F.red_l[i];
-  __syncthreads();
-  return t;
-}
 
 __device__ __forceinline__ int leaves_for(const SArgs& S, int len) {
   return (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
          (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
 }
 
-__global__ __launch_bounds__(kFastNT) void k_fast(const SArgs S, int64_t* ccnt, int64_t* cleaves,
-                                                  int32_t* pend) {
+__device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
+
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
+  const int lane = lane_id();
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  *total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+__device__ __forceinline__ int wave_lca(const KArgs& K, int acc) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc = lca2(K, acc, __shfl_xor(acc, off, 64));
+  return acc;
+}
+
+// Ascending bitonic sort of N = 64 * R keys, element lane + 64 r in x[r].
+template <int R>
+__device__ __forceinline__ void wave_sort(uint64_t (&x)[R]) {
+  const int lane = lane_id();
+  constexpr int N = 64 * R;
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {                                 // partner: same lane, element r ^ (j / 64)
+        const int jr = j >> 6;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (r & jr) continue;
+          const int i = lane + 64 * r;
+          const bool asc = (i & k) == 0;
+          const uint64_t a = x[r], b = x[r | jr];
+          const bool sw = (a > b) == asc;
+          x[r] = sw ? b : a;
+          x[r | jr] = sw ? a : b;
+        }
+      } else {                                       // partner: lane ^ j
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int i = lane + 64 * r;
+          const uint64_t y = __shfl_xor(x[r], j, 64);
+          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+          x[r] = keep_min ? (y < x[r] ? y : x[r]) : (y > x[r] ? y : x[r]);
+        }
+      }
+    }
+  }
+}
+
+template <int R, class SM>
+__device__ __forceinline__ void sort_slice(SM& F, int n_att) {
+  const int lane = lane_id();
+  uint64_t x[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = lane + 64 * r;
+    x[r] = t < n_att ? F.key[t] : ~0ull;
+  }
+  wave_sort<R>(x);
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = lane + 64 * r;
+    if (t < n_att) F.key[t] = x[r];
+  }
+  wave_sync();
+}
+
+template <class SM>
+__device__ __forceinline__ int2 cg_of(SM& F, int s) {
+  const uint64_t k0 = F.key[F.seg[s]];
+  return make_int2((int)(k0 >> kCladeShift), (int)((k0 >> kSlotBits) & (kLoc0 - 1)));
+}
+
+// explain_two + LGT filters + meld_two for one level in the slice (decide_two's arithmetic,
+// orgscorer.py:599-619, 633-744; eval_two / pair_rank / pair_crit of wf_device.h on a
+// Contig whose rows are the potential clades first, then the others).  Returns kDecDone
+// (written), kDecStop, kDecRaise, or -1 when the state does not fit (staged path).
+template <int CAP>
+__device__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int c, int64_t h0, int64_t l0, int G, int ns,
+                        uint64_t um, int Gu, int iteration, int64_t& pair_evals) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
-  __shared__ FastSmem F;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lane = lane_id();
+  const double* v = F.v();
+  const uint64_t allG = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+  // a clade run starting at segment t: max score over all G loci (missing loci are 0.0),
+  // loci at or above the sister threshold, loci present
+  auto run_scan = [&](int t, int clade, double& mx, uint64_t& hmask, uint64_t& present) {
+    mx = -__builtin_inf();
+    hmask = 0;
+    present = 0;
+    for (int q = t; q < ns; ++q) {
+      const int2 cq = cg_of(F, q);
+      if (cq.x != clade) break;
+      const double x = v[q];
+      mx = x > mx ? x : mx;
+      present |= 1ull << cq.y;
+      if (x >= P.sister_thr) hmask |= 1ull << cq.y;
+    }
+    if (present != allG) {
+      mx = 0.0 > mx ? 0.0 : mx;
+      if (0.0 >= P.sister_thr) hmask |= allG & ~present;
+    }
+  };
+  // pass A: clades, potential clades (:603-605), root present
+  int Pn = 0, Pp = 0;
+  bool root = false;
+  for (int t0 = 0; t0 < ns; t0 += 64) {
+    const int t = t0 + lane;
+    bool head = false, pot = false;
+    if (t < ns) {
+      const int clade = cg_of(F, t).x;
+      head = t == 0 || cg_of(F, t - 1).x != clade;
+      if (head) {
+        double mx;
+        uint64_t hmk, pres;
+        run_scan(t, clade, mx, hmk, pres);
+        pot = mx >= P.k2;
+        root = root || clade == K.root;
+      }
+    }
+    Pn += __popcll(__ballot(head));
+    Pp += __popcll(__ballot(pot));
+  }
+  root = __ballot(root) != 0ull;
+  pair_evals += (int64_t)Pp * (Pp - 1) / 2;
+  if (Pp > kPot0 || Pp * G > CAP || Pn > CAP) return -1;
+  // pass B: rows (potential clades first, clade order), S rows, sister data
+  double* Sm = F.S();
+  for (int i = lane; i < Pp * G; i += 64) Sm[i] = 0.0;
+  wave_sync();
+  int prow = 0, nrow = Pp;
+  for (int t0 = 0; t0 < ns; t0 += 64) {
+    const int t = t0 + lane;
+    bool head = false, pot = false;
+    int clade = -1;
+    double mx = 0.0;
+    uint64_t hmk = 0, pres = 0;
+    if (t < ns) {
+      clade = cg_of(F, t).x;
+      head = t == 0 || cg_of(F, t - 1).x != clade;
+      if (head) {
+        run_scan(t, clade, mx, hmk, pres);
+        pot = mx >= P.k2;
+      }
+    }
+    const uint64_t pm = __ballot(pot), nm = __ballot(head && !pot);
+    if (head) {
+      const int row = pot ? prow + __popcll(pm & lanes_below()) : nrow + __popcll(nm & lanes_below());
+      F.cl()[row] = clade;
+      F.sib()[row] = K.sibp[clade];
+      F.hm()[row] = hmk;
+      if (pot)
+        for (int q = t; q < ns; ++q) {
+          const int2 cq = cg_of(F, q);
+          if (cq.x != clade) break;
+          Sm[row * G + cq.y] = v[q];
+        }
+    }
+    prow += __popcll(pm);
+    nrow += __popcll(nm);
+  }
+  if (lane < G) {
+    F.ign()[lane] = ((um >> lane) & 1ull) ? 0 : 1;
+    F.loc_len()[lane] = F.len[lane];
+    if ((um >> lane) & 1ull) F.um()[__popcll(um & lanes_below())] = lane;
+  }
+  wave_sync();
+  Contig C;
+  C.l0 = l0;
+  C.G = G;
+  C.h0 = h0;
+  C.mbase = 2 * h0 + 2 * (int64_t)c;
+  C.S = Sm;
+  C.ign = F.ign();
+  C.um = F.um();
+  C.loc_len = F.loc_len();
+  C.cl_id = F.cl();
+  C.sib_of = F.sib();
+  C.hm = F.hm();
+  const uint64_t full = Gu >= 64 ? ~0ull : ((1ull << Gu) - 1ull);
+  for (int i = lane; i < Pp; i += 64) {             // "crit >= k2" masks over the unmasked loci
+    uint64_t m = 0;
+    for (int u = 0; u < Gu; ++u)
+      if (Sm[i * G + C.um[u]] >= P.k2) m |= 1ull << u;
+    F.pmask()[i] = m;
+  }
+  wave_sync();
+  const uint64_t* pmask = F.pmask();
+  // pass 1: best pair over all pairs clade1 < clade2 (rows in name order), ties -> later pair
+  double br = -__builtin_inf();
+  long long bk = -1;
+  for (int i = 0; i + 1 < Pp; ++i) {
+    const uint64_t mi = pmask[i];
+    for (int j = i + 1 + lane; j < Pp; j += 64) {
+      if ((mi | pmask[j]) != full) continue;
+      const double r = pair_rank(C, i, j, Gu);
+      const long long key = (long long)i * Pp + j;
+      if (better(r, key, br, bk)) { br = r; bk = key; }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double r2 = __shfl_xor(br, off, 64);
+    const long long k2 = __shfl_xor(bk, off, 64);
+    if (better(r2, k2, br, bk)) { br = r2; bk = k2; }
+  }
+  if (bk >= 0) {
+    const int bi = (int)(bk / Pp), bj = (int)(bk % Pp);
+    int b_ok = 0, b_dir = 0, b_c1p = 0, b_c2p = 0;
+    double bcrit = 0.0;
+    if (lane == 0) {
+      const OptEval e = eval_two(K, C, Pn, bi, bj, nullptr, F.best_syn());
+      b_ok = e.ok; b_dir = e.dir; b_c1p = e.c1p; b_c2p = e.c2p;
+      bcrit = pair_crit(C, bi, bj, Gu);
+    }
+    b_ok = __shfl(b_ok, 0, 64); b_dir = __shfl(b_dir, 0, 64);
+    b_c1p = __shfl(b_c1p, 0, 64); b_c2p = __shfl(b_c2p, 0, 64);
+    bcrit = __shfl(bcrit, 0, 64);
+    wave_sync();
+    // pass 2: options within --range of the best get the LGT filters (:636-639)
+    int n_in = 0;
+    bool all_ok = true, all_same = true;
+    uint64_t b1 = 0, b2 = 0;
+    for (int i = 0; i + 1 < Pp; ++i) {
+      const uint64_t mi = pmask[i];
+      for (int j = i + 1 + lane; j < Pp; j += 64) {
+        if ((mi | pmask[j]) != full) continue;
+        const double r = pair_rank(C, i, j, Gu);
+        if (!((br - r) <= P.range)) continue;
+        const OptEval e = eval_two(K, C, Pn, i, j, F.best_syn(), nullptr);
+        ++n_in;
+        all_ok = all_ok && e.ok;
+        all_same = all_same && e.same;
+        b1 |= 1ull << e.c1p;
+        b2 |= 1ull << e.c2p;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      n_in += __shfl_xor(n_in, off, 64);
+      b1 |= __shfl_xor(b1, off, 64);
+      b2 |= __shfl_xor(b2, off, 64);
+    }
+    all_ok = __ballot(!all_ok) == 0ull;
+    all_same = __ballot(!all_same) == 0ull;
+    // meld_two (:640-669): 0 none, 1 best as is, 2 meld, 3 unchecked best, 4 upstream crash
+    int kind;
+    if (n_in == 0) kind = (P.dis2 == 0) ? 3 : (P.dis2 == 1 ? 0 : 4);   // --range < 0
+    else if (n_in == 1 || P.dis2 == 0) kind = 1;
+    else if (P.dis2 == 1) kind = 0;
+    else kind = (all_ok && all_same) ? 2 : 0;
+    if (kind == 4) {
+      if (lane == 0) K.status[c] = WF_E_BADINPUT;
+      return kDecDone;
+    }
+    bool have_ok = false;
+    int lca1 = -1, lca2v = -1;
+    const int m1 = __popcll(b1), m2 = __popcll(b2);
+    if (kind == 2) {
+      const bool in1 = lane < Pp && ((b1 >> lane) & 1ull), in2 = lane < Pp && ((b2 >> lane) & 1ull);
+      lca1 = wave_lca(K, in1 ? F.cl()[lane] : -1);
+      lca2v = wave_lca(K, in2 ? F.cl()[lane] : -1);
+      bool keep = true;
+      if (!P.allow_lca) {
+        const int nl = lca2(K, lca1, lca2v);
+        keep = !(nl == lca1 || nl == lca2v);
+      }
+      have_ok = keep;                                // melded options are all OK
+      if (have_ok) {
+        if (in1) K.meld[C.mbase + __popcll(b1 & lanes_below())] = F.cl()[lane];
+        if (in2) K.meld[C.mbase + m1 + __popcll(b2 & lanes_below())] = F.cl()[lane];
+      }
+    } else if (kind == 1) {
+      have_ok = b_ok != 0;
+    } else if (kind == 3) {
+      have_ok = true;
+    }
+    if (have_ok) {
+      if (lane < G) K.syn[l0 + lane] = F.best_syn()[lane];
+      if (lane == 0) {
+        K.call[c] = WF_CALL_LGT;
+        K.crit[c] = bcrit;
+        K.rank[c] = br;
+        K.dir[c] = (int8_t)b_dir;
+        K.c1[c] = (kind == 2) ? lca1 : F.cl()[b_c1p];
+        K.c2[c] = (kind == 2) ? lca2v : F.cl()[b_c2p];
+        K.nm1[c] = (kind == 2) ? m1 : 0;
+        K.nm2[c] = (kind == 2) ? m2 : 0;
+        K.iters[c] = (int16_t)iteration;
+        K.pair_evals[c] = pair_evals;
+      }
+      return kDecDone;
+    }
+  }
+  return (Pn == 0 || root) ? kDecStop : kDecRaise;
+}
+
+template <int CAP, bool FULL>
+__global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
+                                             const int32_t* list, int n_list, const int64_t* n_dev) {
+  if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
+  const KArgs& K = S.k;
+  const DevParams& P = K.p;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  WaveSmem<CAP, FULL>& F = *reinterpret_cast<WaveSmem<CAP, FULL>*>(smem);
+  const int lane = threadIdx.x;
   const int nsys = K.n_sys;
-  for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
+  for (int ci = blockIdx.x; ci < n_list; ci += gridDim.x) {
+    const int c = list ? list[ci] : ci;
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     const int64_t l0 = K.loc_off[c];
     const int G = (int)(K.loc_off[c + 1] - l0);
-    const int Gs = min(G, kFastLoc);
-    for (int g = tid; g < kFastLoc; g += kFastNT) {
-      F.mx[g] = 0ull;
-      if (g < Gs) {
-        const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
-        const int len = max(a, b) - min(a, b) + 1;
-        F.lo[g] = min(a, b);
-        F.len[g] = len;
-        F.st[g] = K.lstrand[l0 + g];
-        F.nl[g] = leaves_for(S, len);
-      }
+    const int Gs = min(G, kLoc0);
+    // ---- loci (lane g), leaf-table bases ----
+    F.mx[lane] = 0ull;
+    int nl1 = 0;
+    if (lane < Gs) {
+      const int a = K.lstart[l0 + lane], b = K.lend[l0 + lane];
+      const int len = max(a, b) - min(a, b) + 1;
+      F.lo[lane] = min(a, b);
+      F.len[lane] = len;
+      F.st[lane] = K.lstrand[l0 + lane];
+      if (len < kNpyBuf) nl1 = S.lut_off[len + 1] - S.lut_off[len];
+      F.nl1[lane] = (int16_t)nl1;
     }
-    const int nann = Gs * nsys;                    // <= kAnnSlots (checked on the host)
-    for (int i = tid; i < nann; i += kFastNT) { F.abest[i] = 0ull; F.ahit[i] = -1; }
-    if (tid == 0) { F.n_multi = 0; F.n_mem = 0; F.flag = 0; }
-    __syncthreads();
+    int lut_total;
+    const int lb = wave_excl_scan(nl1, &lut_total);
+    F.lbase[lane] = (int16_t)min(lb, 32767);
+    const int nann = Gs * nsys;
+    F.abest[lane] = 0ull;
+    F.ahit[lane] = -1;
+    bool staged = G > kLoc0 || lut_total > kLut0 || nann > kAnn0;
+    wave_sync();
+    if (!staged)                                     // packed leaf tables of the contig's lengths
+      for (int g = 0; g < G; ++g) {
+        const int len = F.len[g], n = F.nl1[g];
+        for (int j = lane; j < n; j += 64) F.lut[F.lbase[g] + j] = pack_leaf(S.lut[S.lut_off[len] + j]);
+      }
 
     // ---- hits -> attachments, in (hit, locus) order (orgscorer.py:359-382) ----
     int n_att = 0;
     long long nl_sum = 0;
-    for (int64_t hb = h0; hb < h1; hb += kFastNT) {
-      const int64_t h = hb + tid;
-      int n = 0;
-      uint64_t am = 0;
-      int qlo = 0, qhi = 0;
-      const bool live = h < h1 && K.scov[h] >= P.min_scov;
-      if (live) {
+    for (int64_t hb = h0; hb < h1; hb += 64) {
+      const int64_t h = hb + lane;
+      int qlo = 0, qhi = 0, hs = 0, clade = 0;
+      double scv = 0.0, sc = 0.0;
+      uint32_t m = 0u;
+      if (h < h1) {                                  // every field in one round of loads
+        scv = K.scov[h];
         qlo = K.qlo[h];
         qhi = K.qhi[h];
-        const int hs = K.hstrand[h];
+        hs = K.hstrand[h];
+        clade = K.taxon[h];
+        sc = K.score[h];
+        if (nsys > 0) m = K.sysmask[h];
+      }
+      int n = 0;
+      uint64_t am = 0;
+      if (h < h1 && scv >= P.min_scov) {
         for (int g = 0; g < G; ++g) {
-          int lo, len, st, nlg;
-          if (g < kFastLoc) {
-            lo = F.lo[g]; len = F.len[g]; st = F.st[g]; nlg = F.nl[g];
+          int lo, len, st;
+          if (g < kLoc0) {
+            lo = F.lo[g]; len = F.len[g]; st = F.st[g];
           } else {                                   // counted only (the contig goes staged)
             const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
-            lo = min(a, b); len = max(a, b) - lo + 1; st = K.lstrand[l0 + g]; nlg = leaves_for(S, len);
+            lo = min(a, b); len = max(a, b) - lo + 1; st = K.lstrand[l0 + g];
           }
           if (attaches(P, qlo, qhi, hs, lo, len, st)) {
             ++n;
-            nl_sum += nlg;
-            if (g < kFastLoc) am |= 1ull << g;
+            nl_sum += leaves_for(S, len);
+            if (g < kLoc0) am |= 1ull << g;
           }
         }
       }
       int total;
-      const int o = fast_scan(n, &total, F);
-      if (n > 0 && G <= kFastLoc && n_att + o + n <= kFastCap) {
-        int clade = K.taxon[h];
+      const int o = wave_excl_scan(n, &total);
+      if (!staged && n > 0 && n_att + o + n <= CAP) {
         for (int j = 0; j < P.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
-        const double sc = K.score[h];
-        const uint32_t m = nsys > 0 ? K.sysmask[h] : 0u;
         const bool ann = m != 0 && sc >= P.annot_ref;
         int slot = n_att + o;
         for (uint64_t bits = am; bits; bits &= bits - 1, ++slot) {
@@ -162,7 +487,8 @@ __global__ __launch_bounds__(kFastNT) void k_fast(const SArgs S, int64_t* ccnt, 
           F.key[slot] = ((uint64_t)(uint32_t)clade << kCladeShift) | ((uint64_t)g << kSlotBits) | (uint64_t)slot;
           F.lohi[slot] = make_int2(start, stop);
           F.sc[slot] = sc;
-          F.hit[slot] = (int)h;
+          F.hit()[slot] = (int)h;
+          F.sm()[slot] = (int)m;
           if (ann)                                   // annotation pass 1: best score bits (:383-392)
             for (int b = 0; b < nsys; ++b)
               if ((m >> b) & 1u) atomicMax(&F.abest[g * nsys + b], dbits(sc));
@@ -170,242 +496,288 @@ __global__ __launch_bounds__(kFastNT) void k_fast(const SArgs S, int64_t* ccnt, 
       }
       n_att += total;
     }
-    const long long leaves = fast_sum(nl_sum, F);
-    bool staged = G > kFastLoc || n_att > kFastCap;
-    if (!staged && G > 0) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nl_sum += __shfl_xor(nl_sum, off, 64);
+    staged = staged || n_att > CAP;
+    wave_sync();
+    if (!staged && G > 0 && nsys > 0) {
       // annotation pass 2: the last hit (largest index) at the best score per (locus, system)
-      if (nsys > 0) {
-        for (int t = tid; t < n_att; t += kFastNT) {
-          const int h = F.hit[t];
-          const uint32_t m = K.sysmask[h];
-          const double sc = F.sc[t];
-          if (m == 0 || !(sc >= P.annot_ref)) continue;
-          const int g = (int)((F.key[t] >> kSlotBits) & (kFastLoc - 1));
-          for (int b = 0; b < nsys; ++b)
-            if (((m >> b) & 1u) && F.abest[g * nsys + b] == dbits(sc)) atomicMax(&F.ahit[g * nsys + b], h);
-        }
-        __syncthreads();
-        for (int i = tid; i < nann; i += kFastNT) K.annot[l0 * nsys + i] = F.ahit[i];
+      for (int t = lane; t < n_att; t += 64) {
+        const uint32_t m = (uint32_t)F.sm()[t];
+        const double sc = F.sc[t];
+        if (m == 0 || !(sc >= P.annot_ref)) continue;
+        const int g = (int)((F.key[t] >> kSlotBits) & (kLoc0 - 1));
+        const int h = F.hit()[t];
+        for (int b = 0; b < nsys; ++b)
+          if (((m >> b) & 1u) && F.abest[g * nsys + b] == dbits(sc)) atomicMax(&F.ahit[g * nsys + b], h);
       }
+      wave_sync();
+      if (lane < nann) K.annot[l0 * nsys + lane] = F.ahit[lane];
     }
-    const bool evaluated = !staged && G > 0 && h1 > h0;   // else: never evaluated (:959)
-    if (evaluated) {
-      // ---- per-contig sort of (clade, locus, slot) keys ----
-      int n2 = 2;
-      while (n2 < n_att) n2 <<= 1;
-      for (int t = n_att + tid; t < n2; t += kFastNT) F.key[t] = ~0ull;
-      __syncthreads();
-      for (int k = 2; k <= n2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = tid; i < (n2 >> 1); i += kFastNT) {
-            const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));
-            const int hi = lo | j;
-            const bool up = (lo & k) == 0;
-            const uint64_t ka = F.key[lo], kb = F.key[hi];
-            if ((ka > kb) == up) { F.key[lo] = kb; F.key[hi] = ka; }
-          }
-          __syncthreads();
+    // ---- levels: sort, segments, means, explain_one [, explain_two, roll-up] ----
+    int64_t pair_evals = 0;
+    for (int level = 0; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
+      const int iteration = level + 1;
+      if (level > 0) {                               // roll up (:431-445): re-key to the parent clade
+        for (int t = lane; t < n_att; t += 64) {
+          const uint64_t k0 = F.key[t];
+          const int parent = K.parent[(int)(k0 >> kCladeShift)];
+          F.key[t] = ((uint64_t)(uint32_t)parent << kCladeShift) | (k0 & ((1ull << kCladeShift) - 1));
         }
+        wave_sync();
       }
+      if (WF_SKIP & 2) {
+      } else if (n_att <= 64) sort_slice<1>(F, n_att);
+      else if (n_att <= 128) sort_slice<2>(F, n_att);
+      else if (CAP <= 256 || n_att <= 256) sort_slice<4>(F, n_att);
+      else sort_slice<CAP / 64>(F, n_att);
       // ---- segments = runs of equal (clade, locus) ----
-      const int per = (n_att + kFastNT - 1) / kFastNT;
-      const int b0 = min(n_att, tid * per), e0 = min(n_att, b0 + per);
-      int heads = 0;
-      for (int t = b0; t < e0; ++t)
-        heads += (t == 0 || (F.key[t] >> kSlotBits) != (F.key[t - 1] >> kSlotBits)) ? 1 : 0;
-      int ns;
-      int so = fast_scan(heads, &ns, F);
-      for (int t = b0; t < e0; ++t)
-        if (t == 0 || (F.key[t] >> kSlotBits) != (F.key[t - 1] >> kSlotBits)) F.seg[so++] = t;
-      if (tid == 0) F.seg[ns] = n_att;
-      __syncthreads();
+      int ns = 0;
+      for (int t0 = 0; t0 < n_att; t0 += 64) {
+        const int t = t0 + lane;
+        const bool head = t < n_att && (t == 0 || (F.key[t] >> kSlotBits) != (F.key[t - 1] >> kSlotBits));
+        const uint64_t hm = __ballot(head);
+        if (head) F.seg[ns + __popcll(hm & lanes_below())] = (uint16_t)t;
+        ns += __popcll(hm);
+      }
+      if (lane == 0) F.seg[ns] = (uint16_t)n_att;
+      wave_sync();
       // ---- segment means (numpy pairwise order, exact) ----
-      for (int s = tid; s < ns; s += kFastNT) {
-        const int kb = F.seg[s], ke = F.seg[s + 1], na = ke - kb;
-        const int g = (int)((F.key[kb] >> kSlotBits) & (kFastLoc - 1));
-        const int len = F.len[g];
-        const int nl = len < kNpyBuf ? S.lut_off[len + 1] - S.lut_off[len] : 1 << 30;
-        const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
-        bool one_run = false;
-        int lo = 0, hi = 0;
-        double v = 0.0;
-        if (na == 1) {
-          if (thread_ok) {
-            const int slot = (int)(F.key[kb] & ((1u << kSlotBits) - 1));
-            lo = F.lohi[slot].x; hi = F.lohi[slot].y; v = F.sc[slot];
-            one_run = true;
-          }
-        } else if (na <= kPruneMax) {
-          double Fw = 0.0;                             // best whole-locus attachment
-          for (int t = kb; t < ke; ++t) {
-            const int slot = (int)(F.key[t] & ((1u << kSlotBits) - 1));
-            const int2 x = F.lohi[slot];
-            const double sc = F.sc[slot];
-            if (x.x <= 0 && x.y >= len && sc > Fw) Fw = sc;
-          }
-          int kept = 0;                                // attachments the envelope still needs
-          for (int t = kb; t < ke; ++t) {
-            const int slot = (int)(F.key[t] & ((1u << kSlotBits) - 1));
-            const int2 x = F.lohi[slot];
-            kept += (x.x < x.y && F.sc[slot] > Fw) ? 1 : 0;
-          }
-          if (kept == 0 && thread_ok) { lo = 0; hi = len; v = Fw; one_run = true; }
-        }
-        if (one_run)
-          F.v[s] = one_run_mean(S.lut + S.lut_off[len], nl, len, lo, hi, v);
-        else if (na <= kFastMultiAtt && nl <= 64 && len < kNpyBuf)
-          F.hit[atomicAdd(&F.n_multi, 1)] = s;
-        else
-          F.flag = 1;                                  // the staged leaf kernels take it
-      }
-      __syncthreads();
-      const int n_multi = F.n_multi;
-      for (int i = w; i < n_multi; i += kFastW) {      // one wave per multi-run segment
-        const int s = F.hit[i];
-        const int kb = F.seg[s], na = F.seg[s + 1] - kb;
-        const int g = (int)((F.key[kb] >> kSlotBits) & (kFastLoc - 1));
-        const int len = F.len[g];
-        int lo = 0, hi = 0;
-        double sc = 0.0;
-        if (lane < na) {
-          const int slot = (int)(F.key[kb + lane] & ((1u << kSlotBits) - 1));
-          const int2 x = F.lohi[slot];
-          if (x.x < x.y) { lo = x.x; hi = x.y; sc = F.sc[slot]; }
-        }
-        const double m = wave_seg_mean(S.lut + S.lut_off[len], S.lut_off[len + 1] - S.lut_off[len], len,
-                                       lo, hi, sc, F.runs[w]);
-        if (lane == 0) F.v[s] = m;
-      }
-      __syncthreads();
-      staged = F.flag != 0;
-      if (!staged) {
-        // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
-        for (int s = tid; s < ns; s += kFastNT) {      // (clade, locus) by segment, into lohi
-          const uint64_t k0 = F.key[F.seg[s]];
-          F.lohi[s] = make_int2((int)(k0 >> kCladeShift), (int)((k0 >> kSlotBits) & (kFastLoc - 1)));
-        }
-        __syncthreads();
-        for (int s = tid; s < ns; s += kFastNT) {      // per-locus max over known clades
-          const int2 cg = F.lohi[s];
-          const double v = F.v[s];
-          if (cg.x != K.unknown && v > 0.0) atomicMax(&F.mx[cg.y], dbits(v));
-        }
-        __syncthreads();
-        if (w == 0) {                                  // weak loci: ignore -> mask, penalize -> none
-          const double mx = __longlong_as_double((long long)F.mx[lane]);
-          const unsigned long long um = __ballot(lane < G && (P.weak != 0 || mx >= P.kmin));
-          if (lane == 0) F.um = um;
-        }
-        __syncthreads();
-        const uint64_t um = F.um;
-        const int Gu = __popcll(um);
-        if (Gu > 0) {                                  // else: skipped contig at level 0 (:959)
-          double br = -__builtin_inf(), bcrit = 0.0;
-          long long bk = -1;
-          for (int t = tid; t < ns; t += kFastNT) {
-            double rk = -1.0;
-            const int clade = F.lohi[t].x;
-            if (t == 0 || F.lohi[t - 1].x != clade) {
-              uint64_t m = um;
-              int q = t;
-              double crit = 0.0;
-              bool firstv = true;
-              auto next = [&]() -> double {
-                const int g = __builtin_ctzll(m);
-                m &= m - 1;
-                while (q < ns && F.lohi[q].x == clade && F.lohi[q].y < g) ++q;
-                const double v = (q < ns && F.lohi[q].x == clade && F.lohi[q].y == g) ? F.v[q] : 0.0;
-                crit = (firstv || v < crit) ? v : crit;
-                firstv = false;
-                return v;
-              };
-              const double rank = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
-              if (crit >= P.k1) {
-                rk = rank;
-                if (better(rank, clade, br, bk)) { br = rank; bk = clade; bcrit = crit; }
-              }
+      double* v = F.v();
+      bool fail = false;
+      for (int s0 = 0; s0 < ns; s0 += 64) {
+        const int s = s0 + lane;
+        bool multi = false;
+        int g = 0, len = 0, nl = 0;
+        if (WF_SKIP & 1) {
+          if (s < ns) v[s] = 0.75;
+        } else if (s < ns) {
+          const int kb = F.seg[s], ke = F.seg[s + 1], na = ke - kb;
+          g = (int)((F.key[kb] >> kSlotBits) & (kLoc0 - 1));
+          len = F.len[g];
+          nl = F.nl1[g];
+          const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
+          bool one_run = false;
+          int lo = 0, hi = 0;
+          double vv = 0.0;
+          if (na == 1) {
+            if (thread_ok) {
+              const int slot = (int)(F.key[kb] & kSlotMask);
+              lo = F.lohi[slot].x; hi = F.lohi[slot].y; vv = F.sc[slot];
+              one_run = true;
             }
-            F.sc[t] = rk;                              // option rank by segment (-1: none)
-          }
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) {
-            const double r2 = __shfl_xor(br, off, 64), c2 = __shfl_xor(bcrit, off, 64);
-            const long long k2 = __shfl_xor(bk, off, 64);
-            if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
-          }
-          if (lane == 0) { F.red_r[w] = br; F.red_k[w] = bk; F.red_c[w] = bcrit; }
-          __syncthreads();
-          br = F.red_r[0]; bk = F.red_k[0]; bcrit = F.red_c[0];
-#pragma unroll
-          for (int i = 1; i < kFastW; ++i)
-            if (better(F.red_r[i], F.red_k[i], br, bk)) { br = F.red_r[i]; bk = F.red_k[i]; bcrit = F.red_c[i]; }
-          if (bk < 0) {
-            staged = true;                             // explain_two (:570): the staged level 0
-          } else {
-            if (P.dis1 == 1)                           // meld_one (:621-631): options within --range
-              for (int t = tid; t < ns; t += kFastNT) {
-                const double rk = F.sc[t];
-                if (rk >= 0.0 && (br - rk) <= P.range) F.hit[atomicAdd(&F.n_mem, 1)] = F.lohi[t].x;
-              }
-            __syncthreads();
-            const int nm = F.n_mem;
-            if (P.dis1 == 1 && nm == 0) {              // negative --range upstream crash
-              if (tid == 0) K.status[c] = WF_E_BADINPUT;
-            } else {
-              int lca = (int)bk;
-              if (P.dis1 == 1) {
-                if (w == 0) {
-                  int acc = -1;
-                  for (int i = lane; i < nm; i += 64) acc = lca2(K, acc, F.hit[i]);
-#pragma unroll
-                  for (int off = 32; off > 0; off >>= 1) acc = lca2(K, acc, __shfl_xor(acc, off, 64));
-                  if (lane == 0) F.lca = acc;
-                }
-                __syncthreads();
-                lca = F.lca;
-              }
-              const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
-              for (int i = tid; i < nm; i += kFastNT) K.meld[mbase + i] = F.hit[i];
-              for (int g = tid; g < G; g += kFastNT)   // set_synteny_one (:495-509)
-                K.syn[l0 + g] = ((um >> g) & 1ull) ? 'A' : '~';
-              if (tid == 0) {
-                K.call[c] = WF_CALL_NO_LGT;
-                K.crit[c] = bcrit;
-                K.rank[c] = br;
-                K.c1[c] = lca;
-                K.c2[c] = -1;
-                K.nm1[c] = nm;
-                K.iters[c] = 1;
-                K.pair_evals[c] = 0;
-              }
+          } else if (na <= kPruneMax) {
+            double Fw = 0.0;                           // best whole-locus attachment
+            for (int t = kb; t < ke; ++t) {
+              const int slot = (int)(F.key[t] & kSlotMask);
+              const int2 x = F.lohi[slot];
+              const double sc = F.sc[slot];
+              if (x.x <= 0 && x.y >= len && sc > Fw) Fw = sc;
             }
+            int kept = 0;                              // attachments the envelope still needs
+            for (int t = kb; t < ke; ++t) {
+              const int slot = (int)(F.key[t] & kSlotMask);
+              const int2 x = F.lohi[slot];
+              kept += (x.x < x.y && F.sc[slot] > Fw) ? 1 : 0;
+            }
+            if (kept == 0 && thread_ok) { lo = 0; hi = len; vv = Fw; one_run = true; }
           }
+          if (one_run)
+            v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
+          else if (na <= kMultiAtt0 && nl <= 64 && len < kNpyBuf)
+            multi = true;
+          else
+            fail = true;                               // the staged leaf kernels take it
+        }
+        for (uint64_t mm = __ballot(multi); mm; mm &= mm - 1) {   // the wave, one segment each
+          const int src = __builtin_ctzll(mm);
+          const int s2 = s0 + src;
+          const int kb = F.seg[s2], na = F.seg[s2 + 1] - kb;
+          const int g2 = __shfl(g, src, 64), len2 = __shfl(len, src, 64), nl2 = __shfl(nl, src, 64);
+          int lo = 0, hi = 0;
+          double sc = 0.0;
+          if (lane < na) {
+            const int slot = (int)(F.key[kb + lane] & kSlotMask);
+            const int2 x = F.lohi[slot];
+            if (x.x < x.y) { lo = x.x; hi = x.y; sc = F.sc[slot]; }
+          }
+          const double mean = wave_seg_mean(PackedLut{F.lut + F.lbase[g2]}, nl2, len2, lo, hi, sc, F.runs());
+          if (lane == 0) v[s2] = mean;
         }
       }
+      staged = __ballot(fail) != 0;
+      wave_sync();
+      if (staged || (WF_SKIP & 4)) break;
+      // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
+      if (FULL) F.mx[lane] = 0ull;
+      wave_sync();
+      for (int s = lane; s < ns; s += 64) {            // per-locus max over known clades
+        const int2 cg = cg_of(F, s);
+        const double x = v[s];
+        if (cg.x != K.unknown && x > 0.0) atomicMax(&F.mx[cg.y], dbits(x));
+      }
+      wave_sync();
+      // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
+      const double mxl = __longlong_as_double((long long)F.mx[lane]);
+      const uint64_t um = __ballot(lane < G && (P.weak != 0 || mxl >= P.kmin));
+      const int Gu = __popcll(um);
+      if (Gu == 0) {                                   // level 0: skipped contig (:959)
+        if (level > 0 && lane == 0) {                  // later: np.min of an empty array upstream
+          K.iters[c] = (int16_t)min(iteration, 32767);
+          K.pair_evals[c] = pair_evals;
+          K.status[c] = WF_E_EMPTYMASK;
+        }
+        break;
+      }
+      double br = -__builtin_inf(), bcrit = 0.0;
+      long long bk = -1;
+      double* rank = F.rank();
+      for (int t = lane; t < ns; t += 64) {
+        double rk = -1.0;
+        const int clade = cg_of(F, t).x;
+        if (t == 0 || cg_of(F, t - 1).x != clade) {
+          uint64_t mq = um;
+          int q = t;
+          int2 cq = cg_of(F, q);
+          double crit = 0.0;
+          bool firstv = true;
+          auto next = [&]() -> double {
+            const int gg = __builtin_ctzll(mq);
+            mq &= mq - 1;
+            while (q < ns && cq.x == clade && cq.y < gg) {
+              ++q;
+              if (q < ns) cq = cg_of(F, q);
+            }
+            const double x = (q < ns && cq.x == clade && cq.y == gg) ? v[q] : 0.0;
+            crit = (firstv || x < crit) ? x : crit;
+            firstv = false;
+            return x;
+          };
+          const double rnk = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+          if (crit >= P.k1) {
+            rk = rnk;
+            if (better(rnk, clade, br, bk)) { br = rnk; bk = clade; bcrit = crit; }
+          }
+        }
+        rank[t] = rk;                                  // option rank by segment (-1: none)
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const double r2 = __shfl_xor(br, off, 64), c2 = __shfl_xor(bcrit, off, 64);
+        const long long k2 = __shfl_xor(bk, off, 64);
+        if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
+      }
+      if (bk >= 0) {
+        wave_sync();
+        int nm = 0;                                    // meld_one (:621-631): options within --range
+        if (P.dis1 == 1)
+          for (int t0 = 0; t0 < ns; t0 += 64) {
+            const int t = t0 + lane;
+            const double rk = t < ns ? rank[t] : -1.0;
+            const bool in = rk >= 0.0 && (br - rk) <= P.range;
+            const uint64_t im = __ballot(in);
+            if (in) F.mem()[nm + __popcll(im & lanes_below())] = cg_of(F, t).x;
+            nm += __popcll(im);
+          }
+        wave_sync();
+        if (P.dis1 == 1 && nm == 0) {                  // negative --range upstream crash
+          if (lane == 0) K.status[c] = WF_E_BADINPUT;
+          break;
+        }
+        int lca = (int)bk;
+        if (P.dis1 == 1) {
+          int acc = -1;
+          for (int i = lane; i < nm; i += 64) acc = lca2(K, acc, F.mem()[i]);
+          lca = wave_lca(K, acc);
+        }
+        const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
+        for (int i = lane; i < nm; i += 64) K.meld[mbase + i] = F.mem()[i];
+        if (lane < G) K.syn[l0 + lane] = ((um >> lane) & 1ull) ? 'A' : '~';   // set_synteny_one
+        if (lane == 0) {
+          K.call[c] = WF_CALL_NO_LGT;
+          K.crit[c] = bcrit;
+          K.rank[c] = br;
+          K.c1[c] = lca;
+          K.c2[c] = -1;
+          K.nm1[c] = nm;
+          K.iters[c] = (int16_t)iteration;
+          K.pair_evals[c] = pair_evals;
+        }
+        break;
+      }
+      if (!FULL) {                                     // explain_two (:570): the next kernel
+        staged = true;
+        break;
+      }
+      wave_sync();
+      int dec = -1;
+      if constexpr (FULL) dec = wave_two(S, F, c, h0, l0, G, ns, um, Gu, iteration, pair_evals);
+      if (dec < 0) {
+        staged = true;
+        break;
+      }
+      if (dec == kDecDone) break;
+      if (dec == kDecRaise && iteration + 1 <= kMaxIter) {
+        wave_sync();
+        continue;
+      }
+      if (lane == 0) {                                 // unclassified after evaluation
+        K.iters[c] = (int16_t)min(dec == kDecRaise ? iteration + 1 : iteration, 32767);
+        K.pair_evals[c] = pair_evals;
+        K.status[c] = dec == kDecRaise ? WF_E_RUNAWAY : 0;
+      }
+      break;
     }
-    if (tid == 0) {
+    if (WF_SKIP) staged = false;                       // variants: time this kernel alone
+    if (lane == 0) {
       ccnt[c] = staged ? n_att : 0;
-      cleaves[c] = staged ? leaves : 0;
+      cleaves[c] = staged ? nl_sum : 0;
       pend[c] = staged ? 1 : 0;
     }
-    __syncthreads();                                   // LDS reuse by the next contig
+    wave_sync();                                       // the slice is reused by the next contig
   }
+}
+
+template <int CAP, bool FULL>
+int blocks_per_cu() {
+  static int n = -1;                                   // per process: one kernel image
+  if (n < 0) {
+    const int bytes = (int)sizeof(WaveSmem<CAP, FULL>);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wave<CAP, FULL>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_wave<CAP, FULL>), 64,
+                                                     bytes) != hipSuccess || b < 1)
+      b = 1;
+    n = b;
+  }
+  return n;
+}
+
+// n_list: the list length, or (n_dev set) an upper bound for the grid
+template <int CAP, bool FULL>
+hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
+                      int n_list, const int64_t* n_dev, int cus, hipStream_t s) {
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_list, (int64_t)cus * blocks_per_cu<CAP, FULL>()));
+  hipLaunchKernelGGL((k_wave<CAP, FULL>), dim3(grid), dim3(64), sizeof(WaveSmem<CAP, FULL>), s, sa, ccnt, cleaves, pend,
+                     list, n_list, n_dev);
+  return hipGetLastError();
 }
 
 }  // namespace
 
-int fast_blocks_per_cu() {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, reinterpret_cast<const void*>(&k_fast), kFastNT, 0) !=
-          hipSuccess || n < 1)
-    n = 1;
-  return n;
+hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
+                       hipStream_t s) {
+  const int N = sa.k.n_contigs;
+  return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, s)
+                         : launch_cap<512, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, s);
 }
 
-hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, unsigned grid,
-                       hipStream_t s) {
-  hipLaunchKernelGGL(k_fast, dim3(grid), dim3(kFastNT), 0, s, sa, ccnt, cleaves, pend);
-  return hipGetLastError();
+hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
+                       const int64_t* n_dev, int max_hits, int cus, hipStream_t s) {
+  const int N = sa.k.n_contigs;
+  return max_hits <= 256 ? launch_cap<256, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, s)
+                         : launch_cap<512, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, s);
 }
 
 }  // namespace wf

@@ -151,18 +151,21 @@ struct DetailsSink {
 };
 
 struct StagedState;
-// Fused level 0 (wf_fast.hip): per contig, 0 = finished here, 1 = handed to the staged
-// path with its attachment and leaf counts in ccnt / cleaves.
-hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, unsigned grid,
+// Per-contig wave kernels (wf_fast.hip): pend[c] = 0 finished there, 1 handed to the
+// staged path with its attachment and leaf counts in ccnt / cleaves.  launch_fast: every
+// contig, explain_one at level 0; launch_full: the contigs of `list` (length *n_dev, on
+// the device), explain_two and the roll-up levels.
+hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                        hipStream_t s);
-int fast_blocks_per_cu();
+hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
+                       const int64_t* n_dev, int max_hits, int cus, hipStream_t s);
 StagedState* staged_create(int device);
 void staged_destroy(StagedState* st);
 void staged_set_lds(StagedState* st, int64_t bytes);
 void staged_set_level0(StagedState* st, bool on);   // fused level 0 (wf_fast.hip) first
 // Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2 with
 // the message in *err (-1 bad input, -2 HIP failure).
-int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t n_hits,
+int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t n_hits,
                  int64_t n_loci, hipStream_t s, std::string* err, DetailsSink* det = nullptr);
 
 }  // namespace wf

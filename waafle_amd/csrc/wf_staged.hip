@@ -600,7 +600,7 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
       }
     }
     if (one_run) {
-      S.seg_mean[s] = one_run_mean(S.lut + S.lut_off[si.len], nl, si.len, lo, hi, v);
+      S.seg_mean[s] = one_run_mean(PtrLut{S.lut + S.lut_off[si.len]}, nl, si.len, lo, hi, v);
       nl = 0;
     } else {
       S.seg_rec[s] = make_int4(si.kb, na, si.len, nl);
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(64) void k_seg_wave(const SArgs S) {
       const int2 x = S.satt_lohi[rec.x + lane];
       if (x.x < x.y) { lo = x.x; hi = x.y; sc = S.satt_sc[rec.x + lane]; }
     }
-    const double m = wave_seg_mean(S.lut + S.lut_off[rec.z], rec.w, rec.z, lo, hi, sc, W);
+    const double m = wave_seg_mean(PtrLut{S.lut + S.lut_off[rec.z]}, rec.w, rec.z, lo, hi, sc, W);
     if (lane == 0) S.seg_mean[s] = m;
   }
 }
@@ -1536,7 +1536,7 @@ static hipError_t details_level(StagedState* st, const SArgs& sa, int level, int
 }
 
 
-int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64_t NH, int64_t NL,
+int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t NH, int64_t NL,
                  hipStream_t s, std::string* err, DetailsSink* det) {
   const int N = k.n_contigs;
   if (N <= 0) return 0;
@@ -1582,9 +1582,24 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int64
   if (level0) {
     ST_TRY(st->pend.ensure(s, (size_t)N * 4));
     ST_TRY(st->act0.ensure(s, (size_t)N * 4));
-    const unsigned fgrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * fast_blocks_per_cu());
-    ST_TRY(launch_fast(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), fgrid,
-                       s));
+    ST_TRY(launch_fast(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
+                       st->cus, s));
+    // the contigs it handed over (explain_two, roll-up) through the second wave form, its
+    // list and count built on the device (WF_FULL=0: straight to the staged kernels)
+    static const char* full_env = getenv("WF_FULL");
+    if (!(full_env && full_env[0] == '0')) {
+      size_t ts = 0;
+      ST_TRY(hipcub::DeviceSelect::Flagged(nullptr, ts, hipcub::CountingInputIterator<int32_t>(0),
+                                           st->pend.as<int32_t>(), st->act0.as<int32_t>(),
+                                           st->red.as<int64_t>() + 3, N, s));
+      ST_TRY(st->tmp.ensure(s, ts));
+      ts = st->tmp.n;
+      ST_TRY(hipcub::DeviceSelect::Flagged(st->tmp.p, ts, hipcub::CountingInputIterator<int32_t>(0),
+                                           st->pend.as<int32_t>(), st->act0.as<int32_t>(),
+                                           st->red.as<int64_t>() + 3, N, s));
+      ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
+                         st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, s));
+    }
   } else {
     hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
                        st->cnt_leaves.as<int64_t>(),

@@ -130,11 +130,13 @@ class WaafleHipError(RuntimeError):
         return (type(self), (self.code, self.msg), {"contigs": getattr(self, "contigs", ())})
 
 
-def load(path=LIB_PATH):
+def load(path=None):
     """Load the in-tree HIP library (raises if it is absent -- no fallback)."""
     global _lib
     if _lib is not None:
         return _lib
+    # WAAFLE_HIP_LIB: a diagnostic build variant (python -m waafle_amd.build --variant=...)
+    path = path or os.environ.get("WAAFLE_HIP_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise ImportError("{} not built: run `python -m waafle_amd.build` "
                           "(the MI355X path has no CPU fallback)".format(path))
