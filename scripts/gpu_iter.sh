@@ -1,11 +1,17 @@
 # Iteration loop on the GPU box: GPU parity tests, then a cfg4 bench line (no CPU legs)
-# under a kernel trace.  OUT names gpurun_out/<OUT>; TESTS selects the pytest target.
+# and the same under a kernel trace.  OUT names gpurun_out/<OUT>; TESTS selects the pytest
+# target (empty: skip the tests).
 set -u
 O=gpurun_out/${OUT:-iter}; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "pytest failed"; tail -40 $O/gpu_tests.log; exit 1; }
-tail -2 $O/gpu_tests.log
-timeout -k 10 300 python3 bench.py --cpu-sample 0 --e2e= --pcie 0 > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
+if [ -n "${TESTS-tests}" ]; then
+  echo "tests start $(date +%T)"
+  timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "pytest failed"; tail -40 $O/gpu_tests.log; exit 1; }
+  tail -2 $O/gpu_tests.log
+fi
+echo "bench start $(date +%T)"
+timeout -k 10 300 python3 bench.py --cpu-sample 0 --e2e= --pcie 0 ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --cpu-sample 0 --e2e= --pcie 0 --steps 3 --warmup 1 > $O/bench_prof.json 2> $O/prof.err || { echo "prof failed"; tail -20 $O/prof.err; exit 1; }
-echo done
+echo "prof start $(date +%T)"
+timeout -k 10 170 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --cpu-sample 0 --e2e= --pcie 0 --steps 3 --warmup 1 ${BENCH_ARGS:-} > $O/bench_prof.json 2> $O/prof.err || { echo "prof failed"; tail -20 $O/prof.err; exit 1; }
+echo "done $(date +%T)"

@@ -38,47 +38,51 @@ namespace {
 
 constexpr int kSlotBits = 9;         // key = clade << 15 | locus << 9 | attachment slot
 constexpr int kCladeShift = 15;
-constexpr uint64_t kSlotMask = (1u << kSlotBits) - 1;
+constexpr uint32_t kSlotMask = (1u << kSlotBits) - 1;
 constexpr int kLoc0 = 64;            // loci per contig (locus bitmasks are 64-bit)
 constexpr int kLut0 = 256;           // packed leaf-table entries of the contig's loci
 constexpr int kAnn0 = 64;            // (locus, system) annotation slots
 constexpr int kRuns0 = 64;           // envelope runs of a multi-attachment segment ...
 constexpr int kMultiAtt0 = 32;       // ... so at most 32 attachments (2 * 32 - 1 runs)
-constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two
+constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two ...
+constexpr int kS0 = 1024;            // ... and their score rows (potential clades x loci)
 
 // One wave's LDS slice.  `scr` is reused phase by phase (offsets in the accessors):
-//   attachments:  hit[CAP] | sm[CAP]                         (annotation pass 2)
-//   means:        v[CAP] | runs                              (multi-run segments)
-//   explain_one:  v | rank[CAP] (FULL; else in sc) | mem[CAP]
-//   explain_two:  v | cl[CAP] | sib[CAP] | hm[CAP] | S[CAP] | masks, loci lists (FULL only)
-// key, lohi and sc (by slot) live across roll-up levels.
+//   attachments:  hit[CAP] | sm[CAP] | abest[64] | ahit[64]      (annotations)
+//   means:        v[CAP] | runs                                  (multi-run segments)
+//   explain_one:  v | rank[CAP] (FULL; else in sc) | mem[CAP] | mx[64]
+//   explain_two:  v | cl[CAP] | sib[CAP] | hm[CAP] | S[kS0] | masks, loci lists (FULL only)
+// key, lohi and sc (by attachment slot) live across roll-up levels.  Keys are 32-bit:
+// clade << 15 | locus << 9 | slot (clade ids < 2^17, checked on the host).
 template <int CAP, bool FULL>
 struct WaveSmem {
-  static constexpr int kScr = FULL ? 32 * CAP + 2048 : 8 * CAP + (4 * CAP > 1792 ? 4 * CAP : 1792);
-  uint64_t key[CAP];                 // keys by slot, then in sorted order
-  int2 lohi[CAP];                    // by slot: site range [lo, hi)
+  static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int kScr = FULL ? 24 * CAP + 8 * kS0 + 2048
+                                   : cmax(cmax(8 * CAP + 768, 8 * CAP + (int)sizeof(WaveRunsT<kRuns0>)), 12 * CAP + 512);
+  uint32_t key[CAP];                 // keys by slot, then in sorted order
+  uint32_t lohi[CAP];                // by slot: site range lo | hi << 16
   double sc[CAP];                    // by slot: score
-  uint16_t seg[CAP + 2];             // segment starts (sorted positions)
+  uint32_t seg[CAP + 2];             // per segment: its head key, slot field = first sorted position
   uint32_t lut[kLut0];               // packed leaf tables, locus g at lbase[g]
   int lo[kLoc0], len[kLoc0];
   int16_t lbase[kLoc0], nl1[kLoc0];
   int8_t st[kLoc0];
-  unsigned long long mx[kLoc0];      // per-locus max score bits over known clades
-  unsigned long long abest[kAnn0];
-  int ahit[kAnn0];
   alignas(16) char scr[kScr];
   __device__ int* hit() { return reinterpret_cast<int*>(scr); }
   __device__ int* sm() { return reinterpret_cast<int*>(scr) + CAP; }
+  __device__ unsigned long long* abest() { return reinterpret_cast<unsigned long long*>(scr + 8 * CAP); }
+  __device__ int* ahit() { return reinterpret_cast<int*>(scr + 8 * CAP + 8 * kAnn0); }
   __device__ double* v() { return reinterpret_cast<double*>(scr); }
   __device__ WaveRunsT<kRuns0>& runs() { return *reinterpret_cast<WaveRunsT<kRuns0>*>(scr + 8 * CAP); }
   __device__ double* rank() { return FULL ? reinterpret_cast<double*>(scr + 8 * CAP) : sc; }
   __device__ int* mem() { return reinterpret_cast<int*>(scr + (FULL ? 16 : 8) * CAP); }
+  __device__ unsigned long long* mx() { return reinterpret_cast<unsigned long long*>(scr + (FULL ? 20 : 12) * CAP); }
   __device__ int* cl() { return reinterpret_cast<int*>(scr + 8 * CAP); }
   __device__ int* sib() { return reinterpret_cast<int*>(scr + 12 * CAP); }
   __device__ uint64_t* hm() { return reinterpret_cast<uint64_t*>(scr + 16 * CAP); }
   __device__ double* S() { return reinterpret_cast<double*>(scr + 24 * CAP); }
-  __device__ uint64_t* pmask() { return reinterpret_cast<uint64_t*>(scr + 32 * CAP); }   // [kPot0]
-  __device__ int* ign() { return reinterpret_cast<int*>(scr + 32 * CAP + 8 * kPot0); }  // [64]
+  __device__ uint64_t* pmask() { return reinterpret_cast<uint64_t*>(scr + 24 * CAP + 8 * kS0); }   // [kPot0]
+  __device__ int* ign() { return reinterpret_cast<int*>(scr + 24 * CAP + 8 * kS0 + 8 * kPot0); }  // [64]
   __device__ int* um() { return ign() + 64; }
   __device__ int* loc_len() { return ign() + 128; }
   __device__ uint8_t* best_syn() { return reinterpret_cast<uint8_t*>(ign() + 192); }    // [64]
@@ -109,72 +113,126 @@ __device__ __forceinline__ int wave_lca(const KArgs& K, int acc) {
   return acc;
 }
 
-// Ascending bitonic sort of N = 64 * R keys, element lane + 64 r in x[r].
-template <int R>
-__device__ __forceinline__ void wave_sort(uint64_t (&x)[R]) {
+// Ascending bitonic sort of N = 64 * R keys, element lane + 64 r in x[r].  The merge
+// size k is a runtime loop (the unrolled network of every R and key width would not fit
+// the instruction cache); the strides j inside it are static, so in-lane partners are
+// static register indices and lane partners static shuffles.
+template <int R, class T>
+__device__ __forceinline__ void wave_sort(T (&x)[R]) {
   const int lane = lane_id();
   constexpr int N = 64 * R;
-#pragma unroll
+#pragma unroll 1
   for (int k = 2; k <= N; k <<= 1) {
 #pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 64) {                                 // partner: same lane, element r ^ (j / 64)
-        const int jr = j >> 6;
+    for (int jr = R / 2; jr >= 1; jr >>= 1) {        // strides 64 * jr: same lane, element r ^ jr
+      if (64 * jr >= k) continue;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (r & jr) continue;
-          const int i = lane + 64 * r;
-          const bool asc = (i & k) == 0;
-          const uint64_t a = x[r], b = x[r | jr];
-          const bool sw = (a > b) == asc;
-          x[r] = sw ? b : a;
-          x[r | jr] = sw ? a : b;
-        }
-      } else {                                       // partner: lane ^ j
+      for (int r = 0; r < R; ++r) {
+        if (r & jr) continue;
+        const int i = lane + 64 * r;
+        const bool asc = (i & k) == 0;
+        const T a = x[r], b = x[r | jr];
+        const bool sw = (a > b) == asc;
+        x[r] = sw ? b : a;
+        x[r | jr] = sw ? a : b;
+      }
+    }
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int i = lane + 64 * r;
-          const uint64_t y = __shfl_xor(x[r], j, 64);
-          const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
-          x[r] = keep_min ? (y < x[r] ? y : x[r]) : (y > x[r] ? y : x[r]);
-        }
+    for (int j = 32; j >= 1; j >>= 1) {              // strides < 64: partner lane ^ j
+      if (j >= k) continue;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int i = lane + 64 * r;
+        const T y = __shfl_xor(x[r], j, 64);
+        const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+        x[r] = keep_min ? (y < x[r] ? y : x[r]) : (y > x[r] ? y : x[r]);
       }
     }
   }
 }
 
+// The slice's keys in sorted order (one network of 64 * R 32-bit keys).
 template <int R, class SM>
 __device__ __forceinline__ void sort_slice(SM& F, int n_att) {
   const int lane = lane_id();
-  uint64_t x[R];
+  uint32_t y[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int t = lane + 64 * r;
-    x[r] = t < n_att ? F.key[t] : ~0ull;
+    y[r] = t < n_att ? F.key[t] : ~0u;
   }
-  wave_sort<R>(x);
+  wave_sort<R>(y);
   wave_sync();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int t = lane + 64 * r;
-    if (t < n_att) F.key[t] = x[r];
+    if (t < n_att) F.key[t] = y[r];
   }
   wave_sync();
 }
 
+// Segment s: (clade, locus) and its sorted attachment range [seg_first(s), seg_first(s+1)).
 template <class SM>
 __device__ __forceinline__ int2 cg_of(SM& F, int s) {
-  const uint64_t k0 = F.key[F.seg[s]];
-  return make_int2((int)(k0 >> kCladeShift), (int)((k0 >> kSlotBits) & (kLoc0 - 1)));
+  const uint32_t w = F.seg[s];
+  return make_int2((int)(w >> kCladeShift), (int)((w >> kSlotBits) & (kLoc0 - 1)));
+}
+template <class SM>
+__device__ __forceinline__ int seg_first(SM& F, int s) { return (int)(F.seg[s] & kSlotMask); }
+__device__ __forceinline__ int lo16(uint32_t w) { return (int)(w & 0xFFFFu); }
+__device__ __forceinline__ int hi16(uint32_t w) { return (int)(w >> 16); }
+
+// Contig.score of the clade run starting at segment t (orgscorer.py:447-461): crit = min
+// and rank = np.mean over the Gu unmasked loci of the clade's row, whose entries are the
+// run's segment means and 0.0 elsewhere.  numpy's order (np_sum_seq): fewer than 8 values
+// are added in order from 0.0; else value u goes to accumulator u % 8 while u < Gu - Gu % 8,
+// the eight are combined as a tree and the rest added in order.  Scores are >= 0, so the
+// 0.0 entries change no partial sum and only the run's segments are visited.
+template <class SM>
+__device__ __forceinline__ void sparse_score(SM& F, const double* v, int t, int ns, int clade, uint64_t um,
+                                             int Gu, double& crit, double& rank) {
+  const int m8 = Gu < 8 ? 0 : Gu - (Gu & 7);
+  double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
+  double mn = 0.0;
+  int cnt = 0;
+  int q = t;
+  for (; q < ns; ++q) {                              // the accumulators (Gu >= 8)
+    const int2 cq = cg_of(F, q);
+    if (cq.x != clade) break;
+    if (!((um >> cq.y) & 1ull)) continue;
+    const double x = v[q];
+    mn = (cnt == 0 || x < mn) ? x : mn;
+    ++cnt;
+    const int u = __popcll(um & ((1ull << cq.y) - 1ull));
+    if (u >= m8) continue;
+    const int a = u & 7;
+    r0 = a == 0 ? r0 + x : r0; r1 = a == 1 ? r1 + x : r1;
+    r2 = a == 2 ? r2 + x : r2; r3 = a == 3 ? r3 + x : r3;
+    r4 = a == 4 ? r4 + x : r4; r5 = a == 5 ? r5 + x : r5;
+    r6 = a == 6 ? r6 + x : r6; r7 = a == 7 ? r7 + x : r7;
+  }
+  double res = m8 > 0 ? leaf_tree(r0, r1, r2, r3, r4, r5, r6, r7) : 0.0;
+  for (int p = t; p < q; ++p) {                      // the rest, in order
+    const int2 cp = cg_of(F, p);
+    if (!((um >> cp.y) & 1ull)) continue;
+    if (__popcll(um & ((1ull << cp.y) - 1ull)) >= m8) res += v[p];
+  }
+  crit = cnt < Gu ? 0.0 : mn;
+  rank = (0.0 + res) / (double)Gu;
 }
 
 // explain_two + LGT filters + meld_two for one level in the slice (decide_two's arithmetic,
 // orgscorer.py:599-619, 633-744; eval_two / pair_rank / pair_crit of wf_device.h on a
 // Contig whose rows are the potential clades first, then the others).  Returns kDecDone
 // (written), kDecStop, kDecRaise, or -1 when the state does not fit (staged path).
+__device__ __noinline__ OptEval eval_two_call(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
+                                              const uint8_t* best, uint8_t* out) {
+  return eval_two(K, C, Pcount, pa, pb, best, out);
+}
+
 template <int CAP>
-__device__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int c, int64_t h0, int64_t l0, int G, int ns,
-                        uint64_t um, int Gu, int iteration, int64_t& pair_evals) {
+__device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int c, int64_t h0, int64_t l0, int G,
+                                     int ns, uint64_t um, int Gu, int iteration, int64_t& pair_evals) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const int lane = lane_id();
@@ -221,7 +279,7 @@ __device__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int c, int64_t h
   }
   root = __ballot(root) != 0ull;
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
-  if (Pp > kPot0 || Pp * G > CAP || Pn > CAP) return -1;
+  if (Pp > kPot0 || Pp * G > kS0 || Pn > CAP) return -1;
   // pass B: rows (potential clades first, clade order), S rows, sister data
   double* Sm = F.S();
   for (int i = lane; i < Pp * G; i += 64) Sm[i] = 0.0;
@@ -307,7 +365,7 @@ __device__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int c, int64_t h
     int b_ok = 0, b_dir = 0, b_c1p = 0, b_c2p = 0;
     double bcrit = 0.0;
     if (lane == 0) {
-      const OptEval e = eval_two(K, C, Pn, bi, bj, nullptr, F.best_syn());
+      const OptEval e = eval_two_call(K, C, Pn, bi, bj, nullptr, F.best_syn());
       b_ok = e.ok; b_dir = e.dir; b_c1p = e.c1p; b_c2p = e.c2p;
       bcrit = pair_crit(C, bi, bj, Gu);
     }
@@ -325,7 +383,7 @@ __device__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int c, int64_t h
         if ((mi | pmask[j]) != full) continue;
         const double r = pair_rank(C, i, j, Gu);
         if (!((br - r) <= P.range)) continue;
-        const OptEval e = eval_two(K, C, Pn, i, j, F.best_syn(), nullptr);
+        const OptEval e = eval_two_call(K, C, Pn, i, j, F.best_syn(), nullptr);
         ++n_in;
         all_ok = all_ok && e.ok;
         all_same = all_same && e.same;
@@ -410,7 +468,6 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
     const int G = (int)(K.loc_off[c + 1] - l0);
     const int Gs = min(G, kLoc0);
     // ---- loci (lane g), leaf-table bases ----
-    F.mx[lane] = 0ull;
     int nl1 = 0;
     if (lane < Gs) {
       const int a = K.lstart[l0 + lane], b = K.lend[l0 + lane];
@@ -425,14 +482,17 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
     const int lb = wave_excl_scan(nl1, &lut_total);
     F.lbase[lane] = (int16_t)min(lb, 32767);
     const int nann = Gs * nsys;
-    F.abest[lane] = 0ull;
-    F.ahit[lane] = -1;
-    bool staged = G > kLoc0 || lut_total > kLut0 || nann > kAnn0;
+    F.abest()[lane] = 0ull;
+    F.ahit()[lane] = -1;
+    const bool long_locus = __ballot(lane < Gs && F.len[lane] > 65535) != 0ull;   // lohi is 16-bit
+    bool staged = G > kLoc0 || lut_total > kLut0 || nann > kAnn0 || long_locus;
     wave_sync();
-    if (!staged)                                     // packed leaf tables of the contig's lengths
-      for (int g = 0; g < G; ++g) {
-        const int len = F.len[g], n = F.nl1[g];
-        for (int j = lane; j < n; j += 64) F.lut[F.lbase[g] + j] = pack_leaf(S.lut[S.lut_off[len] + j]);
+    if (!staged)                                     // packed leaf tables: one flat batch of loads
+      for (int i = lane; i < lut_total; i += 64) {
+        int g = 0;                                   // last locus whose table starts at or before i
+        for (int b = 32; b > 0; b >>= 1)
+          if (g + b < Gs && F.lbase[g + b] <= i) g += b;
+        F.lut[i] = pack_leaf(S.lut[S.lut_off[F.len[g]] + (i - F.lbase[g])]);
       }
 
     // ---- hits -> attachments, in (hit, locus) order (orgscorer.py:359-382) ----
@@ -484,14 +544,14 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
           const int start = min(h1s, len);
           int stop = h2s + 1;                        // site[h1:h2+1], python slice rules
           if (stop < 0) { stop += len; if (stop < 0) stop = 0; }
-          F.key[slot] = ((uint64_t)(uint32_t)clade << kCladeShift) | ((uint64_t)g << kSlotBits) | (uint64_t)slot;
-          F.lohi[slot] = make_int2(start, stop);
+          F.key[slot] = ((uint32_t)clade << kCladeShift) | ((uint32_t)g << kSlotBits) | (uint32_t)slot;
+          F.lohi[slot] = (uint32_t)start | ((uint32_t)stop << 16);
           F.sc[slot] = sc;
           F.hit()[slot] = (int)h;
           F.sm()[slot] = (int)m;
           if (ann)                                   // annotation pass 1: best score bits (:383-392)
             for (int b = 0; b < nsys; ++b)
-              if ((m >> b) & 1u) atomicMax(&F.abest[g * nsys + b], dbits(sc));
+              if ((m >> b) & 1u) atomicMax(&F.abest()[g * nsys + b], dbits(sc));
         }
       }
       n_att += total;
@@ -509,10 +569,10 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
         const int g = (int)((F.key[t] >> kSlotBits) & (kLoc0 - 1));
         const int h = F.hit()[t];
         for (int b = 0; b < nsys; ++b)
-          if (((m >> b) & 1u) && F.abest[g * nsys + b] == dbits(sc)) atomicMax(&F.ahit[g * nsys + b], h);
+          if (((m >> b) & 1u) && F.abest()[g * nsys + b] == dbits(sc)) atomicMax(&F.ahit()[g * nsys + b], h);
       }
       wave_sync();
-      if (lane < nann) K.annot[l0 * nsys + lane] = F.ahit[lane];
+      if (lane < nann) K.annot[l0 * nsys + lane] = F.ahit()[lane];
     }
     // ---- levels: sort, segments, means, explain_one [, explain_two, roll-up] ----
     int64_t pair_evals = 0;
@@ -520,27 +580,23 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
       const int iteration = level + 1;
       if (level > 0) {                               // roll up (:431-445): re-key to the parent clade
         for (int t = lane; t < n_att; t += 64) {
-          const uint64_t k0 = F.key[t];
+          const uint32_t k0 = F.key[t];
           const int parent = K.parent[(int)(k0 >> kCladeShift)];
-          F.key[t] = ((uint64_t)(uint32_t)parent << kCladeShift) | (k0 & ((1ull << kCladeShift) - 1));
+          F.key[t] = ((uint32_t)parent << kCladeShift) | (k0 & ((1u << kCladeShift) - 1));
         }
         wave_sync();
       }
-      if (WF_SKIP & 2) {
-      } else if (n_att <= 64) sort_slice<1>(F, n_att);
-      else if (n_att <= 128) sort_slice<2>(F, n_att);
-      else if (CAP <= 256 || n_att <= 256) sort_slice<4>(F, n_att);
-      else sort_slice<CAP / 64>(F, n_att);
+      if (!(WF_SKIP & 2)) sort_slice<CAP / 64>(F, n_att);   // one network: code size
       // ---- segments = runs of equal (clade, locus) ----
       int ns = 0;
       for (int t0 = 0; t0 < n_att; t0 += 64) {
         const int t = t0 + lane;
         const bool head = t < n_att && (t == 0 || (F.key[t] >> kSlotBits) != (F.key[t - 1] >> kSlotBits));
         const uint64_t hm = __ballot(head);
-        if (head) F.seg[ns + __popcll(hm & lanes_below())] = (uint16_t)t;
+        if (head) F.seg[ns + __popcll(hm & lanes_below())] = (F.key[t] & ~kSlotMask) | (uint32_t)t;
         ns += __popcll(hm);
       }
-      if (lane == 0) F.seg[ns] = (uint16_t)n_att;
+      if (lane == 0) F.seg[ns] = (uint32_t)n_att;    // end of the last segment (n_att <= CAP)
       wave_sync();
       // ---- segment means (numpy pairwise order, exact) ----
       double* v = F.v();
@@ -552,8 +608,8 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
         if (WF_SKIP & 1) {
           if (s < ns) v[s] = 0.75;
         } else if (s < ns) {
-          const int kb = F.seg[s], ke = F.seg[s + 1], na = ke - kb;
-          g = (int)((F.key[kb] >> kSlotBits) & (kLoc0 - 1));
+          const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att, na = ke - kb;
+          g = cg_of(F, s).y;
           len = F.len[g];
           nl = F.nl1[g];
           const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
@@ -563,22 +619,22 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
           if (na == 1) {
             if (thread_ok) {
               const int slot = (int)(F.key[kb] & kSlotMask);
-              lo = F.lohi[slot].x; hi = F.lohi[slot].y; vv = F.sc[slot];
+              lo = lo16(F.lohi[slot]); hi = hi16(F.lohi[slot]); vv = F.sc[slot];
               one_run = true;
             }
           } else if (na <= kPruneMax) {
             double Fw = 0.0;                           // best whole-locus attachment
             for (int t = kb; t < ke; ++t) {
               const int slot = (int)(F.key[t] & kSlotMask);
-              const int2 x = F.lohi[slot];
+              const uint32_t x = F.lohi[slot];
               const double sc = F.sc[slot];
-              if (x.x <= 0 && x.y >= len && sc > Fw) Fw = sc;
+              if (lo16(x) <= 0 && hi16(x) >= len && sc > Fw) Fw = sc;
             }
             int kept = 0;                              // attachments the envelope still needs
             for (int t = kb; t < ke; ++t) {
               const int slot = (int)(F.key[t] & kSlotMask);
-              const int2 x = F.lohi[slot];
-              kept += (x.x < x.y && F.sc[slot] > Fw) ? 1 : 0;
+              const uint32_t x = F.lohi[slot];
+              kept += (lo16(x) < hi16(x) && F.sc[slot] > Fw) ? 1 : 0;
             }
             if (kept == 0 && thread_ok) { lo = 0; hi = len; vv = Fw; one_run = true; }
           }
@@ -592,14 +648,14 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
         for (uint64_t mm = __ballot(multi); mm; mm &= mm - 1) {   // the wave, one segment each
           const int src = __builtin_ctzll(mm);
           const int s2 = s0 + src;
-          const int kb = F.seg[s2], na = F.seg[s2 + 1] - kb;
+          const int kb = seg_first(F, s2), na = (s2 + 1 < ns ? seg_first(F, s2 + 1) : n_att) - kb;
           const int g2 = __shfl(g, src, 64), len2 = __shfl(len, src, 64), nl2 = __shfl(nl, src, 64);
           int lo = 0, hi = 0;
           double sc = 0.0;
           if (lane < na) {
             const int slot = (int)(F.key[kb + lane] & kSlotMask);
-            const int2 x = F.lohi[slot];
-            if (x.x < x.y) { lo = x.x; hi = x.y; sc = F.sc[slot]; }
+            const uint32_t x = F.lohi[slot];
+            if (lo16(x) < hi16(x)) { lo = lo16(x); hi = hi16(x); sc = F.sc[slot]; }
           }
           const double mean = wave_seg_mean(PackedLut{F.lut + F.lbase[g2]}, nl2, len2, lo, hi, sc, F.runs());
           if (lane == 0) v[s2] = mean;
@@ -609,16 +665,16 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
       wave_sync();
       if (staged || (WF_SKIP & 4)) break;
       // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
-      if (FULL) F.mx[lane] = 0ull;
+      F.mx()[lane] = 0ull;
       wave_sync();
       for (int s = lane; s < ns; s += 64) {            // per-locus max over known clades
         const int2 cg = cg_of(F, s);
         const double x = v[s];
-        if (cg.x != K.unknown && x > 0.0) atomicMax(&F.mx[cg.y], dbits(x));
+        if (cg.x != K.unknown && x > 0.0) atomicMax(&F.mx()[cg.y], dbits(x));
       }
       wave_sync();
       // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
-      const double mxl = __longlong_as_double((long long)F.mx[lane]);
+      const double mxl = __longlong_as_double((long long)F.mx()[lane]);
       const uint64_t um = __ballot(lane < G && (P.weak != 0 || mxl >= P.kmin));
       const int Gu = __popcll(um);
       if (Gu == 0) {                                   // level 0: skipped contig (:959)
@@ -636,24 +692,8 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
         double rk = -1.0;
         const int clade = cg_of(F, t).x;
         if (t == 0 || cg_of(F, t - 1).x != clade) {
-          uint64_t mq = um;
-          int q = t;
-          int2 cq = cg_of(F, q);
-          double crit = 0.0;
-          bool firstv = true;
-          auto next = [&]() -> double {
-            const int gg = __builtin_ctzll(mq);
-            mq &= mq - 1;
-            while (q < ns && cq.x == clade && cq.y < gg) {
-              ++q;
-              if (q < ns) cq = cg_of(F, q);
-            }
-            const double x = (q < ns && cq.x == clade && cq.y == gg) ? v[q] : 0.0;
-            crit = (firstv || x < crit) ? x : crit;
-            firstv = false;
-            return x;
-          };
-          const double rnk = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+          double crit, rnk;
+          sparse_score(F, v, t, ns, clade, um, Gu, crit, rnk);
           if (crit >= P.k1) {
             rk = rnk;
             if (better(rnk, clade, br, bk)) { br = rnk; bk = clade; bcrit = crit; }

@@ -1576,8 +1576,9 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   // Fused level 0 (wf_fast.hip) unless --write-details (per-level records of every contig),
   // --weak-loci assign-unknown (virtual "Unknown" row) or HBM annotation slots are needed.
   static const char* l0_env = getenv("WF_LEVEL0");          // 0: staged only (measurement aid)
+  // (the wave kernels' 32-bit keys hold clade ids below 2^17)
   const bool level0 = st->level0 && !det && k.p.weak != 2 && (int64_t)max_loci * k.n_sys <= kAnnSlots &&
-                      !(l0_env && l0_env[0] == '0');
+                      sa.key_tb <= 17 && !(l0_env && l0_env[0] == '0');
   hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, sa.k);
   if (level0) {
     ST_TRY(st->pend.ensure(s, (size_t)N * 4));
