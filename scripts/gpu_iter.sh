@@ -4,6 +4,9 @@
 set -u
 O=gpurun_out/${OUT:-iter}; mkdir -p $O
 export TMPDIR=/tmp
+# heartbeat: a long profiled run prints nothing until it ends
+(while sleep 45; do echo "heartbeat $(date +%T)"; done) & HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 if [ -n "${TESTS-tests}" ]; then
   echo "tests start $(date +%T)"
   timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "pytest failed"; tail -40 $O/gpu_tests.log; exit 1; }

@@ -4,6 +4,9 @@
 set -u
 O=gpurun_out/${OUT:-pmcf}; mkdir -p $O
 export TMPDIR=/tmp
+# heartbeat: a long profiled run prints nothing until it ends
+(while sleep 45; do echo "heartbeat $(date +%T)"; done) & HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 B="python3 bench.py --cpu-sample 0 --e2e= --pcie 0 --contigs ${NC:-200000} --steps 1 --warmup 0"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \

@@ -26,7 +26,8 @@
 #include "wf_device.h"
 
 // WF_SKIP (diagnostic variants only, never the product build): 1 skips the segment means,
-// 2 the sort, 4 explain_one, 8 everything after the attachments -- per-phase cost by
+// 2 the sort, 4 explain_one, 8 everything after the attachments, 16 explain_two (FULL),
+// 32 the roll-up (FULL) -- per-phase cost by
 // difference of kernel times (no contig is handed on, the results are not meaningful).
 #ifndef WF_SKIP
 #define WF_SKIP 0
@@ -49,7 +50,8 @@ constexpr int kS0 = 1024;            // ... and their score rows (potential clad
 
 // One wave's LDS slice.  `scr` is reused phase by phase (offsets in the accessors):
 //   attachments:  hit[CAP] | sm[CAP] | abest[64] | ahit[64]      (annotations)
-//   means:        v[CAP] | runs                                  (multi-run segments)
+//   means:        v[CAP] | runs | list[CAP] | rc[CAP]            (multi-run segments; the
+//                 level-0 pruning: segments to evaluate, clade-run sizes -- !FULL only)
 //   explain_one:  v | rank[CAP] (FULL; else in sc) | mem[CAP] | mx[64]
 //   explain_two:  v | cl[CAP] | sib[CAP] | hm[CAP] | S[kS0] | masks, loci lists (FULL only)
 // key, lohi and sc (by attachment slot) live across roll-up levels.  Keys are 32-bit:
@@ -57,8 +59,9 @@ constexpr int kS0 = 1024;            // ... and their score rows (potential clad
 template <int CAP, bool FULL>
 struct WaveSmem {
   static constexpr int cmax(int a, int b) { return a > b ? a : b; }
+  static constexpr int kRunsB = (int)sizeof(WaveRunsT<kRuns0>);
   static constexpr int kScr = FULL ? 24 * CAP + 8 * kS0 + 2048
-                                   : cmax(cmax(8 * CAP + 768, 8 * CAP + (int)sizeof(WaveRunsT<kRuns0>)), 12 * CAP + 512);
+                                   : cmax(cmax(8 * CAP + 768, 8 * CAP + kRunsB + 3 * CAP), 12 * CAP + 512);
   uint32_t key[CAP];                 // keys by slot, then in sorted order
   uint32_t lohi[CAP];                // by slot: site range lo | hi << 16
   double sc[CAP];                    // by slot: score
@@ -74,6 +77,8 @@ struct WaveSmem {
   __device__ int* ahit() { return reinterpret_cast<int*>(scr + 8 * CAP + 8 * kAnn0); }
   __device__ double* v() { return reinterpret_cast<double*>(scr); }
   __device__ WaveRunsT<kRuns0>& runs() { return *reinterpret_cast<WaveRunsT<kRuns0>*>(scr + 8 * CAP); }
+  __device__ uint16_t* list() { return reinterpret_cast<uint16_t*>(scr + 8 * CAP + kRunsB); }       // !FULL
+  __device__ uint8_t* rc() { return reinterpret_cast<uint8_t*>(scr + 8 * CAP + kRunsB + 2 * CAP); }  // !FULL
   __device__ double* rank() { return FULL ? reinterpret_cast<double*>(scr + 8 * CAP) : sc; }
   __device__ int* mem() { return reinterpret_cast<int*>(scr + (FULL ? 16 : 8) * CAP); }
   __device__ unsigned long long* mx() { return reinterpret_cast<unsigned long long*>(scr + (FULL ? 20 : 12) * CAP); }
@@ -181,6 +186,35 @@ template <class SM>
 __device__ __forceinline__ int seg_first(SM& F, int s) { return (int)(F.seg[s] & kSlotMask); }
 __device__ __forceinline__ int lo16(uint32_t w) { return (int)(w & 0xFFFFu); }
 __device__ __forceinline__ int hi16(uint32_t w) { return (int)(w >> 16); }
+
+// The slice's attachments for SegAttT (wf_device.h): sorted position -> slot -> range, score.
+struct SliceSrc {
+  const uint32_t* key;
+  const uint32_t* lohi;
+  const double* sc;
+  __device__ __forceinline__ int idx(int t) const { return (int)(key[t] & kSlotMask); }
+  __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
+    const uint32_t w = lohi[a];
+    l = lo16(w); h = hi16(w); v = sc[a];
+  }
+};
+
+// Exact mean of one segment (sorted attachments [kb, ke), any count) by one lane: every
+// numpy leaf by SegAttT::leaf (closed forms, else the envelope's runs), folded in tree
+// order on a register stack.  For the roll-up levels, where many segments per block have
+// several attachments and one lane each beats one wave each.
+template <class LT>
+__device__ __noinline__ double lane_seg_mean(SliceSrc src, int kb, int ke, LT lt, int nl, int len) {
+  SegAttT<SliceSrc> at;
+  at.load(src, kb, ke);
+  SumStack stk;
+  for (int q = 0; q < nl; ++q) {
+    const int4 e = lt(q);
+    stk.push(at.leaf(src, e.x, e.y));
+    for (int a = 0; a < e.z; ++a) stk.add_top();
+  }
+  return (0.0 + stk.s0) / (double)len;
+}
 
 // Contig.score of the clade run starting at segment t (orgscorer.py:447-461): crit = min
 // and rank = np.mean over the Gu unmasked loci of the clade's row, whose entries are the
@@ -452,7 +486,7 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
 }
 
 template <int CAP, bool FULL>
-__global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
+__global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
                                              const int32_t* list, int n_list, const int64_t* n_dev) {
   if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
   const KArgs& K = S.k;
@@ -601,9 +635,86 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
       // ---- segment means (numpy pairwise order, exact) ----
       double* v = F.v();
       bool fail = false;
-      for (int s0 = 0; s0 < ns; s0 += 64) {
-        const int s = s0 + lane;
-        bool multi = false;
+      // Level 0 of the first form evaluates only what explain_one can use (exact, k1 > 0):
+      // an option has crit >= k1 > 0, so a segment on every unmasked locus; the weak-locus
+      // mask needs, per locus, one known clade's mean >= kmin, or proof that none reaches
+      // it -- a segment's mean is at most its best attachment score (times 1 + 2e-15 for
+      // the rounded sum), so segments scoring below kmin * (1 - 1e-12) are never evaluated.
+      // Passes: 0 clades on every locus, 1 segments that may settle an open locus, 2 clades
+      // on every unmasked locus; 3 (not pruned) every segment.
+      const bool prune = !FULL && P.k1 > 0.0 && !(WF_SKIP & 1);
+      const uint64_t allG = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+      uint64_t um = 0;
+      uint8_t* rc = F.rc();                            // pruned: per segment, its clade run's size
+      // segments of the clade run starting at t that lie on loci of `mask`
+      auto run_count = [&](int t, uint64_t mask) -> int {
+        const int clade = cg_of(F, t).x;
+        int cnt = 0;
+        for (int q = t; q < ns; ++q) {
+          const int2 cq = cg_of(F, q);
+          if (cq.x != clade) break;
+          cnt += (int)((mask >> cq.y) & 1ull);
+        }
+        return cnt;
+      };
+      // per-locus bits of evaluated known-clade segments with mean >= kmin
+      auto sure_bits = [&]() -> uint64_t {
+        uint64_t b = 0;
+        for (int t = lane; t < ns; t += 64) {
+          const int2 cg = cg_of(F, t);
+          if (cg.x != K.unknown && v[t] >= 0.0 && v[t] >= P.kmin) b |= 1ull << cg.y;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off, 64);
+        return b;
+      };
+      if (prune) {
+        for (int t = lane; t < ns; t += 64) {
+          v[t] = -1.0;                                 // not evaluated
+          if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
+            const int cnt = run_count(t, ~0ull);
+            for (int q = t; q < t + cnt; ++q) rc[q] = (uint8_t)cnt;
+          }
+        }
+        wave_sync();
+      }
+      const double bound = P.kmin * (1.0 - 1e-12);
+      uint64_t open = 0;
+      for (int pass = prune ? 0 : 3; pass <= 3;) {
+      int n = ns;
+      const uint16_t* list = nullptr;
+      if (pass < 3) {                                  // compact this pass's segments
+        uint16_t* lst = F.list();
+        const int gu = __popcll(um);
+        n = 0;
+        for (int t0 = 0; t0 < ns; t0 += 64) {
+          const int t = t0 + lane;
+          bool in = false;
+          if (t < ns) {
+            const int2 cg = cg_of(F, t);
+            if (pass == 0) {
+              in = (int)rc[t] == G;
+            } else if (pass == 1) {
+              if (v[t] < 0.0 && cg.x != K.unknown && ((open >> cg.y) & 1ull)) {
+                const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
+                double ub = 0.0;
+                for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[F.key[q] & kSlotMask]);
+                in = ub >= bound;
+              }
+            } else {
+              in = v[t] < 0.0 && ((um >> cg.y) & 1ull) && (int)rc[t] == gu;
+            }
+          }
+          const uint64_t im = __ballot(in);
+          if (in) lst[n + __popcll(im & lanes_below())] = (uint16_t)t;
+          n += __popcll(im);
+        }
+        wave_sync();
+        list = lst;
+      }
+      for (int s0 = 0; s0 < n; s0 += 64) {
+        const int s = s0 + lane < n ? (list ? (int)list[s0 + lane] : s0 + lane) : ns;
+        bool multi = false, big = false;               // big: too many attachments for the wave path
         int g = 0, len = 0, nl = 0;
         if (WF_SKIP & 1) {
           if (s < ns) v[s] = 0.75;
@@ -640,14 +751,25 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
           }
           if (one_run)
             v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
-          else if (na <= kMultiAtt0 && nl <= 64 && len < kNpyBuf)
+          else if ((FULL || na <= kMultiAtt0) && nl <= 64 && len < kNpyBuf) {
             multi = true;
+            big = na > kMultiAtt0;
+          }
           else
             fail = true;                               // the staged leaf kernels take it
         }
-        for (uint64_t mm = __ballot(multi); mm; mm &= mm - 1) {   // the wave, one segment each
+        uint64_t mlist = __ballot(multi);
+        if (FULL && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
+          // several multi-attachment segments (roll-up levels): one lane each
+          if (multi) {
+            const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
+            v[s] = lane_seg_mean(SliceSrc{F.key, F.lohi, F.sc}, kb, ke, PackedLut{F.lut + F.lbase[g]}, nl, len);
+          }
+          mlist = 0;
+        }
+        for (uint64_t mm = mlist; mm; mm &= mm - 1) {  // the wave, one segment each
           const int src = __builtin_ctzll(mm);
-          const int s2 = s0 + src;
+          const int s2 = __shfl(s, src, 64);
           const int kb = seg_first(F, s2), na = (s2 + 1 < ns ? seg_first(F, s2 + 1) : n_att) - kb;
           const int g2 = __shfl(g, src, 64), len2 = __shfl(len, src, 64), nl2 = __shfl(nl, src, 64);
           int lo = 0, hi = 0;
@@ -661,21 +783,51 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
           if (lane == 0) v[s2] = mean;
         }
       }
+      wave_sync();
+      // after the pass: the weak-locus mask, the next pass
+      if (pass == 3) break;
+      if (pass == 0) {
+        if (P.weak != 0 || P.kmin <= 0.0) {
+          um = allG;                                   // penalize: no mask; kmin <= 0: nothing masked
+          break;                                       // (every locus unmasked: pass 0 covered the options)
+        }
+        um = sure_bits();
+        open = allG & ~um;                             // loci no full clade settles
+        pass = open ? 1 : 3;
+        if (!open) break;
+        continue;
+      }
+      if (pass == 1) {
+        um |= sure_bits();
+        if (um == allG || um == 0ull) break;
+        for (int t = lane; t < ns; t += 64)            // clade runs' sizes on the unmasked loci
+          if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
+            const int cnt = run_count(t, ~0ull), cu = run_count(t, um);
+            for (int q = t; q < t + cnt; ++q) rc[q] = (uint8_t)cu;
+          }
+        wave_sync();
+        pass = 2;
+        continue;
+      }
+      break;                                           // pass 2 done
+      }
       staged = __ballot(fail) != 0;
       wave_sync();
       if (staged || (WF_SKIP & 4)) break;
       // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
-      F.mx()[lane] = 0ull;
-      wave_sync();
-      for (int s = lane; s < ns; s += 64) {            // per-locus max over known clades
-        const int2 cg = cg_of(F, s);
-        const double x = v[s];
-        if (cg.x != K.unknown && x > 0.0) atomicMax(&F.mx()[cg.y], dbits(x));
+      if (!prune) {
+        F.mx()[lane] = 0ull;
+        wave_sync();
+        for (int s = lane; s < ns; s += 64) {          // per-locus max over known clades
+          const int2 cg = cg_of(F, s);
+          const double x = v[s];
+          if (cg.x != K.unknown && x > 0.0) atomicMax(&F.mx()[cg.y], dbits(x));
+        }
+        wave_sync();
+        // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
+        const double mxl = __longlong_as_double((long long)F.mx()[lane]);
+        um = __ballot(lane < G && (P.weak != 0 || mxl >= P.kmin));
       }
-      wave_sync();
-      // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
-      const double mxl = __longlong_as_double((long long)F.mx()[lane]);
-      const uint64_t um = __ballot(lane < G && (P.weak != 0 || mxl >= P.kmin));
       const int Gu = __popcll(um);
       if (Gu == 0) {                                   // level 0: skipped contig (:959)
         if (level > 0 && lane == 0) {                  // later: np.min of an empty array upstream
@@ -691,8 +843,8 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
       for (int t = lane; t < ns; t += 64) {
         double rk = -1.0;
         const int clade = cg_of(F, t).x;
-        if (t == 0 || cg_of(F, t - 1).x != clade) {
-          double crit, rnk;
+        if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || run_count(t, um) == Gu)) {
+          double crit, rnk;                            // (pruned: only runs on every unmasked locus)
           sparse_score(F, v, t, ns, clade, um, Gu, crit, rnk);
           if (crit >= P.k1) {
             rk = rnk;
@@ -751,7 +903,8 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
       }
       wave_sync();
       int dec = -1;
-      if constexpr (FULL) dec = wave_two(S, F, c, h0, l0, G, ns, um, Gu, iteration, pair_evals);
+      if constexpr (FULL) dec = (WF_SKIP & 16) ? kDecStop : wave_two(S, F, c, h0, l0, G, ns, um, Gu, iteration, pair_evals);
+      if ((WF_SKIP & 32) && dec == kDecRaise) dec = kDecStop;
       if (dec < 0) {
         staged = true;
         break;
@@ -768,7 +921,7 @@ __global__ __launch_bounds__(64) void k_wave(const SArgs S, int64_t* ccnt, int64
       }
       break;
     }
-    if (WF_SKIP) staged = false;                       // variants: time this kernel alone
+    if (WF_SKIP & 15) staged = false;                  // variants: time this kernel alone
     if (lane == 0) {
       ccnt[c] = staged ? n_att : 0;
       cleaves[c] = staged ? nl_sum : 0;
