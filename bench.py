@@ -136,8 +136,12 @@ def cpu_baseline(config, n_one, n_shard):
         import multiprocessing as mp
         shards = [(i * n_shard, (i + 1) * n_shard) for i in range(P)]
         t0 = time.perf_counter()
-        with mp.get_context("fork").Pool(P) as pool:
+        pool = mp.get_context("fork").Pool(P)      # close + join (see synth.generate_batch)
+        try:
             secs = pool.starmap(_oracle_contigs, shards)
+        finally:
+            pool.close()
+            pool.join()
         wall = time.perf_counter() - t0
         out["parallel"] = {"value": P * n_shard / max(secs), "unit": "contigs/s", "cores": P,
                            "kind": "port", "slowest_shard_s": max(secs), "wall_s": wall,

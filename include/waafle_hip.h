@@ -39,13 +39,14 @@ enum wf_status {
 enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
 
 /* Execution form of wf_score (the results are identical).
- * WF_MODE_LEVEL0 (default): one workgroup per contig carries level 0 from hits to the
- *   explain_one decision in LDS; the contigs it cannot finish (explain_two, roll-up, over-
- *   size) continue in the staged kernels.
+ * WF_MODE_LEVEL0 (default): per-contig wave kernels carry level 0 (explain_one, then
+ *   explain_two) in LDS; contigs that roll up, or exceed a wave's LDS slice, continue in the
+ *   staged kernels.
+ * WF_MODE_WAVES: as LEVEL0, but the wave kernel also carries the roll-up levels.
  * WF_MODE_STAGED: every contig through the staged kernels (one kernel per phase over all
  *   contigs: attachments, per-contig sort, segment means, decisions; one pass per level).
  * The ABI-1 WF_MODE_FUSED form (1) stays retired; wf_set_mode rejects it. */
-enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2 };
+enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
 
 typedef struct wf_ctx wf_ctx;
 
@@ -256,7 +257,7 @@ void wf_free(wf_ctx* ctx);
 const char* wf_last_error(const wf_ctx* ctx);
 int wf_set_stream(wf_ctx* ctx, void* hip_stream);     /* NULL = the context's own stream */
 int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes);     /* decision arena per workgroup (LDS) */
-int wf_set_mode(wf_ctx* ctx, int mode);               /* WF_MODE_LEVEL0 (default) or WF_MODE_STAGED */
+int wf_set_mode(wf_ctx* ctx, int mode);               /* WF_MODE_LEVEL0 (default), _WAVES or _STAGED */
 int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* tax);
 int wf_score(wf_ctx* ctx, const wf_batch* batch, const wf_params* params, wf_result* out);
 int wf_synchronize(wf_ctx* ctx);

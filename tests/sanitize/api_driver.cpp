@@ -122,6 +122,7 @@ int main() {
   CHECK(wf_init(0, &ctx) == WF_OK);
   CHECK(wf_set_mode(ctx, 1) == WF_E_BADINPUT);
   CHECK(wf_set_mode(ctx, WF_MODE_STAGED) == WF_OK);
+  CHECK(wf_set_mode(ctx, WF_MODE_WAVES) == WF_OK);
   CHECK(wf_set_mode(ctx, WF_MODE_LEVEL0) == WF_OK);
   CHECK(wf_set_lds_bytes(ctx, 10) == WF_E_BADINPUT);
 

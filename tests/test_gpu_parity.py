@@ -25,10 +25,11 @@ FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n
           "n_meld2", "annot_hit", "pair_evals", "iterations", "status")
 
 
-@pytest.fixture(scope="module", params=["level0", "staged"])
+@pytest.fixture(scope="module", params=["level0", "waves", "staged"])
 def scorer(request):
-    """Both execution forms: the fused level-0 kernel with the staged kernels behind it
-    (default), and every contig through the staged kernels."""
+    """Every execution form: the level-0 wave kernels with the staged kernels behind them
+    (default), the wave kernels carrying the roll-up levels too, and every contig through
+    the staged kernels."""
     s = engine.GpuScorer(0, mode=request.param)
     yield s
     s.close()
@@ -220,7 +221,7 @@ def test_full_size_cfg2_properties(scorer):
     assert_same_results(a, b, batch)
     for kw in (dict(lds_bytes=8192),          # small decision arena: HBM decision slots
                dict(lds_bytes=65536),         # large arena: every contig in LDS
-               dict(mode="staged"), dict(mode="level0"),
+               dict(mode="staged"), dict(mode="level0"), dict(mode="waves"),
                dict()):
         small = engine.GpuScorer(0, **kw)
         small.set_taxonomy(tax)

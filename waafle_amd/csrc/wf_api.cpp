@@ -245,8 +245,8 @@ int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes) {
 
 int wf_set_mode(wf_ctx* ctx, int mode) {
   if (!ctx) return WF_E_BADINPUT;
-  if (mode != WF_MODE_STAGED && mode != WF_MODE_LEVEL0)
-    return fail(ctx, WF_E_BADINPUT, "mode must be WF_MODE_LEVEL0 (2) or WF_MODE_STAGED (0)");
+  if (mode != WF_MODE_STAGED && mode != WF_MODE_LEVEL0 && mode != WF_MODE_WAVES)
+    return fail(ctx, WF_E_BADINPUT, "mode must be WF_MODE_LEVEL0 (2), WF_MODE_WAVES (3) or WF_MODE_STAGED (0)");
   ctx->mode = mode;
   return WF_OK;
 }
@@ -348,7 +348,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   K.unknown = ctx->unknown;
   if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
   if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
-  wf::staged_set_level0(ctx->staged, ctx->mode == WF_MODE_LEVEL0);
+  wf::staged_set_level0(ctx->staged, ctx->mode != WF_MODE_STAGED, ctx->mode == WF_MODE_WAVES);
   std::pair<int, int> el{-1, -1};
   if (ctx->timing) {
     if (take_event_pair(ctx, ctx->ev_lds) < 0) return fail(ctx, WF_E_HIP, "hipEventCreate failed");

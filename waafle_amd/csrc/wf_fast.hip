@@ -22,6 +22,7 @@
 // those contigs only.  Contigs finished here never write attachments, keys or segment
 // records to HBM: their traffic is the hits and loci read once plus the result record.
 #include <algorithm>
+#include <cstdlib>
 
 #include "wf_device.h"
 
@@ -486,8 +487,11 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
 }
 
 template <int CAP, bool FULL>
+// rollup (FULL): carry a contig through its roll-up levels in the slice; else hand it to
+// the staged kernels at its first raise (they run every contig of a level together,
+// which measured 3x faster per contig-level on cfg4 than one wave per contig here).
 __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
-                                             const int32_t* list, int n_list, const int64_t* n_dev) {
+                                             const int32_t* list, int n_list, const int64_t* n_dev, int rollup) {
   if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
   const KArgs& K = S.k;
   const DevParams& P = K.p;
@@ -632,20 +636,29 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       if (lane == 0) F.seg[ns] = (uint32_t)n_att;    // end of the last segment (n_att <= CAP)
       wave_sync();
-      // ---- segment means (numpy pairwise order, exact) ----
+      // ---- segment means (numpy pairwise order, exact), evaluated pass by pass ----
+      // Only what the decision can use is evaluated (exact for k1 > 0):
+      //  - explain_one: an option has crit >= k1 > 0, so a segment on every unmasked locus;
+      //    the weak-locus mask needs, per locus, one known clade's mean >= kmin, or proof that
+      //    none reaches it -- a segment's mean is at most its best attachment score (times
+      //    1 + 2e-15 for the rounded sum), so segments scoring below kmin * (1 - 1e-12) are
+      //    never evaluated;
+      //  - explain_two (FULL, k2 > 0 and a positive sister threshold): a potential clade has
+      //    a mean >= k2 (bound as above); its whole row is evaluated; the sister checks read
+      //    clades whose listed parent is the parent of a potential clade, at scores >= the
+      //    sister threshold (bound as above).
+      // Passes: 0 clades on every locus, 1 segments that may settle an open locus, 2 clades on
+      // every unmasked locus, 3 every segment (not pruned), 4 potential-clade candidates,
+      // 5 potential rows + sister candidates, 6 every segment not yet evaluated.
       double* v = F.v();
       bool fail = false;
-      // Level 0 of the first form evaluates only what explain_one can use (exact, k1 > 0):
-      // an option has crit >= k1 > 0, so a segment on every unmasked locus; the weak-locus
-      // mask needs, per locus, one known clade's mean >= kmin, or proof that none reaches
-      // it -- a segment's mean is at most its best attachment score (times 1 + 2e-15 for
-      // the rounded sum), so segments scoring below kmin * (1 - 1e-12) are never evaluated.
-      // Passes: 0 clades on every locus, 1 segments that may settle an open locus, 2 clades
-      // on every unmasked locus; 3 (not pruned) every segment.
-      const bool prune = !FULL && P.k1 > 0.0 && !(WF_SKIP & 1);
+      const bool prune = P.k1 > 0.0 && !(WF_SKIP & 1);
+      const bool prune2 = FULL && prune && P.k2 > 0.0 && (!P.sister_on || P.sister_thr > 0.0);
       const uint64_t allG = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
       uint64_t um = 0;
-      uint8_t* rc = F.rc();                            // pruned: per segment, its clade run's size
+      uint8_t* rc = F.rc();                            // per segment: its clade run's size / flag
+      int* pp = reinterpret_cast<int*>(F.mx());        // parents of the potential clades (FULL)
+      int npp = 0;
       // segments of the clade run starting at t that lie on loci of `mask`
       auto run_count = [&](int t, uint64_t mask) -> int {
         const int clade = cg_of(F, t).x;
@@ -668,6 +681,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
         for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off, 64);
         return b;
       };
+      auto best_score = [&](int t) -> double {       // upper bound of segment t's mean
+        const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
+        double ub = 0.0;
+        for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[F.key[q] & kSlotMask]);
+        return ub;
+      };
       if (prune) {
         for (int t = lane; t < ns; t += 64) {
           v[t] = -1.0;                                 // not evaluated
@@ -678,229 +697,272 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
         }
         wave_sync();
       }
-      const double bound = P.kmin * (1.0 - 1e-12);
+      const double bound = P.kmin * (1.0 - 1e-12), bound2 = P.k2 * (1.0 - 1e-12);
+      const double bound_s = P.sister_thr * (1.0 - 1e-12);
       uint64_t open = 0;
-      for (int pass = prune ? 0 : 3; pass <= 3;) {
-      int n = ns;
-      const uint16_t* list = nullptr;
-      if (pass < 3) {                                  // compact this pass's segments
-        uint16_t* lst = F.list();
-        const int gu = __popcll(um);
-        n = 0;
-        for (int t0 = 0; t0 < ns; t0 += 64) {
-          const int t = t0 + lane;
-          bool in = false;
-          if (t < ns) {
-            const int2 cg = cg_of(F, t);
-            if (pass == 0) {
-              in = (int)rc[t] == G;
-            } else if (pass == 1) {
-              if (v[t] < 0.0 && cg.x != K.unknown && ((open >> cg.y) & 1ull)) {
-                const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
-                double ub = 0.0;
-                for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[F.key[q] & kSlotMask]);
-                in = ub >= bound;
-              }
-            } else {
-              in = v[t] < 0.0 && ((um >> cg.y) & 1ull) && (int)rc[t] == gu;
-            }
-          }
-          const uint64_t im = __ballot(in);
-          if (in) lst[n + __popcll(im & lanes_below())] = (uint16_t)t;
-          n += __popcll(im);
-        }
-        wave_sync();
-        list = lst;
-      }
-      for (int s0 = 0; s0 < n; s0 += 64) {
-        const int s = s0 + lane < n ? (list ? (int)list[s0 + lane] : s0 + lane) : ns;
-        bool multi = false, big = false;               // big: too many attachments for the wave path
-        int g = 0, len = 0, nl = 0;
-        if (WF_SKIP & 1) {
-          if (s < ns) v[s] = 0.75;
-        } else if (s < ns) {
-          const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att, na = ke - kb;
-          g = cg_of(F, s).y;
-          len = F.len[g];
-          nl = F.nl1[g];
-          const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
-          bool one_run = false;
-          int lo = 0, hi = 0;
-          double vv = 0.0;
-          if (na == 1) {
-            if (thread_ok) {
-              const int slot = (int)(F.key[kb] & kSlotMask);
-              lo = lo16(F.lohi[slot]); hi = hi16(F.lohi[slot]); vv = F.sc[slot];
-              one_run = true;
-            }
-          } else if (na <= kPruneMax) {
-            double Fw = 0.0;                           // best whole-locus attachment
-            for (int t = kb; t < ke; ++t) {
-              const int slot = (int)(F.key[t] & kSlotMask);
-              const uint32_t x = F.lohi[slot];
-              const double sc = F.sc[slot];
-              if (lo16(x) <= 0 && hi16(x) >= len && sc > Fw) Fw = sc;
-            }
-            int kept = 0;                              // attachments the envelope still needs
-            for (int t = kb; t < ke; ++t) {
-              const int slot = (int)(F.key[t] & kSlotMask);
-              const uint32_t x = F.lohi[slot];
-              kept += (lo16(x) < hi16(x) && F.sc[slot] > Fw) ? 1 : 0;
-            }
-            if (kept == 0 && thread_ok) { lo = 0; hi = len; vv = Fw; one_run = true; }
-          }
-          if (one_run)
-            v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
-          else if ((FULL || na <= kMultiAtt0) && nl <= 64 && len < kNpyBuf) {
-            multi = true;
-            big = na > kMultiAtt0;
-          }
-          else
-            fail = true;                               // the staged leaf kernels take it
-        }
-        uint64_t mlist = __ballot(multi);
-        if (FULL && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
-          // several multi-attachment segments (roll-up levels): one lane each
-          if (multi) {
-            const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
-            v[s] = lane_seg_mean(SliceSrc{F.key, F.lohi, F.sc}, kb, ke, PackedLut{F.lut + F.lbase[g]}, nl, len);
-          }
-          mlist = 0;
-        }
-        for (uint64_t mm = mlist; mm; mm &= mm - 1) {  // the wave, one segment each
-          const int src = __builtin_ctzll(mm);
-          const int s2 = __shfl(s, src, 64);
-          const int kb = seg_first(F, s2), na = (s2 + 1 < ns ? seg_first(F, s2 + 1) : n_att) - kb;
-          const int g2 = __shfl(g, src, 64), len2 = __shfl(len, src, 64), nl2 = __shfl(nl, src, 64);
-          int lo = 0, hi = 0;
-          double sc = 0.0;
-          if (lane < na) {
-            const int slot = (int)(F.key[kb + lane] & kSlotMask);
-            const uint32_t x = F.lohi[slot];
-            if (lo16(x) < hi16(x)) { lo = lo16(x); hi = hi16(x); sc = F.sc[slot]; }
-          }
-          const double mean = wave_seg_mean(PackedLut{F.lut + F.lbase[g2]}, nl2, len2, lo, hi, sc, F.runs());
-          if (lane == 0) v[s2] = mean;
-        }
-      }
-      wave_sync();
-      // after the pass: the weak-locus mask, the next pass
-      if (pass == 3) break;
-      if (pass == 0) {
-        if (P.weak != 0 || P.kmin <= 0.0) {
-          um = allG;                                   // penalize: no mask; kmin <= 0: nothing masked
-          break;                                       // (every locus unmasked: pass 0 covered the options)
-        }
-        um = sure_bits();
-        open = allG & ~um;                             // loci no full clade settles
-        pass = open ? 1 : 3;
-        if (!open) break;
-        continue;
-      }
-      if (pass == 1) {
-        um |= sure_bits();
-        if (um == allG || um == 0ull) break;
-        for (int t = lane; t < ns; t += 64)            // clade runs' sizes on the unmasked loci
-          if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
-            const int cnt = run_count(t, ~0ull), cu = run_count(t, um);
-            for (int q = t; q < t + cnt; ++q) rc[q] = (uint8_t)cu;
-          }
-        wave_sync();
-        pass = 2;
-        continue;
-      }
-      break;                                           // pass 2 done
-      }
-      staged = __ballot(fail) != 0;
-      wave_sync();
-      if (staged || (WF_SKIP & 4)) break;
-      // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
-      if (!prune) {
-        F.mx()[lane] = 0ull;
-        wave_sync();
-        for (int s = lane; s < ns; s += 64) {          // per-locus max over known clades
-          const int2 cg = cg_of(F, s);
-          const double x = v[s];
-          if (cg.x != K.unknown && x > 0.0) atomicMax(&F.mx()[cg.y], dbits(x));
-        }
-        wave_sync();
-        // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
-        const double mxl = __longlong_as_double((long long)F.mx()[lane]);
-        um = __ballot(lane < G && (P.weak != 0 || mxl >= P.kmin));
-      }
-      const int Gu = __popcll(um);
-      if (Gu == 0) {                                   // level 0: skipped contig (:959)
-        if (level > 0 && lane == 0) {                  // later: np.min of an empty array upstream
-          K.iters[c] = (int16_t)min(iteration, 32767);
-          K.pair_evals[c] = pair_evals;
-          K.status[c] = WF_E_EMPTYMASK;
-        }
-        break;
-      }
-      double br = -__builtin_inf(), bcrit = 0.0;
-      long long bk = -1;
-      double* rank = F.rank();
-      for (int t = lane; t < ns; t += 64) {
-        double rk = -1.0;
-        const int clade = cg_of(F, t).x;
-        if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || run_count(t, um) == Gu)) {
-          double crit, rnk;                            // (pruned: only runs on every unmasked locus)
-          sparse_score(F, v, t, ns, clade, um, Gu, crit, rnk);
-          if (crit >= P.k1) {
-            rk = rnk;
-            if (better(rnk, clade, br, bk)) { br = rnk; bk = clade; bcrit = crit; }
-          }
-        }
-        rank[t] = rk;                                  // option rank by segment (-1: none)
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        const double r2 = __shfl_xor(br, off, 64), c2 = __shfl_xor(bcrit, off, 64);
-        const long long k2 = __shfl_xor(bk, off, 64);
-        if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
-      }
-      if (bk >= 0) {
-        wave_sync();
-        int nm = 0;                                    // meld_one (:621-631): options within --range
-        if (P.dis1 == 1)
+      int outcome = 0;                                 // 2: decided (or stopped) by explain_one
+      for (int pass = prune ? 0 : 3;;) {
+        int n = ns;
+        const uint16_t* list = nullptr;
+        if (pass != 3) {                               // compact this pass's segments
+          uint16_t* lst = F.list();
+          const int gu = __popcll(um);
+          n = 0;
           for (int t0 = 0; t0 < ns; t0 += 64) {
             const int t = t0 + lane;
-            const double rk = t < ns ? rank[t] : -1.0;
-            const bool in = rk >= 0.0 && (br - rk) <= P.range;
+            bool in = false;
+            if (t < ns) {
+              const int2 cg = cg_of(F, t);
+              if (pass == 0) {
+                in = (int)rc[t] == G;
+              } else if (pass == 1) {
+                in = v[t] < 0.0 && cg.x != K.unknown && ((open >> cg.y) & 1ull) && best_score(t) >= bound;
+              } else if (pass == 2) {
+                in = v[t] < 0.0 && ((um >> cg.y) & 1ull) && (int)rc[t] == gu;
+              } else if (pass == 4) {
+                in = v[t] < 0.0 && best_score(t) >= bound2;
+              } else if (pass == 5) {
+                if (v[t] < 0.0) {
+                  in = rc[t] != 0;                     // a potential clade's row
+                  if (!in && P.sister_on && best_score(t) >= bound_s) {
+                    const int sp = K.sibp[cg.x];
+                    for (int i = 0; i < npp && !in; ++i) in = pp[i] == sp;
+                  }
+                }
+              } else {
+                in = v[t] < 0.0;
+              }
+            }
             const uint64_t im = __ballot(in);
-            if (in) F.mem()[nm + __popcll(im & lanes_below())] = cg_of(F, t).x;
-            nm += __popcll(im);
+            if (in) lst[n + __popcll(im & lanes_below())] = (uint16_t)t;
+            n += __popcll(im);
           }
+          wave_sync();
+          list = lst;
+        }
+        for (int s0 = 0; s0 < n; s0 += 64) {
+          const int s = s0 + lane < n ? (list ? (int)list[s0 + lane] : s0 + lane) : ns;
+          bool multi = false, big = false;               // big: too many attachments for the wave path
+          int g = 0, len = 0, nl = 0;
+          if (WF_SKIP & 1) {
+            if (s < ns) v[s] = 0.75;
+          } else if (s < ns) {
+            const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att, na = ke - kb;
+            g = cg_of(F, s).y;
+            len = F.len[g];
+            nl = F.nl1[g];
+            const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
+            bool one_run = false;
+            int lo = 0, hi = 0;
+            double vv = 0.0;
+            if (na == 1) {
+              if (thread_ok) {
+                const int slot = (int)(F.key[kb] & kSlotMask);
+                lo = lo16(F.lohi[slot]); hi = hi16(F.lohi[slot]); vv = F.sc[slot];
+                one_run = true;
+              }
+            } else if (na <= kPruneMax) {
+              double Fw = 0.0;                           // best whole-locus attachment
+              for (int t = kb; t < ke; ++t) {
+                const int slot = (int)(F.key[t] & kSlotMask);
+                const uint32_t x = F.lohi[slot];
+                const double sc = F.sc[slot];
+                if (lo16(x) <= 0 && hi16(x) >= len && sc > Fw) Fw = sc;
+              }
+              int kept = 0;                              // attachments the envelope still needs
+              for (int t = kb; t < ke; ++t) {
+                const int slot = (int)(F.key[t] & kSlotMask);
+                const uint32_t x = F.lohi[slot];
+                kept += (lo16(x) < hi16(x) && F.sc[slot] > Fw) ? 1 : 0;
+              }
+              if (kept == 0 && thread_ok) { lo = 0; hi = len; vv = Fw; one_run = true; }
+            }
+            if (one_run)
+              v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
+            else if ((FULL || na <= kMultiAtt0) && nl <= 64 && len < kNpyBuf) {
+              multi = true;
+              big = na > kMultiAtt0;
+            }
+            else
+              fail = true;                               // the staged leaf kernels take it
+          }
+          uint64_t mlist = __ballot(multi);
+          if (FULL && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
+            // several multi-attachment segments (roll-up levels): one lane each
+            if (multi) {
+              const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
+              v[s] = lane_seg_mean(SliceSrc{F.key, F.lohi, F.sc}, kb, ke, PackedLut{F.lut + F.lbase[g]}, nl, len);
+            }
+            mlist = 0;
+          }
+          for (uint64_t mm = mlist; mm; mm &= mm - 1) {  // the wave, one segment each
+            const int src = __builtin_ctzll(mm);
+            const int s2 = __shfl(s, src, 64);
+            const int kb = seg_first(F, s2), na = (s2 + 1 < ns ? seg_first(F, s2 + 1) : n_att) - kb;
+            const int g2 = __shfl(g, src, 64), len2 = __shfl(len, src, 64), nl2 = __shfl(nl, src, 64);
+            int lo = 0, hi = 0;
+            double sc = 0.0;
+            if (lane < na) {
+              const int slot = (int)(F.key[kb + lane] & kSlotMask);
+              const uint32_t x = F.lohi[slot];
+              if (lo16(x) < hi16(x)) { lo = lo16(x); hi = hi16(x); sc = F.sc[slot]; }
+            }
+            const double mean = wave_seg_mean(PackedLut{F.lut + F.lbase[g2]}, nl2, len2, lo, hi, sc, F.runs());
+            if (lane == 0) v[s2] = mean;
+          }
+        }
         wave_sync();
-        if (P.dis1 == 1 && nm == 0) {                  // negative --range upstream crash
-          if (lane == 0) K.status[c] = WF_E_BADINPUT;
+        // after the pass: the weak-locus mask, explain_one, the next pass
+        bool e1_now = false;
+        if (pass == 0) {
+          if (P.weak != 0 || P.kmin <= 0.0) {
+            um = allG;                                 // penalize: no mask; kmin <= 0: nothing masked
+            e1_now = true;                             // (every locus unmasked: pass 0 had the options)
+          } else {
+            um = sure_bits();
+            open = allG & ~um;                         // loci no full clade settles
+            if (open) { pass = 1; continue; }
+            e1_now = true;
+          }
+        } else if (pass == 1) {
+          um |= sure_bits();
+          if (um != allG && um != 0ull) {
+            for (int t = lane; t < ns; t += 64)        // clade runs' sizes on the unmasked loci
+              if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
+                const int cnt = run_count(t, ~0ull), cu = run_count(t, um);
+                for (int q = t; q < t + cnt; ++q) rc[q] = (uint8_t)cu;
+              }
+            wave_sync();
+            pass = 2;
+            continue;
+          }
+          e1_now = true;
+        } else if (pass == 2) {
+          e1_now = true;
+        } else if (pass == 3) {
+          // weak loci from every mean: ignore -> mask (:420-427), penalize -> none (:413-414)
+          F.mx()[lane] = 0ull;
+          wave_sync();
+          for (int t = lane; t < ns; t += 64) {        // per-locus max over known clades
+            const int2 cg = cg_of(F, t);
+            const double x = v[t];
+            if (cg.x != K.unknown && x > 0.0) atomicMax(&F.mx()[cg.y], dbits(x));
+          }
+          wave_sync();
+          const double mxl = __longlong_as_double((long long)F.mx()[lane]);
+          um = __ballot(lane < G && (P.weak != 0 || mxl >= P.kmin));
+          e1_now = true;
+        } else if (pass == 4) {                        // potential clades: a mean >= k2 (:603-605)
+          for (int t = lane; t < ns; t += 64)
+            if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
+              const int cnt = run_count(t, ~0ull);
+              bool pot = false;
+              for (int q = t; q < t + cnt; ++q) pot = pot || (v[q] >= P.k2);
+              for (int q = t; q < t + cnt; ++q) rc[q] = pot ? 1 : 0;
+            }
+          wave_sync();
+          npp = 0;                                     // their parents (sister checks, :717-744)
+          for (int t0 = 0; t0 < ns; t0 += 64) {
+            const int t = t0 + lane;
+            const bool in = t < ns && rc[t] && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
+            const uint64_t im = __ballot(in);
+            if (in && npp + __popcll(im & lanes_below()) < 64)
+              pp[npp + __popcll(im & lanes_below())] = K.parent[cg_of(F, t).x];
+            npp = min(npp + __popcll(im), 64);
+          }
+          wave_sync();
+          pass = 5;
+          continue;
+        } else {
+          break;                                       // passes 5 / 6: explain_two's inputs
+        }
+        if (!e1_now) break;
+        if (__ballot(fail) != 0ull || (WF_SKIP & 4)) { staged = __ballot(fail) != 0ull; outcome = 2; break; }
+        // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
+        const int Gu = __popcll(um);
+        if (Gu == 0) {                                 // level 0: skipped contig (:959)
+          if (level > 0 && lane == 0) {                // later: np.min of an empty array upstream
+            K.iters[c] = (int16_t)min(iteration, 32767);
+            K.pair_evals[c] = pair_evals;
+            K.status[c] = WF_E_EMPTYMASK;
+          }
+          outcome = 2;
           break;
         }
-        int lca = (int)bk;
-        if (P.dis1 == 1) {
-          int acc = -1;
-          for (int i = lane; i < nm; i += 64) acc = lca2(K, acc, F.mem()[i]);
-          lca = wave_lca(K, acc);
+          double br = -__builtin_inf(), bcrit = 0.0;
+          long long bk = -1;
+          double* rank = F.rank();
+          for (int t = lane; t < ns; t += 64) {
+            double rk = -1.0;
+            const int clade = cg_of(F, t).x;
+            if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || run_count(t, um) == Gu)) {
+              double crit, rnk;                            // (pruned: only runs on every unmasked locus)
+              sparse_score(F, v, t, ns, clade, um, Gu, crit, rnk);
+              if (crit >= P.k1) {
+                rk = rnk;
+                if (better(rnk, clade, br, bk)) { br = rnk; bk = clade; bcrit = crit; }
+              }
+            }
+            rank[t] = rk;                                  // option rank by segment (-1: none)
+          }
+    #pragma unroll
+          for (int off = 32; off > 0; off >>= 1) {
+            const double r2 = __shfl_xor(br, off, 64), c2 = __shfl_xor(bcrit, off, 64);
+            const long long k2 = __shfl_xor(bk, off, 64);
+            if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
+          }
+          if (bk >= 0) {
+            wave_sync();
+            int nm = 0;                                    // meld_one (:621-631): options within --range
+            if (P.dis1 == 1)
+              for (int t0 = 0; t0 < ns; t0 += 64) {
+                const int t = t0 + lane;
+                const double rk = t < ns ? rank[t] : -1.0;
+                const bool in = rk >= 0.0 && (br - rk) <= P.range;
+                const uint64_t im = __ballot(in);
+                if (in) F.mem()[nm + __popcll(im & lanes_below())] = cg_of(F, t).x;
+                nm += __popcll(im);
+              }
+            wave_sync();
+            if (P.dis1 == 1 && nm == 0) {                  // negative --range upstream crash
+              if (lane == 0) K.status[c] = WF_E_BADINPUT;
+              outcome = 2;
+              break;
+            }
+            int lca = (int)bk;
+            if (P.dis1 == 1) {
+              int acc = -1;
+              for (int i = lane; i < nm; i += 64) acc = lca2(K, acc, F.mem()[i]);
+              lca = wave_lca(K, acc);
+            }
+            const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
+            for (int i = lane; i < nm; i += 64) K.meld[mbase + i] = F.mem()[i];
+            if (lane < G) K.syn[l0 + lane] = ((um >> lane) & 1ull) ? 'A' : '~';   // set_synteny_one
+            if (lane == 0) {
+              K.call[c] = WF_CALL_NO_LGT;
+              K.crit[c] = bcrit;
+              K.rank[c] = br;
+              K.c1[c] = lca;
+              K.c2[c] = -1;
+              K.nm1[c] = nm;
+              K.iters[c] = (int16_t)iteration;
+              K.pair_evals[c] = pair_evals;
+            }
+            outcome = 2;
+            break;
+          }
+        if (!FULL) {                                   // explain_two (:570): the next kernel
+          staged = true;
+          outcome = 2;
+          break;
         }
-        const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
-        for (int i = lane; i < nm; i += 64) K.meld[mbase + i] = F.mem()[i];
-        if (lane < G) K.syn[l0 + lane] = ((um >> lane) & 1ull) ? 'A' : '~';   // set_synteny_one
-        if (lane == 0) {
-          K.call[c] = WF_CALL_NO_LGT;
-          K.crit[c] = bcrit;
-          K.rank[c] = br;
-          K.c1[c] = lca;
-          K.c2[c] = -1;
-          K.nm1[c] = nm;
-          K.iters[c] = (int16_t)iteration;
-          K.pair_evals[c] = pair_evals;
-        }
-        break;
+        if (pass == 3) break;                          // every mean is there already
+        pass = prune2 ? 4 : 6;
       }
-      if (!FULL) {                                     // explain_two (:570): the next kernel
-        staged = true;
-        break;
-      }
+      staged = staged || __ballot(fail) != 0ull;
+      wave_sync();
+      if (staged || outcome == 2) break;
+      const int Gu = __popcll(um);
       wave_sync();
       int dec = -1;
       if constexpr (FULL) dec = (WF_SKIP & 16) ? kDecStop : wave_two(S, F, c, h0, l0, G, ns, um, Gu, iteration, pair_evals);
@@ -911,6 +973,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       if (dec == kDecDone) break;
       if (dec == kDecRaise && iteration + 1 <= kMaxIter) {
+        if (!rollup) {
+          staged = true;
+          break;
+        }
         wave_sync();
         continue;
       }
@@ -950,10 +1016,10 @@ int blocks_per_cu() {
 // n_list: the list length, or (n_dev set) an upper bound for the grid
 template <int CAP, bool FULL>
 hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
-                      int n_list, const int64_t* n_dev, int cus, hipStream_t s) {
+                      int n_list, const int64_t* n_dev, int cus, int rollup, hipStream_t s) {
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_list, (int64_t)cus * blocks_per_cu<CAP, FULL>()));
   hipLaunchKernelGGL((k_wave<CAP, FULL>), dim3(grid), dim3(64), sizeof(WaveSmem<CAP, FULL>), s, sa, ccnt, cleaves, pend,
-                     list, n_list, n_dev);
+                     list, n_list, n_dev, rollup);
   return hipGetLastError();
 }
 
@@ -962,15 +1028,15 @@ hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t*
 hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                        hipStream_t s) {
   const int N = sa.k.n_contigs;
-  return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, s)
-                         : launch_cap<512, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, s);
+  return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s)
+                         : launch_cap<512, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s);
 }
 
 hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
-                       const int64_t* n_dev, int max_hits, int cus, hipStream_t s) {
+                       const int64_t* n_dev, int max_hits, int cus, bool rollup, hipStream_t s) {
   const int N = sa.k.n_contigs;
-  return max_hits <= 256 ? launch_cap<256, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, s)
-                         : launch_cap<512, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, s);
+  return max_hits <= 256 ? launch_cap<256, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, rollup, s)
+                         : launch_cap<512, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, rollup, s);
 }
 
 }  // namespace wf

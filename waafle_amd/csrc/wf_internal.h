@@ -158,11 +158,12 @@ struct StagedState;
 hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                        hipStream_t s);
 hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
-                       const int64_t* n_dev, int max_hits, int cus, hipStream_t s);
+                       const int64_t* n_dev, int max_hits, int cus, bool rollup, hipStream_t s);
 StagedState* staged_create(int device);
 void staged_destroy(StagedState* st);
 void staged_set_lds(StagedState* st, int64_t bytes);
-void staged_set_level0(StagedState* st, bool on);   // fused level 0 (wf_fast.hip) first
+// wave kernels (wf_fast.hip) first; rollup: they also carry the roll-up levels
+void staged_set_level0(StagedState* st, bool on, bool rollup);
 // Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2 with
 // the message in *err (-1 bad input, -2 HIP failure).
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t n_hits,

@@ -1340,7 +1340,8 @@ struct StagedState {
   int big_slots = 512;
   Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
   Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp, pend;
-  bool level0 = true;               // fused level 0 (k_fast) before the staged kernels
+  bool level0 = true;               // wave kernels (wf_fast.hip) before the staged kernels
+  bool rollup = false;              // ... carrying the roll-up levels too
   bool lut_ready = false;
   int64_t dec_lds = 24 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
@@ -1382,7 +1383,10 @@ StagedState* staged_create(int device) {
 
 void staged_destroy(StagedState* st) { delete st; }
 
-void staged_set_level0(StagedState* st, bool on) { st->level0 = on; }
+void staged_set_level0(StagedState* st, bool on, bool rollup) {
+  st->level0 = on;
+  st->rollup = rollup;
+}
 
 void staged_set_lds(StagedState* st, int64_t bytes) {
   st->dec_lds = bytes;
@@ -1599,7 +1603,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
                                            st->pend.as<int32_t>(), st->act0.as<int32_t>(),
                                            st->red.as<int64_t>() + 3, N, s));
       ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
-                         st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, s));
+                         st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
     }
   } else {
     hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),

@@ -19,7 +19,7 @@ DIS_ONE = {"report-best": 0, "meld": 1}
 DIS_TWO = {"report-best": 0, "jump": 1, "meld": 2}
 LEVEL = {"off": 0, "lenient": 1, "strict": 2}
 WEAK = {"ignore": 0, "penalize": 1, "assign-unknown": 2}
-MODES = {"staged": L.MODE_STAGED, "level0": L.MODE_LEVEL0}
+MODES = {"staged": L.MODE_STAGED, "level0": L.MODE_LEVEL0, "waves": L.MODE_WAVES}
 
 
 def params_struct(p):

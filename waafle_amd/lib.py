@@ -14,6 +14,7 @@ WF_OK, WF_E_BADINPUT, WF_E_HIP, WF_E_RUNAWAY, WF_E_NOMEM, WF_E_STATE, WF_E_EMPTY
 CALL_UNCLASSIFIED, CALL_NO_LGT, CALL_LGT = 0, 1, 2
 MODE_STAGED = 0
 MODE_LEVEL0 = 2
+MODE_WAVES = 3
 
 _P = C.c_void_p
 

@@ -274,8 +274,14 @@ def generate_batch(name, lo=0, hi=None, seed=None, workers=None, chunk=None, n_t
         workers = min(16, len(os.sched_getaffinity(0)), len(jobs))
     if workers > 1:
         import multiprocessing as mp
-        with mp.get_context("fork").Pool(workers) as pool:
+        # close + join, not the context manager's terminate(): SIGTERM'd workers hang in an
+        # attached profiler's signal handler (rocprofv3), and the parent waits on them
+        pool = mp.get_context("fork").Pool(workers)
+        try:
             parts = pool.map(_pack_chunk, jobs, chunksize=1)
+        finally:
+            pool.close()
+            pool.join()
     else:
         parts = [_pack_chunk(j) for j in jobs]
     # trim to [lo, hi)
