@@ -647,9 +647,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       //    a mean >= k2 (bound as above); its whole row is evaluated; the sister checks read
       //    clades whose listed parent is the parent of a potential clade, at scores >= the
       //    sister threshold (bound as above).
-      // Passes: 0 clades on every locus, 1 segments that may settle an open locus, 2 clades on
-      // every unmasked locus, 3 every segment (not pruned), 4 potential-clade candidates,
-      // 5 potential rows + sister candidates, 6 every segment not yet evaluated.
+      // Passes: 0 clades on every locus, 1 the best-scoring segment of each open locus, 7 the
+      // other segments that may settle a locus still open, 2 clades on every unmasked locus,
+      // 3 every segment (not pruned), 4 potential-clade candidates, 5 potential rows + sister
+      // candidates, 6 every segment not yet evaluated.
       double* v = F.v();
       bool fail = false;
       const bool prune = P.k1 > 0.0 && !(WF_SKIP & 1);
@@ -704,6 +705,16 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       for (int pass = prune ? 0 : 3;;) {
         int n = ns;
         const uint16_t* list = nullptr;
+        if (pass == 1) {                               // per open locus: its best attachment score
+          F.mx()[lane] = 0ull;
+          wave_sync();
+          for (int t = lane; t < ns; t += 64) {
+            const int2 cg = cg_of(F, t);
+            if (v[t] < 0.0 && cg.x != K.unknown && ((open >> cg.y) & 1ull))
+              atomicMax(&F.mx()[cg.y], dbits(best_score(t)));
+          }
+          wave_sync();
+        }
         if (pass != 3) {                               // compact this pass's segments
           uint16_t* lst = F.list();
           const int gu = __popcll(um);
@@ -715,8 +726,14 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
               const int2 cg = cg_of(F, t);
               if (pass == 0) {
                 in = (int)rc[t] == G;
-              } else if (pass == 1) {
+              } else if (pass == 1 || pass == 7) {
                 in = v[t] < 0.0 && cg.x != K.unknown && ((open >> cg.y) & 1ull) && best_score(t) >= bound;
+                if (pass == 1 && in) {                 // first only the best-scoring one per locus
+                  const double ub = best_score(t);
+                  in = false;
+                  const unsigned long long want = ((unsigned long long)dbits(ub) << 0);
+                  in = F.mx()[cg.y] == want;
+                }
               } else if (pass == 2) {
                 in = v[t] < 0.0 && ((um >> cg.y) & 1ull) && (int)rc[t] == gu;
               } else if (pass == 4) {
@@ -824,8 +841,13 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             if (open) { pass = 1; continue; }
             e1_now = true;
           }
-        } else if (pass == 1) {
+        } else if (pass == 1 || pass == 7) {
           um |= sure_bits();
+          if (pass == 1 && (open & ~um)) {             // loci the best segments did not settle
+            open &= ~um;
+            pass = 7;
+            continue;
+          }
           if (um != allG && um != 0ull) {
             for (int t = lane; t < ns; t += 64)        // clade runs' sizes on the unmasked loci
               if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
@@ -895,7 +917,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
           for (int t = lane; t < ns; t += 64) {
             double rk = -1.0;
             const int clade = cg_of(F, t).x;
-            if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || run_count(t, um) == Gu)) {
+            if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || (int)rc[t] == Gu)) {
               double crit, rnk;                            // (pruned: only runs on every unmasked locus)
               sparse_score(F, v, t, ns, clade, um, Gu, crit, rnk);
               if (crit >= P.k1) {
