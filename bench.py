@@ -325,7 +325,7 @@ def main():
         "kernel_ms": {"wf_score_pass": pass_ms},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "wf_score pass (staged: all kernels, HIP events on its stream)",
+                     "kernel": "wf_score pass (every kernel of one pass: wave kernels + staged remainder; HIP events on its stream)",
                      "algorithmic_bytes_per_launch": b_alg,
                      "algorithmic_bytes_rule": "24 B/hit + 12 B/locus + 96 B/contig",
                      "traffic_detail": tsrc},

@@ -42,6 +42,11 @@ def main():
                                         "peak_per_s": FP64_OPS_PEAK,
                                         "frac": kc["ops_pair"] / t / FP64_OPS_PEAK},
            "source": {"bench": bench_p, "kernel_stats": stats_p, "passes": passes}}
+    # contigs that fit the wave kernels (<= 512 hits) run explain_two inside k_wave<CAP,true>
+    # together with their level-0 evaluation; reported beside, not folded into, the k2 time
+    full = [r for r in csv.DictReader(open(stats_p)) if "k_wave<" in r["Name"] and ", true>" in r["Name"]]
+    if full:
+        res["wave_form_s_per_pass"] = sum(float(r["TotalDurationNs"]) for r in full) * 1e-9 / passes
     if pmc:
         files = glob.glob(pmc + "/**/*counter_collection.csv", recursive=True)
         valu = waves = 0.0

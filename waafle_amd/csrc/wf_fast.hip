@@ -19,7 +19,8 @@
 // A contig neither can finish (more attachments than a slice holds, more than 64 loci, a
 // leaf table, segment or explain_two state the slice cannot hold) is handed to the staged
 // path (wf_staged.hip) with its attachment and leaf counts; the staged level 0 then runs on
-// those contigs only.  Contigs finished here never write attachments, keys or segment
+// those contigs only.  A contig k_wave<CAP, true> evaluated and raised at level 0 (roll-up
+// not carried here) is handed over as a seed of the staged level 1.  Contigs finished here never write attachments, keys or segment
 // records to HBM: their traffic is the hits and loci read once plus the result record.
 #include <algorithm>
 #include <cstdlib>
@@ -614,6 +615,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     }
     // ---- levels: sort, segments, means, explain_one [, explain_two, roll-up] ----
     int64_t pair_evals = 0;
+    bool seed = false;                                 // raised at level 0: staged level 1 seed
     for (int level = 0; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
       const int iteration = level + 1;
       if (level > 0) {                               // roll up (:431-445): re-key to the parent clade
@@ -995,8 +997,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       if (dec == kDecDone) break;
       if (dec == kDecRaise && iteration + 1 <= kMaxIter) {
-        if (!rollup) {
+        if (!rollup) {                                 // the staged kernels start at level 1
           staged = true;
+          seed = iteration == 1;
+          if (lane == 0) K.pair_evals[c] = pair_evals;
           break;
         }
         wave_sync();
@@ -1013,7 +1017,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     if (lane == 0) {
       ccnt[c] = staged ? n_att : 0;
       cleaves[c] = staged ? nl_sum : 0;
-      pend[c] = staged ? 1 : 0;
+      pend[c] = staged ? (seed ? 2 : 1) : 0;
     }
     wave_sync();                                       // the slice is reused by the next contig
   }

@@ -313,7 +313,7 @@ __global__ __launch_bounds__(NT) void k_sort_contig(const SArgs S, int n_act,
       if (tid == 0) S.seg_cnt[cr] = 0;
       continue;
     }
-    const int64_t base = level == 0 ? a0 : S.act_base[cr];
+    const int64_t base = S.act_base ? S.act_base[cr] : a0;   // level 0: own offsets
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
     for (int t = tid; t < n2; t += NT) {
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(64) void k_seg_build(const SArgs S, int n_act, int 
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const int c = S.act ? S.act[cr] : cr;
     const int n = (int)(S.catt_off[c + 1] - S.catt_off[c]);
-    const int64_t base = level == 0 ? S.catt_off[c] : S.act_base[cr];
+    const int64_t base = S.act_base ? S.act_base[cr] : S.catt_off[c];
     int sbase = S.crank_first[cr];
     const int64_t l0 = K.loc_off[c];
     const int G = (int)(K.loc_off[c + 1] - l0);
@@ -1339,11 +1339,11 @@ struct StagedState {
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
   int big_slots = 512;
   Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
-  Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp, pend;
+  Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp, pend, act_l0;
   bool level0 = true;               // wave kernels (wf_fast.hip) before the staged kernels
   bool rollup = false;              // ... carrying the roll-up levels too
   bool lut_ready = false;
-  int64_t dec_lds = 24 * 1024;       // decision arena (grows with the data, see staged_score)
+  int64_t dec_lds = 32 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
   unsigned long long* host_counters = nullptr;   // pinned
   // host-coherent mailbox: k_publish writes counts + a sequence word, the host spins on it
@@ -1364,7 +1364,7 @@ StagedState* staged_create(int device) {
   st->device = device;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) st->cus = prop.multiProcessorCount;
-  if (hipHostMalloc(reinterpret_cast<void**>(&st->host_counters), 8 * sizeof(unsigned long long)) != hipSuccess)
+  if (hipHostMalloc(reinterpret_cast<void**>(&st->host_counters), 16 * sizeof(unsigned long long)) != hipSuccess)
     st->host_counters = nullptr;
   if (hipHostMalloc(reinterpret_cast<void**>(&st->host_lvl), (kMaxIter + 2) * sizeof(unsigned long long)) !=
       hipSuccess)
@@ -1540,6 +1540,68 @@ static hipError_t details_level(StagedState* st, const SArgs& sa, int level, int
 }
 
 
+// ---- the contigs the wave kernels hand over (wf_fast.hip) -------------------------------
+// pend[c]: 0 finished there, 1 staged from level 0, 2 evaluated and raised at level 0 there:
+// a seed of staged level 1 (its attachments re-keyed here, its pair count in K.pair_evals).
+struct PendIs {
+  int v;
+  __host__ __device__ bool operator()(int32_t p) const { return p == v; }
+};
+
+// attachments of list[i] (0 at and past the device count *n): the exclusive scan of it gives
+// each listed contig's compact key base, and its element N the list's key total
+struct ListAtt {
+  const int32_t* list;
+  const int64_t* cnt;
+  const int64_t* n;
+  __host__ __device__ int64_t operator()(int i) const { return i < *n ? cnt[list[i]] : 0; }
+};
+
+__global__ void k_seed_info(int64_t* red, const int64_t* base0, const int64_t* base1, int n) {
+  if (threadIdx.x == 0) {
+    red[6] = base0[n];
+    red[7] = base1[n];
+  }
+}
+
+__global__ void k_set_word(unsigned long long* p, unsigned long long v) {
+  if (threadIdx.x == 0) *p = v;
+}
+
+// the seeds' attachments to the parent clade (what the staged level 0 does on a raise)
+__global__ void k_rekey_seeds(const int32_t* list, int n, const int64_t* catt_off, int32_t* att_clade,
+                              const int32_t* parent) {
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int c = list[i];
+    const int64_t a1 = catt_off[c + 1];
+    for (int64_t a = catt_off[c] + threadIdx.x; a < a1; a += blockDim.x) att_clade[a] = parent[att_clade[a]];
+  }
+}
+
+template <class It>
+static hipError_t scan_list(StagedState* st, hipStream_t s, It in, int64_t* out, int n) {
+  size_t ts = 0;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, ts, in, out, n, s);
+  if (e != hipSuccess) return e;
+  e = st->tmp.ensure(s, ts);
+  if (e != hipSuccess) return e;
+  ts = st->tmp.n;
+  return hipcub::DeviceScan::ExclusiveSum(st->tmp.p, ts, in, out, n, s);
+}
+
+template <class Flags>
+static hipError_t select_list(StagedState* st, hipStream_t s, Flags flags, int32_t* out, int64_t* count, int n) {
+  size_t ts = 0;
+  hipError_t e = hipcub::DeviceSelect::Flagged(nullptr, ts, hipcub::CountingInputIterator<int32_t>(0), flags, out,
+                                               count, n, s);
+  if (e != hipSuccess) return e;
+  e = st->tmp.ensure(s, ts);
+  if (e != hipSuccess) return e;
+  ts = st->tmp.n;
+  return hipcub::DeviceSelect::Flagged(st->tmp.p, ts, hipcub::CountingInputIterator<int32_t>(0), flags, out,
+                                       count, n, s);
+}
+
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t NH, int64_t NL,
                  hipStream_t s, std::string* err, DetailsSink* det) {
   const int N = k.n_contigs;
@@ -1570,11 +1632,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   ST_TRY(st->cnt.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
   ST_TRY(st->cnt_leaves.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
   ST_TRY(st->att_off.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
-  ST_TRY(st->red.ensure(s, 4 * sizeof(int64_t)));
+  ST_TRY(st->red.ensure(s, 8 * sizeof(int64_t)));
   sa.catt_off = st->att_off.as<int64_t>();
   static const char* ag_env = getenv("WF_ATT_GRID");        // blocks per CU (measurement aid)
   const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * (ag_env ? atoi(ag_env) : 32));
-  ST_TRY(hipMemsetAsync(st->red.p, 0, 4 * sizeof(int64_t), s));
+  ST_TRY(hipMemsetAsync(st->red.p, 0, 8 * sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt.as<int64_t>() + N, 0, sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt_leaves.as<int64_t>() + N, 0, sizeof(int64_t), s));
   // Fused level 0 (wf_fast.hip) unless --write-details (per-level records of every contig),
@@ -1593,15 +1655,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     // list and count built on the device (WF_FULL=0: straight to the staged kernels)
     static const char* full_env = getenv("WF_FULL");
     if (!(full_env && full_env[0] == '0')) {
-      size_t ts = 0;
-      ST_TRY(hipcub::DeviceSelect::Flagged(nullptr, ts, hipcub::CountingInputIterator<int32_t>(0),
-                                           st->pend.as<int32_t>(), st->act0.as<int32_t>(),
-                                           st->red.as<int64_t>() + 3, N, s));
-      ST_TRY(st->tmp.ensure(s, ts));
-      ts = st->tmp.n;
-      ST_TRY(hipcub::DeviceSelect::Flagged(st->tmp.p, ts, hipcub::CountingInputIterator<int32_t>(0),
-                                           st->pend.as<int32_t>(), st->act0.as<int32_t>(),
-                                           st->red.as<int64_t>() + 3, N, s));
+      ST_TRY(select_list(st, s, st->pend.as<int32_t>(), st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, N));
       ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                          st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
     }
@@ -1642,19 +1696,39 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
                                            st->red.as<int64_t>() + 2, N, s));
     }
   }
+  if (level0) {
+    // staged level 0 list (pend 1) and level 1 seeds (pend 2), each with compact key bases
+    ST_TRY(st->act_l0.ensure(s, (size_t)N * 4)); ST_TRY(st->act1.ensure(s, (size_t)N * 4));
+    ST_TRY(st->base0.ensure(s, (size_t)(N + 1) * 8)); ST_TRY(st->base1.ensure(s, (size_t)(N + 1) * 8));
+    int64_t* red = st->red.as<int64_t>();
+    using PendIt = hipcub::TransformInputIterator<bool, PendIs, const int32_t*>;
+    const int32_t* pend = st->pend.as<int32_t>();
+    ST_TRY(select_list(st, s, PendIt(pend, PendIs{1}), st->act_l0.as<int32_t>(), red + 4, N));
+    ST_TRY(select_list(st, s, PendIt(pend, PendIs{2}), st->act1.as<int32_t>(), red + 5, N));
+    using AttIt = hipcub::TransformInputIterator<int64_t, ListAtt, hipcub::CountingInputIterator<int>>;
+    const int64_t* cnt = st->cnt.as<int64_t>();
+    ST_TRY(scan_list(st, s, AttIt(hipcub::CountingInputIterator<int>(0), ListAtt{st->act_l0.as<int32_t>(), cnt, red + 4}),
+                     st->base0.as<int64_t>(), N + 1));
+    ST_TRY(scan_list(st, s, AttIt(hipcub::CountingInputIterator<int>(0), ListAtt{st->act1.as<int32_t>(), cnt, red + 5}),
+                     st->base1.as<int64_t>(), N + 1));
+    hipLaunchKernelGGL(k_seed_info, dim3(1), dim3(64), 0, s, red, st->base0.as<int64_t>(), st->base1.as<int64_t>(), N);
+    ST_TRY(hipGetLastError());
+  }
   static const char* mb_env = getenv("WF_MAILBOX");         // 0: copy + event (measurement aid)
   const bool mailbox = st->mbox && !(mb_env && mb_env[0] == '0');
   if (mailbox) {
-    ST_TRY(publish_sync(st, s, st->att_off.as<int64_t>() + N, 1, st->red.p, 3,
+    ST_TRY(publish_sync(st, s, st->att_off.as<int64_t>() + N, 1, st->red.p, 8,
                         reinterpret_cast<unsigned long long*>(&hc[2])));
   } else {
     ST_TRY(hipMemcpyAsync(&hc[2], st->att_off.as<int64_t>() + N, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    ST_TRY(hipMemcpyAsync(&hc[3], st->red.p, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     ST_TRY(spin_sync(s, st->lvl_ev[0]));
   }
   const int64_t A = hc[2], TLB = hc[3], max_att = hc[4];
-  const int n_first = level0 ? (int)hc[5] : N;     // contigs of the staged level 0
-  if (n_first == 0) return 0;                       // k_fast finished every contig
+  const int n_first = level0 ? (int)hc[5] : N;     // contigs handed over (their attachments)
+  if (n_first == 0) return 0;                       // the wave kernels finished every contig
+  const int n_l0 = level0 ? (int)hc[7] : N, n_seed = level0 ? (int)hc[8] : 0;
+  const int64_t keys_l0 = level0 ? hc[9] : hc[2], keys_seed = level0 ? hc[10] : 0;
   // per-contig LDS sort when every contig's attachments fit one workgroup's LDS
   // (WF_LDS_SORT=0: device radix sort of the whole level; measurement aid)
   static const char* ls_env = getenv("WF_LDS_SORT");
@@ -1689,7 +1763,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   ST_TRY(st->run_crit.ensure(s, A1 * 8)); ST_TRY(st->run_rank.ensure(s, A1 * 8));
   ST_TRY(st->satt_lohi.ensure(s, A1 * 8)); ST_TRY(st->satt_sc.ensure(s, A1 * 8));
   ST_TRY(st->act0.ensure(s, (size_t)N * 4)); ST_TRY(st->act1.ensure(s, (size_t)N * 4));
-  ST_TRY(st->base0.ensure(s, (size_t)N * 8)); ST_TRY(st->base1.ensure(s, (size_t)N * 8));
+  ST_TRY(st->base0.ensure(s, (size_t)(N + 1) * 8)); ST_TRY(st->base1.ensure(s, (size_t)(N + 1) * 8));
   ST_TRY(st->big_list.ensure(s, (size_t)N * 8));
   ST_TRY(st->two_list.ensure(s, (size_t)N * 8));
   ST_TRY(st->one_list.ensure(s, (size_t)N * 8));
@@ -1779,21 +1853,34 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   // the trailing empty level and the always-launched HBM-slot kernel, so it is opt-in
   // (WF_PIPELINE=1) until a level has fewer launches.
   static const char* pipe_env = getenv("WF_PIPELINE");
-  const bool pipelined = sa.sort_cap > 0 && !flat_one && !det && pipe_env && pipe_env[0] == '1';
-  int n_act = n_first;
-  int64_t n_keys = A;
+  const bool pipelined = sa.sort_cap > 0 && !flat_one && !det && pipe_env && pipe_env[0] == '1' && n_l0 > 0;
+  int n_act = n_l0;
+  int64_t n_keys = keys_l0;
+  int start = 0;
+  if (n_seed > 0) {                     // level 1 begins with the seeds (level 0 appends)
+    hipLaunchKernelGGL(k_set_word, dim3(1), dim3(64), 0, s, lvl_ctr,
+                       ((unsigned long long)n_seed << 40) | (unsigned long long)keys_seed);
+    hipLaunchKernelGGL(k_rekey_seeds, dim3(std::min(n_seed, st->cus * 8)), dim3(256), 0, s, st->act1.as<int32_t>(),
+                       n_seed, sa.catt_off, sa.att_clade, k.parent);
+    ST_TRY(hipGetLastError());
+    if (n_l0 == 0) {
+      start = 1;
+      n_act = n_seed;
+      n_keys = keys_seed;
+    }
+  }
   if (det) {
     det->levels.clear();
     ST_TRY(st->span_cnt.ensure(s, A1 * 4));
     ST_TRY(st->spans.ensure(s, A1 * 8));
   }
-  for (int level = 0; n_act > 0 && level <= kMaxIter; ++level) {
+  for (int level = start; n_act > 0 && level <= kMaxIter; ++level) {
     const bool async = pipelined && level >= 1;
     sa.counters = lvl_ctr + 8 * level;
     sa.in_counts = async ? lvl_ctr + 8 * (level - 1) : nullptr;
     const int cur = level & 1;
-    sa.act = level == 0 ? (level0 ? st->act0.as<int32_t>() : nullptr) : act[cur]->as<int32_t>();
-    sa.act_base = level == 0 ? nullptr : base[cur]->as<int64_t>();
+    sa.act = level == 0 ? (level0 ? st->act_l0.as<int32_t>() : nullptr) : act[cur]->as<int32_t>();
+    sa.act_base = level == 0 && !level0 ? nullptr : base[cur]->as<int64_t>();
     sa.act_next = act[cur ^ 1]->as<int32_t>();
     sa.act_base_next = base[cur ^ 1]->as<int64_t>();
     const int cb = bits_for(n_act);
@@ -1955,8 +2042,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
                             hipMemcpyDeviceToHost, s));
       ST_TRY(spin_sync(s, st->lvl_ev[0]));
     }
-    if (level == 0 && !st->dec_lds_fixed && n_big * 50 > n_act && st->dec_lds < 48 * 1024)
-      st->dec_lds += 8 * 1024;   // adaptive arena: grows while > 2% of contigs overflow
+    if (level == start && !st->dec_lds_fixed && n_big * 50 > n_act && st->dec_lds < 48 * 1024)
+      st->dec_lds += 8 * 1024;   // adaptive arena: grows while > 2% of a first level overflow
     n_act = (int)(st->host_counters[0] >> 40);
     n_keys = (int64_t)(st->host_counters[0] & ((1ull << 40) - 1));
     if (pipelined && level == 0 && n_act > 0) {
