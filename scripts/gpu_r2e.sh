@@ -18,7 +18,7 @@ echo write ok
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d $O/pmc_valu -o run --output-format csv -- $B --steps 1 --warmup 0 > $O/pmc_valu.json 2> $O/pmc_valu.err || { echo "valu pmc failed"; tail -20 $O/pmc_valu.err; exit 1; }
 echo valu ok
 K="$B --config cfg5"
-timeout -k 10 400 python3 $K --steps 3 --warmup 1 > $O/bench_cfg5.json 2> $O/bench_cfg5.err || { echo "cfg5 bench failed"; tail -20 $O/bench_cfg5.err; exit 1; }
+timeout -k 10 400 $K --steps 3 --warmup 1 > $O/bench_cfg5.json 2> $O/bench_cfg5.err || { echo "cfg5 bench failed"; tail -20 $O/bench_cfg5.err; exit 1; }
 cat $O/bench_cfg5.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_cfg5 -o run --output-format csv -- $K --steps 3 --warmup 1 > $O/bench_cfg5_prof.json 2> $O/prof_cfg5.err || { echo "cfg5 prof failed"; tail -20 $O/prof_cfg5.err; exit 1; }
 echo prof_cfg5 ok
