@@ -46,9 +46,15 @@ constexpr int kLoc0 = 64;            // loci per contig (locus bitmasks are 64-b
 constexpr int kLut0 = 256;           // packed leaf-table entries of the contig's loci
 constexpr int kAnn0 = 64;            // (locus, system) annotation slots
 constexpr int kRuns0 = 64;           // envelope runs of a multi-attachment segment ...
-constexpr int kMultiAtt0 = 32;       // ... so at most 32 attachments (2 * 32 - 1 runs)
+constexpr int kMultiAtt0 = 32;       // ... so at most 32 attachments (2 * 32 - 1 runs);
+constexpr int kRunsL0 = 32;          // the level-0 form: 16 attachments (a 10 KB slice:
+constexpr int kMultiAttL0 = 16;      // 16 waves per CU, see WaveSmem)
 constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two ...
-constexpr int kS0 = 1024;            // ... and their score rows (potential clades x loci)
+#ifndef WF_KS0
+#define WF_KS0 640
+#endif
+constexpr int kS0 = WF_KS0;          // ... and their score rows (potential clades x loci;
+                                     // 640 = 64 x 10 and a 20 KB slice: 8 waves per CU)
 
 // One wave's LDS slice.  `scr` is reused phase by phase (offsets in the accessors):
 //   attachments:  hit[CAP] | sm[CAP] | abest[64] | ahit[64]      (annotations)
@@ -58,10 +64,14 @@ constexpr int kS0 = 1024;            // ... and their score rows (potential clad
 //   explain_two:  v | cl[CAP] | sib[CAP] | hm[CAP] | S[kS0] | masks, loci lists (FULL only)
 // key, lohi and sc (by attachment slot) live across roll-up levels.  Keys are 32-bit:
 // clade << 15 | locus << 9 | slot (clade ids < 2^17, checked on the host).
+// LDS per slice sets the occupancy (160 KB per CU): CAP 224, level-0 form = 10,096 B -> 16
+// waves per CU (the VGPR limit too); the FULL form at CAP 256 = 20,296 B -> 8.
 template <int CAP, bool FULL>
 struct WaveSmem {
   static constexpr int cmax(int a, int b) { return a > b ? a : b; }
-  static constexpr int kRunsB = (int)sizeof(WaveRunsT<kRuns0>);
+  static constexpr int kRunsN = FULL ? kRuns0 : kRunsL0;
+  using Runs = WaveRunsT<kRunsN>;
+  static constexpr int kRunsB = (int)sizeof(Runs);
   static constexpr int kScr = FULL ? 24 * CAP + 8 * kS0 + 2048
                                    : cmax(cmax(8 * CAP + 768, 8 * CAP + kRunsB + 3 * CAP), 12 * CAP + 512);
   uint32_t key[CAP];                 // keys by slot, then in sorted order
@@ -78,7 +88,7 @@ struct WaveSmem {
   __device__ unsigned long long* abest() { return reinterpret_cast<unsigned long long*>(scr + 8 * CAP); }
   __device__ int* ahit() { return reinterpret_cast<int*>(scr + 8 * CAP + 8 * kAnn0); }
   __device__ double* v() { return reinterpret_cast<double*>(scr); }
-  __device__ WaveRunsT<kRuns0>& runs() { return *reinterpret_cast<WaveRunsT<kRuns0>*>(scr + 8 * CAP); }
+  __device__ Runs& runs() { return *reinterpret_cast<Runs*>(scr + 8 * CAP); }
   __device__ uint16_t* list() { return reinterpret_cast<uint16_t*>(scr + 8 * CAP + kRunsB); }       // !FULL
   __device__ uint8_t* rc() { return reinterpret_cast<uint8_t*>(scr + 8 * CAP + kRunsB + 2 * CAP); }  // !FULL
   __device__ double* rank() { return FULL ? reinterpret_cast<double*>(scr + 8 * CAP) : sc; }
@@ -94,6 +104,11 @@ struct WaveSmem {
   __device__ int* loc_len() { return ign() + 128; }
   __device__ uint8_t* best_syn() { return reinterpret_cast<uint8_t*>(ign() + 192); }    // [64]
 };
+
+#if WF_KS0 == 640
+static_assert(sizeof(WaveSmem<224, false>) <= 160 * 1024 / 16, "level-0 slice: 16 waves per CU");
+static_assert(sizeof(WaveSmem<256, true>) <= 160 * 1024 / 8, "FULL slice: 8 waves per CU");
+#endif
 
 __device__ __forceinline__ int leaves_for(const SArgs& S, int len) {
   return (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
@@ -626,7 +641,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
         }
         wave_sync();
       }
-      if (!(WF_SKIP & 2)) sort_slice<CAP / 64>(F, n_att);   // one network: code size
+      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64>(F, n_att);   // one network: code size
       // ---- segments = runs of equal (clade, locus) ----
       int ns = 0;
       for (int t0 = 0; t0 < n_att; t0 += 64) {
@@ -798,7 +813,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             }
             if (one_run)
               v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
-            else if ((FULL || na <= kMultiAtt0) && nl <= 64 && len < kNpyBuf) {
+            else if ((FULL || na <= kMultiAttL0) && nl <= 64 && len < kNpyBuf) {
               multi = true;
               big = na > kMultiAtt0;
             }
@@ -1054,6 +1069,9 @@ hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t*
 hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                        hipStream_t s) {
   const int N = sa.k.n_contigs;
+#ifndef WF_NO_CAP224
+  if (max_hits <= 224) return launch_cap<224, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s);
+#endif
   return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s)
                          : launch_cap<512, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s);
 }

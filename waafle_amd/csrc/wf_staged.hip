@@ -1944,7 +1944,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
                            st->span_cnt.as<int32_t>(), st->spans.as<int32_t>());
       if (thread_mean) {
         hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
-        hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 8), dim3(64), 0, s, sa);
+        // one wave per segment, a serial envelope sweep (shuffle chains): as many waves as
+        // fit (62 VGPRs, 2.8 KB LDS -> 32 per CU); roll-up levels have ~10^5 such segments
+        static const char* sw_env = getenv("WF_SEGWAVE_PER_CU");   // measurement aid
+        hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * (sw_env ? atoi(sw_env) : 32)), dim3(64), 0, s, sa);
       }
       else
         hipLaunchKernelGGL(k_seg_rec<false>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
