@@ -47,6 +47,8 @@ def parse_args():
     ap.add_argument("--config", default="cfg4")
     ap.add_argument("--contigs", type=int, default=None, help="override total contigs")
     ap.add_argument("--lds-bytes", type=int, default=None)
+    ap.add_argument("--mode", default=None, choices=["level0", "waves", "staged"],
+                    help="execution form (wf_set_mode; default: the library's, level0)")
     ap.add_argument("--cpu-sample", type=int, default=5000,
                     help="contigs timed on the CPU oracle, 1 core (rank 0, N=1); 0 disables")
     ap.add_argument("--cpu-shard", type=int, default=600,
@@ -216,6 +218,8 @@ def main():
             raise RuntimeError(so.wf_last_error(h).decode())
     if args.lds_bytes:
         chk(so.wf_set_lds_bytes(h, args.lds_bytes))
+    if args.mode:
+        chk(so.wf_set_mode(h, engine.MODES[args.mode]))
     tstruct = engine.taxonomy_struct(tax)
     chk(so.wf_set_taxonomy(h, C.byref(tstruct)))
     stream = torch.cuda.current_stream(dev)
