@@ -49,6 +49,10 @@ constexpr int kRuns0 = 64;           // envelope runs of a multi-attachment segm
 constexpr int kMultiAtt0 = 32;       // ... so at most 32 attachments (2 * 32 - 1 runs);
 constexpr int kRunsL0 = 32;          // the level-0 form: 16 attachments (a 10 KB slice:
 constexpr int kMultiAttL0 = 16;      // 16 waves per CU, see WaveSmem)
+constexpr int kXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
+#ifndef WF_XCD_MAP
+#define WF_XCD_MAP 1
+#endif
 constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two ...
 #ifndef WF_KS0
 #define WF_KS0 640
@@ -515,7 +519,16 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
   WaveSmem<CAP, FULL>& F = *reinterpret_cast<WaveSmem<CAP, FULL>*>(smem);
   const int lane = threadIdx.x;
   const int nsys = K.n_sys;
-  for (int ci = blockIdx.x; ci < n_list; ci += gridDim.x) {
+  // XCD-aware contig order.  Workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8),
+  // so a plain grid stride puts neighbouring contigs on different XCDs, and the record
+  // fields of 8 neighbours (1-8 B each, one array per field) share cache lines that 8 L2s
+  // write back partially.  Instead XCD x's j-th workgroup takes contig (8 k + x) * B + j at
+  // step k (B = grid / 8): each XCD walks runs of B consecutive contigs.
+  const bool xmap = WF_XCD_MAP && gridDim.x % kXcds == 0;
+  const int xb = (int)gridDim.x / kXcds, xj = (int)blockIdx.x / kXcds, xx = (int)blockIdx.x % kXcds;
+  for (int it = 0;; ++it) {
+    const int ci = xmap ? (it * kXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
+    if (ci >= n_list) break;
     const int c = list ? list[ci] : ci;
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     const int64_t l0 = K.loc_off[c];

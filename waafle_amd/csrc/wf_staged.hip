@@ -1622,6 +1622,9 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   sa.key_tb = bits_for(std::max(n_tax, 1));
   sa.lut_off = st->lut_off.as<int32_t>();
   sa.lut = st->lut.as<int4>();
+  // WF_DEC_LDS (measurement aid) fixes the arena like wf_set_lds_bytes; read before the
+  // kernels' copy of the arena size is taken, so the two always agree
+  if (const char* dl = getenv("WF_DEC_LDS")) { st->dec_lds = atoll(dl); st->dec_lds_fixed = true; }
   sa.dec_lds_bytes = st->dec_lds;
   // kernels take SArgs by value (kernarg segment): no argument uploads, and the pointers
   // loaded from it are known to be global (global_* instead of flat_* memory operations)
@@ -1823,7 +1826,6 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   // which measured faster on cfg2/cfg3 once its arena is sized to the data)
   static const char* flat_env = getenv("WF_FLAT_ONE");
   const bool flat_one = k.p.weak != 2 && max_loci <= 64 && flat_env && flat_env[0] == '1';
-  if (const char* dl = getenv("WF_DEC_LDS")) { st->dec_lds = atoll(dl); st->dec_lds_fixed = true; }
   // explain_one by one wave per contig (k_one), the dense workgroup only for the contigs it
   // hands over (WF_ONE_FAST=0: dense workgroup for every contig; measurement aid)
   static const char* one_env = getenv("WF_ONE_FAST");
@@ -2002,7 +2004,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     // explain_two contigs are latency chains, so they should all be in flight at once
     const unsigned dec_per_cu =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>(12, (160 * 1024) / std::max<int64_t>(st->dec_lds, 1)));
-    if (one_fast && level > 0)          // few open contigs: four waves each
+    // above WF_DEC_WIDE_MAX active contigs a level's explain_two runs one wave per contig
+    // (more contigs in flight) instead of four (measurement aid; default: always four)
+    static const char* dw_env = getenv("WF_DEC_WIDE_MAX");
+    const bool wide = !dw_env || n_act <= atoi(dw_env);
+    if (one_fast && level > 0 && wide)  // few open contigs: four waves each
       hipLaunchKernelGGL((k_decide<3, 256>), dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
                          dim3(256), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     else if (one_fast)                  // k_one's overflow list and its open contigs
