@@ -95,3 +95,30 @@ def test_two_rank_gloo_error_reaches_every_rank(tmp_path):
     kind, code, contigs = str(r["outcome"]).split(":")
     assert kind == "err" and int(code) == L.WF_E_RUNAWAY
     assert eval(contigs)[0] > 1
+
+
+def test_oversized_batch_is_scored_in_halves():
+    """GpuScorer.score splits a batch the device rejects as too large (32-bit attachment
+    indices) into contig halves and concatenates the records (meld slots, rebased
+    annotation winners): the result equals the unsplit one.  The oracle stands in for
+    the device (test-only), rejecting batches of more than 7 contigs."""
+    from waafle_amd import synth
+    data = synth.generate(n=30, genes=5, clades=30, seed=11)
+    batch, tax = synth.to_batch(data, with_codes=False)
+    inner = _oracle_scorer(data, tax)
+    calls = []
+
+    def fake_once(self, sub, params):
+        calls.append(sub.n_contigs)
+        if sub.n_contigs > 7:
+            raise L.WaafleHipError(L.WF_E_BADINPUT, engine.SPLIT_MSG + " (split it)")
+        return inner(sub)
+
+    s = engine.GpuScorer.__new__(engine.GpuScorer)
+    s._score_once = fake_once.__get__(s)
+    got = s.score(batch, None)
+    want = inner(batch)
+    assert max(calls) == 30 and min(calls) <= 7
+    for f in engine.Results.__dataclass_fields__:
+        a, b = getattr(got, f), getattr(want, f)
+        assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), f

@@ -101,6 +101,9 @@ def taxonomy_struct(t):
                         root=t.root, unknown=t.unknown)
 
 
+SPLIT_MSG = "too many hit-locus attachments for one batch"   # wf_staged.hip staged_score
+
+
 class GpuScorer:
     """One libwaafle_hip context on one device."""
 
@@ -126,6 +129,20 @@ class GpuScorer:
         self._check(self.lib.wf_set_taxonomy(self.h, C.byref(self._tax)))
 
     def score(self, batch, params):
+        """wf_score over the batch.  A batch whose hit-locus attachments (or their leaves)
+        overflow the device's 32-bit work indices is scored in contig halves (contigs are
+        independent, so the records are the same)."""
+        try:
+            return self._score_once(batch, params)
+        except L.WaafleHipError as err:
+            if SPLIT_MSG not in str(err) or batch.n_contigs < 2:
+                raise
+        mid = batch.n_contigs // 2
+        parts = [self.score(batch.slice(0, mid), params),
+                 self.score(batch.slice(mid, batch.n_contigs), params)]
+        return Results.concat(parts, [0, int(batch.hit_off[mid])])
+
+    def _score_once(self, batch, params):
         res = Results.empty(batch.n_contigs, batch.n_hits, batch.n_loci, len(batch.systems))
         bs, ps, rs = batch_struct(batch), params_struct(params), res.struct()
         rc = self.lib.wf_score(self.h, C.byref(bs), C.byref(ps), C.byref(rs))
