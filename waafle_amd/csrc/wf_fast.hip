@@ -280,7 +280,14 @@ __device__ __forceinline__ void sparse_score(SM& F, const double* v, int t, int 
 // orgscorer.py:599-619, 633-744; eval_two / pair_rank / pair_crit of wf_device.h on a
 // Contig whose rows are the potential clades first, then the others).  Returns kDecDone
 // (written), kDecStop, kDecRaise, or -1 when the state does not fit (staged path).
-__device__ __noinline__ OptEval eval_two_call(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
+// eval_two inlined into wave_two: out of line, every call spilled the caller's live VGPRs
+// to scratch (cfg4: the FULL form 8.56 -> 8.35 ms inlined); WF_EVAL_OUTLINE: the old form
+#ifdef WF_EVAL_OUTLINE
+#define WF_EVAL_ATTR __noinline__
+#else
+#define WF_EVAL_ATTR __forceinline__
+#endif
+__device__ WF_EVAL_ATTR OptEval eval_two_call(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
                                               const uint8_t* best, uint8_t* out) {
   return eval_two(K, C, Pcount, pa, pb, best, out);
 }
@@ -591,8 +598,8 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             lo = min(a, b); len = max(a, b) - lo + 1; st = K.lstrand[l0 + g];
           }
           if (attaches(P, qlo, qhi, hs, lo, len, st)) {
-            ++n;
-            nl_sum += leaves_for(S, len);
+            ++n;                                     // leaves: the LDS count below 8192 sites
+            nl_sum += (g < kLoc0 && len < kNpyBuf) ? F.nl1[g] : leaves_for(S, len);
             if (g < kLoc0) am |= 1ull << g;
           }
         }

@@ -2041,7 +2041,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     const int n_big = (int)st->host_counters[2];
     if (n_big > 0) {
       const int64_t slot = ((int64_t)st->host_counters[3] + 255) & ~int64_t(255);
-      const int slots = std::min(n_big, st->cus * 2);
+      // HBM-slot workgroups in flight (135 VGPRs: 3 four-wave workgroups per CU);
+      // WF_BIG_PER_CU overrides (measurement aid)
+      static const char* bp_env = getenv("WF_BIG_PER_CU");
+      const int slots = std::min(n_big, st->cus * (bp_env ? std::max(1, atoi(bp_env)) : 2));
       ST_TRY(st->big_ws.ensure(s, (size_t)slot * slots));
       sa.k.big_ws = st->big_ws.as<char>();
       sa.k.slot_bytes = slot;
