@@ -53,6 +53,9 @@ constexpr int kXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its 
 #ifndef WF_XCD_MAP
 #define WF_XCD_MAP 1
 #endif
+#ifndef WF_PREFETCH0
+#define WF_PREFETCH0 0
+#endif
 constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two ...
 #ifndef WF_KS0
 #define WF_KS0 640
@@ -538,6 +541,19 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     if (ci >= n_list) break;
     const int c = list ? list[ci] : ci;
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
+#if WF_PREFETCH0
+    // the first 64 hits' fields, issued together with the loci loads below (one global
+    // round trip fewer per contig on the serial path)
+    double p_scv = 0.0, p_sc = 0.0;
+    int p_qlo = 0, p_qhi = 0, p_hs = 0, p_clade = 0;
+    uint32_t p_m = 0u;
+    if (h0 + lane < h1) {
+      const int64_t h = h0 + lane;
+      p_scv = K.scov[h]; p_qlo = K.qlo[h]; p_qhi = K.qhi[h]; p_hs = K.hstrand[h];
+      p_clade = K.taxon[h]; p_sc = K.score[h];
+      if (nsys > 0) p_m = K.sysmask[h];
+    }
+#endif
     const int64_t l0 = K.loc_off[c];
     const int G = (int)(K.loc_off[c + 1] - l0);
     const int Gs = min(G, kLoc0);
@@ -577,6 +593,11 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       int qlo = 0, qhi = 0, hs = 0, clade = 0;
       double scv = 0.0, sc = 0.0;
       uint32_t m = 0u;
+#if WF_PREFETCH0
+      if (h < h1 && hb == h0) {
+        scv = p_scv; qlo = p_qlo; qhi = p_qhi; hs = p_hs; clade = p_clade; sc = p_sc; m = p_m;
+      } else
+#endif
       if (h < h1) {                                  // every field in one round of loads
         scv = K.scov[h];
         qlo = K.qlo[h];
