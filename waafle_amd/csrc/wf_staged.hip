@@ -2041,10 +2041,12 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     const int n_big = (int)st->host_counters[2];
     if (n_big > 0) {
       const int64_t slot = ((int64_t)st->host_counters[3] + 255) & ~int64_t(255);
-      // HBM-slot workgroups in flight (135 VGPRs: 3 four-wave workgroups per CU);
-      // WF_BIG_PER_CU overrides (measurement aid)
+      // HBM-slot workgroups: as many as are resident at once (135 VGPRs: 3 four-wave
+      // workgroups per CU); cfg5 (30 k stress contigs) measured 234.7 ms/pass at 2 per CU,
+      // 222.8 at 3, 264.5 at 4 (a second, partial round), 230.2 at 8.  WF_BIG_PER_CU
+      // overrides (measurement aid)
       static const char* bp_env = getenv("WF_BIG_PER_CU");
-      const int slots = std::min(n_big, st->cus * (bp_env ? std::max(1, atoi(bp_env)) : 2));
+      const int slots = std::min(n_big, st->cus * (bp_env ? std::max(1, atoi(bp_env)) : 3));
       ST_TRY(st->big_ws.ensure(s, (size_t)slot * slots));
       sa.k.big_ws = st->big_ws.as<char>();
       sa.k.slot_bytes = slot;
