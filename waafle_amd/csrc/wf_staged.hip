@@ -1345,6 +1345,8 @@ struct StagedState {
   bool lut_ready = false;
   int64_t dec_lds = 32 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
+  int wide_res = -1;                 // resident k_decide<3, 256> workgroups per CU ...
+  int64_t wide_res_lds = -1;         // ... at this arena size
   unsigned long long* host_counters = nullptr;   // pinned
   // host-coherent mailbox: k_publish writes counts + a sequence word, the host spins on it
   unsigned long long* mbox = nullptr;
@@ -2008,8 +2010,22 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     // (more contigs in flight) instead of four (measurement aid; default: always four)
     static const char* dw_env = getenv("WF_DEC_WIDE_MAX");
     const bool wide = !dw_env || n_act <= atoi(dw_env);
+    // the four-wave form gets at most the workgroups resident at once (VGPRs allow 3 per
+    // CU at 137): each workgroup walks its contigs grid-stride, so a second, partial round
+    // of workgroups only lengthens the tail (WF_DEC_WIDE_PER_CU overrides; measurement aid)
+    if (st->wide_res_lds != st->dec_lds) {           // per context: no shared host state
+      int b = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_decide<3, 256>), 256,
+                                                       (size_t)st->dec_lds) != hipSuccess || b < 1)
+        b = (int)dec_per_cu;
+      st->wide_res = b;
+      st->wide_res_lds = st->dec_lds;
+    }
+    static const char* wp_env = getenv("WF_DEC_WIDE_PER_CU");
+    const unsigned wide_per_cu = wp_env ? (unsigned)std::max(1, atoi(wp_env))
+                                        : std::min<unsigned>(dec_per_cu, (unsigned)st->wide_res);
     if (one_fast && level > 0 && wide)  // few open contigs: four waves each
-      hipLaunchKernelGGL((k_decide<3, 256>), dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
+      hipLaunchKernelGGL((k_decide<3, 256>), dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * wide_per_cu)),
                          dim3(256), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     else if (one_fast)                  // k_one's overflow list and its open contigs
       hipLaunchKernelGGL(k_decide<3>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
