@@ -218,5 +218,11 @@ int main() {
   }
   wf_free(ctx);
   std::printf("api_driver ok check=%llu\n", check);
-  return 0;
+  // Every check above has run and every context is freed.  Leave without the HIP/HSA
+  // runtimes' static destructors: under ASan they free runtime memory after the
+  // sanitizer's device-allocator hooks are gone, and ASan aborts in its own CHECK
+  // (sanitizer_allocator_device.h, dev_runtime_unloaded_) -- a teardown-order artefact,
+  // not a finding in this code.
+  std::fflush(stdout);
+  std::_Exit(0);
 }
