@@ -1,23 +1,29 @@
-"""Benchmark: contigs scored/sec (+ k2 clade-pair evals/sec) on MI355X.
+"""Benchmark: contigs scored/sec + k2 clade-pair evals/sec on MI355X.
 
-Workload (BASELINE.json configs[3], the north-star configuration): synthetic 1,000,000
-contigs x 10 genes x 2000 clades, 20 decoy hits per gene (210 M hits), default
-waafle_orgscorer parameters, roll-up enabled, on one MI355X (it fits: ~7 GB of hits).
-One step = one wf_score pass over the whole batch with inputs already resident in HBM.
-For N GPUs (torch.distributed.run, one process per GPU) the SAME 1M-contig batch is split
-into N contiguous contig ranges (strong scaling; dist.rank_bounds over the per-contig cost,
-uniform for this homogeneous generator); contigs are independent, so there is no
-data-path collective -- only the barrier and the max-over-ranks timing.
+Main line (`value`): BASELINE.json configs[3], the north-star configuration -- synthetic
+1,000,000 contigs x 10 genes x 2000 clades, 20 decoy hits per gene (210 M hits), default
+waafle_orgscorer parameters, roll-up enabled, one wf_score pass over the whole batch with
+inputs resident in HBM.  For N GPUs (torch.distributed.run, one process per GPU) the SAME
+1M-contig batch is split into N contiguous contig ranges (strong scaling); contigs are
+independent, so there is no data-path collective -- only the barrier and the max-over-ranks
+timing.
 
-Each rank generates only its own contig range: the generator draws every 10k-contig
-chunk from its own seed (synth.generate_batch), in parallel worker processes, before the
-GPU is touched.  cfg2 / cfg3 / cfg5 stay available with --config.
+k2 leg (`k2`, top-level `k2_pair_evals_per_sec`): BASELINE.json configs[4], the explain_two
+stress set (20 genes, 5000 clades, ~12.5 M reference clade pairs per contig).  Every rank
+times its 6,250-contig share of the 50,000 contigs (the per-GPU share at 8 GPUs: at N = 8
+the leg is the whole config), with the per-phase HIP-event timing of the library
+(wf_timing.phase_ms): the explain_two kernels' time, the B_k2 bytes they stand for, and
+the whole pass.
 
-Extra keys on the line (rank 0, N=1): `cpu_baseline` (the oracle port on 1 core and on
-disjoint shards in parallel processes, a bounded sample of the same workload),
-`pcie_inclusive` (scope ii: host arrays -> wf_score host mode -> host results),
-`cli_end_to_end` (scope iii: text files -> `python -m waafle_amd.orgscorer` -> TSVs, cfg2),
-`k2` (the isolated explain_two kernel at cfg5, from profiles/ when present).
+Each rank generates its contig ranges before the GPU is touched (synth.generate_batch:
+every chunk from its own seed, in parallel worker processes).  cfg2 / cfg3 / cfg5 stay
+available as the main workload with --config.
+
+Extra keys on the line (rank 0, N=1): `cpu_baseline` (the oracle port on 1 core, on the
+job's cores in parallel processes over disjoint shards, and its explain_two pair rate on a
+stress contig), `pcie_inclusive` (scope ii: host arrays -> wf_score host mode -> host
+results), `cli_end_to_end` (scope iii: text files -> `python -m waafle_amd.orgscorer` ->
+TSVs, cfg2 and cfg3).
 
     python bench.py [--gpus N --steps K --warmup W] [--config cfg2|cfg3|cfg4|cfg5]
 """
@@ -51,12 +57,18 @@ def parse_args():
                     help="execution form (wf_set_mode; default: the library's, level0)")
     ap.add_argument("--cpu-sample", type=int, default=5000,
                     help="contigs timed on the CPU oracle, 1 core (rank 0, N=1); 0 disables")
-    ap.add_argument("--cpu-shard", type=int, default=600,
-                    help="contigs per process of the parallel CPU leg; 0 disables")
-    ap.add_argument("--e2e", default="cfg2", help="CLI end-to-end config ('' disables)")
+    ap.add_argument("--cpu-parallel", type=int, default=10000,
+                    help="contigs of the parallel CPU leg (split over the job's cores); 0 disables")
+    ap.add_argument("--cpu-k2-clades", type=int, default=1000,
+                    help="clades of the stress contig timed for the CPU pair rate; 0 disables")
+    ap.add_argument("--e2e", default="cfg2,cfg3", help="CLI end-to-end configs ('' disables)")
     ap.add_argument("--pcie", type=int, default=1, help="time the host-array scope")
+    ap.add_argument("--k2-contigs", type=int, default=6250,
+                    help="cfg5 contigs per rank for the k2 leg; 0 disables")
+    ap.add_argument("--k2-steps", type=int, default=3)
     ap.add_argument("--traffic-json", default=None)
-    ap.add_argument("--k2-json", default=os.path.join(PROFILES, "r02_k2_cfg5.json"))
+    ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r03_k2_pmc.json"),
+                    help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
     return ap.parse_args()
 
 
@@ -114,10 +126,28 @@ def _oracle_contigs(a, b):
     return time.perf_counter() - t0
 
 
-def cpu_baseline(config, n_one, n_shard):
+def _oracle_pairs(clades, seed=5):
+    """The oracle's explain_two on one cfg5-shaped stress contig with `clades` clades
+    (P_pot ~ clades): (reference-equivalent pairs, seconds of the scoring call)."""
+    from oracle import orgscorer_oracle as orc
+    from oracle_bridge import oracle_hits_from_batch, oracle_loci_from_batch
+    from waafle_amd import cli, synth
+    data = synth.generate(n=1, genes=20, clades=clades, seed=seed, stress=True)
+    batch, tax = synth.to_batch(data, with_codes=False)
+    hits, loci = oracle_hits_from_batch(batch, tax), oracle_loci_from_batch(batch)
+    lengths = dict(zip(batch.contig_names, batch.contig_lengths.tolist()))
+    params = orc.Params(**cli.param_dict(cli.parse_flags([])))
+    t0 = time.perf_counter()
+    contigs = orc.score_contigs(lengths, loci, hits, orc.Taxonomy(data.tax.edges), params)
+    dt = time.perf_counter() - t0
+    return sum(C.pair_evals for C in contigs.values()), dt
+
+
+def cpu_baseline(config, n_one, n_par, k2_clades):
     """The oracle (Python/numpy restatement of waafle_orgscorer) on chunk 0 of the same
-    workload, inputs pre-parsed (same scope as the GPU value): one core, then P processes
-    on disjoint contig shards (fork), rate = contigs / slowest shard."""
+    workload, inputs pre-parsed (same scope as the GPU value): one core; then the job's P
+    cores as P processes on disjoint contig shards (fork), rate = contigs / slowest shard;
+    and the explain_two pair rate on one stress contig (cfg5 shape, fewer clades)."""
     from oracle import orgscorer_oracle as orc
     from waafle_amd import cli, synth
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -133,10 +163,12 @@ def cpu_baseline(config, n_one, n_shard):
            "sample": "contigs 0..{} of the {} workload (chunk 0), oracle (Python/numpy "
                      "restatement of waafle_orgscorer) on 1 host core, inputs pre-parsed; "
                      "{:.1f} s".format(n_one, config, dt)}
-    P = min(cores, batch.n_contigs // max(n_shard, 1)) if n_shard else 0
-    if P >= 2:
+    n_par = min(n_par, batch.n_contigs)
+    if n_par > 0 and cores >= 2:
         import multiprocessing as mp
-        shards = [(i * n_shard, (i + 1) * n_shard) for i in range(P)]
+        P = cores
+        cuts = np.linspace(0, n_par, P + 1).astype(int)
+        shards = [(int(x), int(y)) for x, y in zip(cuts[:-1], cuts[1:])]
         t0 = time.perf_counter()
         pool = mp.get_context("fork").Pool(P)      # close + join (see synth.generate_batch)
         try:
@@ -145,33 +177,173 @@ def cpu_baseline(config, n_one, n_shard):
             pool.close()
             pool.join()
         wall = time.perf_counter() - t0
-        out["parallel"] = {"value": P * n_shard / max(secs), "unit": "contigs/s", "cores": P,
+        out["parallel"] = {"value": n_par / max(secs), "unit": "contigs/s", "cores": P,
                            "kind": "port", "slowest_shard_s": max(secs), "wall_s": wall,
-                           "sample": "{} processes x {} disjoint contigs of chunk 0, "
-                                     "rate = contigs / slowest shard".format(P, n_shard)}
+                           "sample": "contigs 0..{} of chunk 0 in {} processes (disjoint "
+                                     "shards of ~{}), rate = contigs / slowest shard; {} = "
+                                     "this job's CPU share (sched_getaffinity, "
+                                     "OMP_NUM_THREADS)".format(n_par, P, n_par // P, P)}
+    if k2_clades > 0:
+        pairs, sec = _oracle_pairs(k2_clades)
+        full = 12_497_500
+        out["k2_pairs"] = {
+            "value": pairs / sec, "unit": "clade-pair evals/s", "cores": 1, "kind": "port",
+            "pairs": pairs, "seconds": sec,
+            "extrapolated_s_per_cfg5_contig": full / (pairs / sec),
+            "sample": "one cfg5-shaped stress contig with {} clades (P_pot ~ {}), oracle "
+                      "explain_two on 1 core; a cfg5 contig (5000 clades, 12,497,500 pairs) "
+                      "extrapolated at the same per-pair rate".format(k2_clades, k2_clades)}
     return out
 
 
 # ---- scope (iii): CLI text -> TSV ---------------------------------------------------------
-def cli_end_to_end(config):
+def cli_end_to_end(config, workers):
     """`python -m waafle_amd.orgscorer` on the text rendering of a config (native ingest,
-    one GPU, TSV writer): wall clock of the whole process, and the CLI's own phase split."""
+    one GPU, TSV writer): wall clock of the whole process, and the CLI's own phase split.
+    The text is written chunk-parallel (synth.write_text_chunked) before the timed run."""
     from waafle_amd import synth
-    data = synth.generate_config(config)
     with tempfile.TemporaryDirectory() as tmp:
-        paths = synth.write_text(data, tmp, "e2e")
+        t0 = time.perf_counter()
+        paths, n, nh = synth.write_text_chunked(config, tmp, "e2e", workers=workers)
+        t_text = time.perf_counter() - t0
+        size = sum(os.path.getsize(p) for p in paths)
         cmd = [sys.executable, "-m", "waafle_amd.orgscorer"] + paths + ["--outdir", tmp]
         t0 = time.perf_counter()
-        run = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO, timeout=600)
+        run = subprocess.run(cmd, capture_output=True, text=True, cwd=REPO, timeout=900)
         wall = time.perf_counter() - t0
     if run.returncode != 0:
-        return {"error": run.stderr.strip().splitlines()[-3:]}
+        return {"config": config, "error": run.stderr.strip().splitlines()[-3:]}
     phases = [l for l in run.stderr.splitlines() if l.startswith("Finished successfully")]
-    return {"config": config, "contigs": data.n_contigs, "hits": data.n_hits,
-            "value": data.n_contigs / wall, "unit": "contigs/s", "wall_s": wall,
+    return {"config": config, "contigs": n, "hits": nh, "input_bytes": size,
+            "value": n / wall, "unit": "contigs/s", "wall_s": wall, "text_write_s": t_text,
             "phases": phases[-1] if phases else None,
             "scope": "text files -> native ingest -> wf_score (1 GPU) -> 3 TSVs, one process "
                      "incl. interpreter start and GPU init"}
+
+
+class DeviceBatch:
+    """A batch's arrays and result records in HBM (torch tensors) with the wf_batch /
+    wf_result structs pointing at them."""
+
+    def __init__(self, batch, dev):
+        import torch
+        from waafle_amd import lib as L
+        N, NH, NL = batch.n_contigs, batch.n_hits, batch.n_loci
+        self.d = {}
+        for f in ("hit_off", "hit_qlo", "hit_qhi", "hit_taxon", "hit_strand", "hit_score",
+                  "hit_scov", "hit_sysmask", "loc_off", "loc_start", "loc_end", "loc_strand"):
+            arr = getattr(batch, f)
+            if arr.dtype == np.uint32:
+                arr = arr.view(np.int32)
+            self.d[f] = torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+        e = lambda n, t: torch.empty(max(n, 1), dtype=t, device=dev)
+        self.out = {
+            "call": e(N, torch.int8), "crit": e(N, torch.float64), "rank": e(N, torch.float64),
+            "clade1": e(N, torch.int32), "clade2": e(N, torch.int32),
+            "direction": e(N, torch.int8), "iterations": e(N, torch.int16),
+            "synteny": e(NL, torch.uint8), "n_meld1": e(N, torch.int32),
+            "n_meld2": e(N, torch.int32), "meld": e(2 * NH + 2 * N, torch.int32),
+            "annot_hit": e(NL, torch.int32), "pair_evals": e(N, torch.int64),
+            "status": e(N, torch.int32), "need_bytes": e(N, torch.int64)}
+        self.bs = L.WfBatch(n_contigs=N, n_systems=1, n_hits=NH, n_loci=NL,
+                            max_hits=batch.max_hits, max_loci=batch.max_loci,
+                            device_resident=1, _pad=0,
+                            **{f: C.c_void_p(self.d[f].data_ptr()) for f in self.d})
+        self.rs = L.WfResult(**{f: C.c_void_p(self.out[f].data_ptr())
+                                for f, _ in L.WfResult._fields_})
+
+    def host(self, f):
+        return self.out[f].cpu().numpy()
+
+
+def timed_passes(so, h, chk, db, params, steps, warmup, dist, dev):
+    """W untimed passes, then K passes bracketed by barrier + synchronize, with the
+    library's HIP-event timing on: (elapsed seconds max over ranks, wf_timing)."""
+    import torch
+    from waafle_amd import dist as wdist, lib as L
+
+    def step():
+        chk(so.wf_score(h, C.byref(db.bs), C.byref(params), C.byref(db.rs)))
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    status = db.host("status")
+    assert not status.any(), "contig status errors: {}".format(np.unique(status))
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    chk(so.wf_timing_enable(h, 1))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    tm = L.WfTiming()
+    chk(so.wf_timing_read(h, C.byref(tm)))
+    chk(so.wf_timing_enable(h, 0))
+    return wdist.max_over_ranks(t1 - t0, dist, dev), tm
+
+
+def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json):
+    """The explain_two stress leg (BASELINE configs[4]) on this rank's cfg5 share."""
+    import torch
+    db = DeviceBatch(kbatch, dev)
+    elapsed, tm = timed_passes(so, h, chk, db, params, steps, 1, dist, dev)
+    pe = db.host("pair_evals")
+    calls = db.host("call")
+    counts = k2_algorithmic(pe, kbatch)
+    del db
+    torch.cuda.empty_cache()
+    ph = tm.phases()
+    per = lambda k: ph[k][0] / max(1, tm.passes)
+    k2_ms = per("decide") + per("big")
+    # whole-job: pairs and B_k2 summed over ranks, times max over ranks
+    v = np.array([counts["pairs"], counts["b_k2_bytes"], kbatch.n_contigs,
+                  float((calls == 2).sum())], dtype=np.float64)
+    if dist:
+        t = torch.tensor(v, device=dev)
+        dist.all_reduce(t)
+        v = t.cpu().numpy()
+    k2_s = np.array([k2_ms * 1e-3])
+    k2_max = float(wdist_max(k2_s[0], dist, dev))
+    pass_s = elapsed / steps
+    achieved = v[1] / k2_max / 1e9
+    out = {
+        "source": "this run: {} timed passes, HIP events per phase (wf_timing)".format(steps),
+        "workload": "cfg5 stress: {} contigs per GPU x {} GPUs (rank r: contigs "
+                    "[6250r, 6250(r+1)) of the 50,000), 20 genes, 5000 clades".format(
+                        kbatch.n_contigs, world),
+        "contigs": int(v[2]), "lgt_calls": int(v[3]),
+        "pairs_reference_equivalent": v[0],
+        "k2_pair_evals_per_sec": v[0] / pass_s,
+        "contigs_per_sec": v[2] / pass_s,
+        "pass_ms": pass_s * 1e3,
+        "explain_two_ms_per_pass": k2_max * 1e3,
+        "explain_two_phases_ms": {"decide": per("decide"), "big": per("big")},
+        "other_phases_ms": {k: per(k) for k in ("waves", "attach", "segments")},
+        "b_k2_bytes": v[1], "b_k2_rule": "sum over explain_two contigs of P_pot * G * 8 "
+                                        "(SURVEY 8(d): the potential clades' score rows)",
+        "hbm": {"achieved_GBs": achieved, "peak_GBs": HBM_PEAK_GBS,
+                "frac": achieved / HBM_PEAK_GBS},
+        "p_pot_max": counts["p_pot_max"],
+    }
+    if pmc_json and os.path.exists(pmc_json):
+        with open(pmc_json) as fh:
+            pj = json.load(fh)
+        if pj.get("contigs") == kbatch.n_contigs:
+            insts = pj["valu_insts_per_pass"]
+            peak = pj.get("valu_peak_insts_per_s", 2.4576e12)
+            out["valu"] = {"insts_per_pass": insts, "achieved_insts_per_s": insts / (k2_max),
+                           "peak_insts_per_s": peak, "frac": insts / k2_max / peak,
+                           "source": pj.get("source")}
+    return out
+
+
+def wdist_max(x, dist, dev):
+    from waafle_amd import dist as wdist
+    return wdist.max_over_ranks(x, dist, dev)
 
 
 def main():
@@ -180,21 +352,26 @@ def main():
     from waafle_amd import synth
     rank, world, local = wdist.rank_env()
     cores, _ = host_cpus()
+    workers = max(1, min(16, cores // world))
 
-    # ---- generate this rank's contig range BEFORE touching the GPU (fork-safe) ----
+    # ---- generate this rank's contig ranges BEFORE touching the GPU (fork-safe) ----
     n_total = args.contigs or synth.CONFIGS[args.config]["n"]
     a, b = wdist.rank_bounds(np.ones(n_total), world)[rank]    # uniform expected cost
     t_gen = time.perf_counter()
-    batch, tax = synth.generate_batch(args.config, a, b, workers=max(1, min(16, cores // world)),
-                                      n_total=n_total)
+    batch, tax = synth.generate_batch(args.config, a, b, workers=workers, n_total=n_total)
+    kbatch = ktax = None
+    if args.k2_contigs > 0:
+        k0 = (rank * args.k2_contigs) % synth.CONFIGS["cfg5"]["n"]
+        kbatch, ktax = synth.generate_batch("cfg5", k0, k0 + args.k2_contigs, workers=workers)
     t_gen = time.perf_counter() - t_gen
     # CPU legs before the GPU is initialised: the parallel leg forks worker processes, and
-    # the end-to-end leg is its own process that initialises the GPU itself
-    cpu_line = e2e_line = None
+    # the end-to-end legs are processes that initialise the GPU themselves
+    cpu_line, e2e_lines = None, []
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu_line = cpu_baseline(args.config, args.cpu_sample, args.cpu_shard)
+        cpu_line = cpu_baseline(args.config, args.cpu_sample, args.cpu_parallel,
+                                args.cpu_k2_clades)
     if rank == 0 and world == 1 and args.e2e:
-        e2e_line = cli_end_to_end(args.e2e)
+        e2e_lines = [cli_end_to_end(c, workers) for c in args.e2e.split(",") if c]
 
     import torch
     from waafle_amd import cli, engine, lib as L
@@ -206,7 +383,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    N, NH, NL = batch.n_contigs, batch.n_hits, batch.n_loci
+    N, NH = batch.n_contigs, batch.n_hits
     pdict = cli.param_dict(cli.parse_flags([]))
     params = engine.params_struct(pdict)
     so = L.load()
@@ -225,68 +402,17 @@ def main():
     stream = torch.cuda.current_stream(dev)
     chk(so.wf_set_stream(h, C.c_void_p(stream.cuda_stream)))
 
-    d = {}
-    for f in ("hit_off", "hit_qlo", "hit_qhi", "hit_taxon", "hit_strand", "hit_score",
-              "hit_scov", "hit_sysmask", "loc_off", "loc_start", "loc_end", "loc_strand"):
-        arr = getattr(batch, f)
-        if arr.dtype == np.uint32:
-            arr = arr.view(np.int32)
-        d[f] = torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
-    out = {
-        "call": torch.empty(N, dtype=torch.int8, device=dev),
-        "crit": torch.empty(N, dtype=torch.float64, device=dev),
-        "rank": torch.empty(N, dtype=torch.float64, device=dev),
-        "clade1": torch.empty(N, dtype=torch.int32, device=dev),
-        "clade2": torch.empty(N, dtype=torch.int32, device=dev),
-        "direction": torch.empty(N, dtype=torch.int8, device=dev),
-        "iterations": torch.empty(N, dtype=torch.int16, device=dev),
-        "synteny": torch.empty(max(NL, 1), dtype=torch.uint8, device=dev),
-        "n_meld1": torch.empty(N, dtype=torch.int32, device=dev),
-        "n_meld2": torch.empty(N, dtype=torch.int32, device=dev),
-        "meld": torch.empty(2 * NH + 2 * N, dtype=torch.int32, device=dev),
-        "annot_hit": torch.empty(max(NL, 1), dtype=torch.int32, device=dev),
-        "pair_evals": torch.empty(N, dtype=torch.int64, device=dev),
-        "status": torch.empty(N, dtype=torch.int32, device=dev),
-        "need_bytes": torch.empty(N, dtype=torch.int64, device=dev),
-    }
-    bs = L.WfBatch(n_contigs=N, n_systems=1, n_hits=NH, n_loci=NL, max_hits=batch.max_hits,
-                   max_loci=batch.max_loci, device_resident=1, _pad=0,
-                   **{f: C.c_void_p(d[f].data_ptr()) for f in d})
-    rs = L.WfResult(**{f: C.c_void_p(out[f].data_ptr()) for f, _ in L.WfResult._fields_})
-
-    def step():
-        chk(so.wf_score(h, C.byref(bs), C.byref(params), C.byref(rs)))
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    status = out["status"].cpu().numpy()
-    assert not status.any(), "contig status errors: {}".format(np.unique(status))
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    chk(so.wf_timing_enable(h, 1))
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
-    tm = L.WfTiming()
-    chk(so.wf_timing_read(h, C.byref(tm)))
-    elapsed = wdist.max_over_ranks(t1 - t0, dist, dev)
-
-    calls = out["call"].cpu().numpy()
-    pe = out["pair_evals"].cpu().numpy()
+    db = DeviceBatch(batch, dev)
+    elapsed, tm = timed_passes(so, h, chk, db, params, args.steps, args.warmup, dist, dev)
+    calls, pe, iters = db.host("call"), db.host("pair_evals"), db.host("iterations")
+    del db
+    torch.cuda.empty_cache()
     pairs = float(pe.sum())
     k2_counts = k2_algorithmic(pe, batch)
-    iters = out["iterations"].cpu().numpy()
     if dist:          # whole-job counts
-        import torch as T
-        v = T.tensor([pairs, float((calls == 2).sum()), float((calls == 1).sum()),
-                      float((calls == 0).sum()), float((iters > 1).sum())], dtype=T.float64,
-                     device=dev)
+        v = torch.tensor([pairs, float((calls == 2).sum()), float((calls == 1).sum()),
+                          float((calls == 0).sum()), float((iters > 1).sum())],
+                         dtype=torch.float64, device=dev)
         dist.all_reduce(v)
         pairs, n_lgt, n_no, n_un, n_up = v.tolist()
     else:
@@ -298,7 +424,7 @@ def main():
     b_alg = algorithmic_bytes(batch)
     achieved = b_alg / (pass_ms * 1e-3) / 1e9
     traffic, tsrc = None, None
-    tpath = args.traffic_json or os.path.join(PROFILES, "r02_traffic_{}.json".format(args.config))
+    tpath = args.traffic_json or os.path.join(PROFILES, "r03_traffic_{}.json".format(args.config))
     if os.path.exists(tpath):
         with open(tpath) as fh:
             tj = json.load(fh)
@@ -319,26 +445,34 @@ def main():
                                        NH * world if world == 1 else "~{}".format(NH * world)),
                    "contigs_total": n_total, "contigs_per_gpu": N, "hits_per_gpu": NH,
                    "parallelism": "dp{} (static contig split, no collective)".format(world)},
-        "k2_pair_evals_per_sec": pairs / (elapsed / args.steps),
+        "k2_pair_evals_per_sec": None,
         "k2_pair_evals_note": "reference-equivalent count: sum of P_pot(P_pot-1)/2 over "
                               "explain_two calls (orgscorer.py:606-608 score(c1,c2) calls), "
-                              "not pairs the mask-class search evaluates",
-        "k2_counts": k2_counts,
+                              "on the cfg5 stress leg (`k2`); the mask-class search "
+                              "evaluates far fewer pairs",
         "calls": {"lgt": int(n_lgt), "no_lgt": int(n_no), "unclassified": int(n_un),
                   "rolled_up": int(n_up)},
-        "kernel_ms": {"wf_score_pass": pass_ms},
+        "main_k2_counts": dict(k2_counts, pair_evals_per_sec=pairs / (elapsed / args.steps)),
+        "kernel_ms": dict({"wf_score_pass": pass_ms},
+                          **{"phase_" + k: v[0] / max(1, tm.passes)
+                             for k, v in tm.phases().items()}),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "wf_score pass (every kernel of one pass: wave kernels + staged remainder; HIP events on its stream)",
+                     "kernel": "wf_score pass (every kernel of one pass: wave kernels + "
+                               "staged remainder; HIP events on its stream)",
                      "algorithmic_bytes_per_launch": b_alg,
                      "algorithmic_bytes_rule": "24 B/hit + 12 B/locus + 96 B/contig",
                      "traffic_detail": tsrc},
         "generate_s": t_gen,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and os.path.exists(args.k2_json):
-        with open(args.k2_json) as fh:
-            result["k2"] = json.load(fh)
+    if kbatch is not None:
+        if ktax.names != tax.names:
+            tk = engine.taxonomy_struct(ktax)
+            chk(so.wf_set_taxonomy(h, C.byref(tk)))
+        result["k2"] = k2_leg(so, h, chk, kbatch, params, args.k2_steps, dist, dev, world,
+                              args.k2_pmc_json)
+        result["k2_pair_evals_per_sec"] = result["k2"]["k2_pair_evals_per_sec"]
     if rank == 0 and world == 1 and args.pcie:
         # scope (ii): host (pageable numpy) arrays in, host results out, second call timed
         s = engine.GpuScorer(local)
@@ -356,8 +490,8 @@ def main():
             "scope": "host arrays -> wf_score host mode (H2D, kernels, D2H of the records)"}
     so.wf_free(h)
     result["cpu_baseline"] = cpu_line
-    if e2e_line is not None:
-        result["cli_end_to_end"] = e2e_line
+    if e2e_lines:
+        result["cli_end_to_end"] = e2e_lines
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

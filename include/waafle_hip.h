@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 2
+#define WF_ABI_VERSION 3
 
 enum wf_status {
   WF_OK = 0,
@@ -33,7 +33,9 @@ enum wf_status {
   WF_E_RUNAWAY = -3,   /* > 100 roll-up iterations: orgscorer.py:580-581 */
   WF_E_NOMEM = -4,     /* per-contig workspace too small (see wf_result.need_bytes) */
   WF_E_STATE = -5,     /* call order (e.g. wf_score before wf_set_taxonomy) */
-  WF_E_EMPTYMASK = -6  /* every locus masked at a roll-up level (np.min of empty) */
+  WF_E_EMPTYMASK = -6, /* every locus masked at a roll-up level (np.min of empty) */
+  WF_E_TOOBIG = -7     /* the batch's hit-locus attachments exceed one call's limit
+                          (WF_OPT_ATT_LIMIT, at most 2^31 - 1): score it in parts */
 };
 
 enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
@@ -47,6 +49,16 @@ enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
  *   contigs: attachments, per-contig sort, segment means, decisions; one pass per level).
  * The ABI-1 WF_MODE_FUSED form (1) stays retired; wf_set_mode rejects it. */
 enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
+
+/* Context options (wf_set_option); every one leaves the results unchanged.
+ * WF_OPT_SPARSE_BIG: 1 (default) contigs whose gene-score matrix outgrows the LDS arena
+ *   take the decision straight from the segment table, one wave per contig; 0: the dense
+ *   matrix in an HBM slot (the only form for > 63 loci or --weak-loci assign-unknown);
+ *   2: every decision the staged kernels make goes to the segment-table form (a test
+ *   setting: it exercises that form on every input).
+ * WF_OPT_ATT_LIMIT: hit-locus attachments one wf_score call accepts (default and maximum
+ *   2^31 - 1; more -> WF_E_TOOBIG, nothing scored). */
+enum wf_option { WF_OPT_SPARSE_BIG = 1, WF_OPT_ATT_LIMIT = 2 };
 
 typedef struct wf_ctx wf_ctx;
 
@@ -136,9 +148,19 @@ typedef struct wf_result {
 
 /* Pass timing accumulated while enabled: HIP events recorded on the context stream
  * around every kernel of each wf_score pass. */
+enum wf_phase {
+  WF_PHASE_WAVES = 0,         /* wave kernels: level 0, explain_one / explain_two in LDS */
+  WF_PHASE_ATTACH = 1,        /* staged: attachment counts, offsets, attachments */
+  WF_PHASE_SEGMENTS = 2,      /* staged, per level: sort, segments, exact segment means */
+  WF_PHASE_DECIDE = 3,        /* staged, per level: k_one + k_decide (LDS arena) */
+  WF_PHASE_BIG = 4,           /* staged, per level: k_big_sparse + k_decide_big */
+  WF_N_PHASES = 8
+};
 typedef struct wf_timing {
   double pass_ms;             /* sum over timed passes */
   int64_t passes;             /* number of wf_score calls timed */
+  double phase_ms[WF_N_PHASES];       /* per wf_phase, summed over timed passes */
+  int64_t phase_spans[WF_N_PHASES];   /* timed spans (one per phase and level) */
 } wf_timing;
 
 /* ---- waafle_genecaller (waafle_genecaller.py:107-233) -------------------------------
@@ -258,6 +280,7 @@ const char* wf_last_error(const wf_ctx* ctx);
 int wf_set_stream(wf_ctx* ctx, void* hip_stream);     /* NULL = the context's own stream */
 int wf_set_lds_bytes(wf_ctx* ctx, int64_t bytes);     /* decision arena per workgroup (LDS) */
 int wf_set_mode(wf_ctx* ctx, int mode);               /* WF_MODE_LEVEL0 (default), _WAVES or _STAGED */
+int wf_set_option(wf_ctx* ctx, int option, int64_t value);   /* wf_option */
 int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* tax);
 int wf_score(wf_ctx* ctx, const wf_batch* batch, const wf_params* params, wf_result* out);
 int wf_synchronize(wf_ctx* ctx);

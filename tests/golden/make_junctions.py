@@ -56,14 +56,19 @@ CASES = [
     ("small", ["--min-overlap-sites", "80"], ["--min-junction-hits", "0"]),
     ("short", [], []),
     ("short", ["--min-overlap-sites", "200"], ["--min-junction-hits", "1"]),
+    # <= 0: every locus counts as hit (overlap 0 >= 0), including loci right of the pair
+    ("small", ["--min-overlap-sites", "0"], []),
+    ("short", ["--min-overlap-sites", "-3"], ["--min-junction-hits", "2"]),
 ]
 
 
 def tag(flags):
-    return "default" if not flags else "_".join(f.lstrip("-").replace(".", "p") for f in flags)
+    def one(f):   # "--flag" -> "flag", "-3" -> "m3"
+        return "m" + f[1:] if f[:1] == "-" and f[1:2].isdigit() else f.lstrip("-").replace(".", "p")
+    return "default" if not flags else "_".join(one(f) for f in flags)
 
 
-def main():
+def main(outdir=HERE):
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", PYTHONHASHSEED="0")
     with tempfile.TemporaryDirectory() as tmp:
         for set_name, jflags, qflags in CASES:
@@ -105,7 +110,7 @@ def main():
                       gene_hits=texts[".gene_hits.tsv"], site_hits=texts[".site_hits.tsv"],
                       junctions_stderr=run.stderr, qc_returncode=qrun.returncode,
                       qc_stderr=qrun.stderr, qc_pass=qc_text)
-            with gzip.open(os.path.join(HERE, name + ".junc.json.gz"), "wt") as fh:
+            with gzip.open(os.path.join(outdir, name + ".junc.json.gz"), "wt") as fh:
                 json.dump(fx, fh, sort_keys=True)
             print("{:50s} junction rows {:5d}  qc rc {} kept {}".format(
                 name, texts[".junctions.tsv"].count("\n") - 1, qrun.returncode,
@@ -113,4 +118,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(*sys.argv[1:2])

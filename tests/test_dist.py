@@ -111,7 +111,7 @@ def test_oversized_batch_is_scored_in_halves():
     def fake_once(self, sub, params):
         calls.append(sub.n_contigs)
         if sub.n_contigs > 7:
-            raise L.WaafleHipError(L.WF_E_BADINPUT, engine.SPLIT_MSG + " (split it)")
+            raise L.WaafleHipError(L.WF_E_TOOBIG, "too many hit-locus attachments (split it)")
         return inner(sub)
 
     s = engine.GpuScorer.__new__(engine.GpuScorer)
@@ -122,3 +122,46 @@ def test_oversized_batch_is_scored_in_halves():
     for f in engine.Results.__dataclass_fields__:
         a, b = getattr(got, f), getattr(want, f)
         assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), f
+
+
+def test_split_half_failure_names_batch_contig():
+    """A contig failing inside the second half of a split batch is reported by its index
+    in the whole batch (the half-relative index named the wrong contig)."""
+    from waafle_amd import synth
+    data = synth.generate(n=20, genes=5, clades=30, seed=12)
+    batch, tax = synth.to_batch(data, with_codes=False)
+    inner = _oracle_scorer(data, tax)
+    bad_name = batch.contig_names[13]
+
+    def fake_once(self, sub, params):
+        if sub.n_contigs > 6:
+            raise L.WaafleHipError(L.WF_E_TOOBIG, "too many hit-locus attachments (split it)")
+        if bad_name in sub.contig_names:
+            err = L.WaafleHipError(L.WF_E_RUNAWAY, "runaway")
+            err.contigs = np.array([list(sub.contig_names).index(bad_name)])
+            raise err
+        return inner(sub)
+
+    s = engine.GpuScorer.__new__(engine.GpuScorer)
+    s._score_once = fake_once.__get__(s)
+    with pytest.raises(L.WaafleHipError) as ei:
+        s.score(batch, None)
+    assert ei.value.code == L.WF_E_RUNAWAY
+    assert list(ei.value.contigs) == [13]
+
+
+def test_other_errors_do_not_split():
+    from waafle_amd import synth
+    data = synth.generate(n=10, genes=5, clades=30, seed=13)
+    batch, _ = synth.to_batch(data, with_codes=False)
+    calls = []
+
+    def fake_once(self, sub, params):
+        calls.append(sub.n_contigs)
+        raise L.WaafleHipError(L.WF_E_BADINPUT, "too many hit-locus attachments")
+
+    s = engine.GpuScorer.__new__(engine.GpuScorer)
+    s._score_once = fake_once.__get__(s)
+    with pytest.raises(L.WaafleHipError):
+        s.score(batch, None)
+    assert calls == [10]                       # the code decides, not the message text

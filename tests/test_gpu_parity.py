@@ -25,12 +25,24 @@ FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n
           "n_meld2", "annot_hit", "pair_evals", "iterations", "status")
 
 
-@pytest.fixture(scope="module", params=["level0", "waves", "staged"])
+FORMS = {
+    "level0": dict(mode="level0"),
+    "waves": dict(mode="waves"),
+    "staged": dict(mode="staged"),
+    # every staged decision from the segment table (k_big_sparse, wf_sparse.h)
+    "sparse": dict(mode="staged", options={lib.OPT_SPARSE_BIG: 2}),
+    # every staged decision that outgrows a 4 KB arena in an HBM slot (k_decide_big)
+    "dense_big": dict(mode="staged", lds_bytes=4096, options={lib.OPT_SPARSE_BIG: 0}),
+}
+
+
+@pytest.fixture(scope="module", params=list(FORMS))
 def scorer(request):
     """Every execution form: the level-0 wave kernels with the staged kernels behind them
-    (default), the wave kernels carrying the roll-up levels too, and every contig through
-    the staged kernels."""
-    s = engine.GpuScorer(0, mode=request.param)
+    (default), the wave kernels carrying the roll-up levels too, every contig through the
+    staged kernels, and those with every decision in the segment-table form or in the
+    dense HBM-slot form."""
+    s = engine.GpuScorer(0, **FORMS[request.param])
     yield s
     s.close()
 
@@ -220,6 +232,8 @@ def test_full_size_cfg2_properties(scorer):
     b = scorer.score(batch, params)
     assert_same_results(a, b, batch)
     for kw in (dict(lds_bytes=8192),          # small decision arena: HBM decision slots
+               dict(lds_bytes=8192, options={lib.OPT_SPARSE_BIG: 0}),   # ... dense form only
+               dict(mode="staged", options={lib.OPT_SPARSE_BIG: 2}),   # segment-table form
                dict(lds_bytes=65536),         # large arena: every contig in LDS
                dict(mode="staged"), dict(mode="level0"), dict(mode="waves"),
                dict()):

@@ -46,6 +46,8 @@ struct wf_ctx {
   int64_t launches = 0;
   bool lds_set = false;            // wf_set_lds_bytes called: also the staged decision arena
   int mode = WF_MODE_LEVEL0;       // wf_set_mode
+  int sparse_big = 1;              // wf_set_option(WF_OPT_SPARSE_BIG)
+  int64_t att_limit = (int64_t(1) << 31) - 1;   // wf_set_option(WF_OPT_ATT_LIMIT)
   wf::StagedState* staged = nullptr;
   // --write-details
   bool details_on = false;
@@ -251,6 +253,23 @@ int wf_set_mode(wf_ctx* ctx, int mode) {
   return WF_OK;
 }
 
+int wf_set_option(wf_ctx* ctx, int option, int64_t value) {
+  if (!ctx) return WF_E_BADINPUT;
+  switch (option) {
+    case WF_OPT_SPARSE_BIG:
+      if (value < 0 || value > 2) return fail(ctx, WF_E_BADINPUT, "WF_OPT_SPARSE_BIG is 0, 1 or 2");
+      ctx->sparse_big = (int)value;
+      return WF_OK;
+    case WF_OPT_ATT_LIMIT:
+      if (value < 1 || value > (int64_t(1) << 31) - 1)
+        return fail(ctx, WF_E_BADINPUT, "WF_OPT_ATT_LIMIT %lld out of [1, 2^31 - 1]", (long long)value);
+      ctx->att_limit = value;
+      return WF_OK;
+    default:
+      return fail(ctx, WF_E_BADINPUT, "unknown option %d", option);
+  }
+}
+
 int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* t) {
   if (!ctx || !t) return WF_E_BADINPUT;
   if (t->n <= 0 || !t->parent || !t->depth || !t->sib_parent || !t->leaf_count)
@@ -349,6 +368,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
   if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
   wf::staged_set_level0(ctx->staged, ctx->mode != WF_MODE_STAGED, ctx->mode == WF_MODE_WAVES);
+  wf::staged_set_options(ctx->staged, ctx->sparse_big, ctx->att_limit);
   std::pair<int, int> el{-1, -1};
   if (ctx->timing) {
     if (take_event_pair(ctx, ctx->ev_lds) < 0) return fail(ctx, WF_E_HIP, "hipEventCreate failed");
@@ -358,7 +378,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   std::string err;
   const int rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->max_hits, b->n_hits, b->n_loci, ctx->stream,
                                   &err, ctx->details_on ? &ctx->det : nullptr);
-  if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : WF_E_HIP, "%s", err.c_str());
+  if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : (rc == WF_E_TOOBIG ? WF_E_TOOBIG : WF_E_HIP), "%s", err.c_str());
   if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
   ++ctx->launches;
   return WF_OK;
@@ -556,7 +576,9 @@ int wf_junctions(wf_ctx* ctx, const wf_jn_batch* b, const wf_jn_params* p, wf_jn
       return fail(ctx, WF_E_BADINPUT, "pair %lld contig out of range", (long long)i);
   wf::JnArgs a{};
   a.n_contigs = (int)N;
-  a.loc_forward = forward;
+  // the early exit past the pair's right end holds only while a disjoint locus misses
+  // (overlap 0 < min_sites); with --min-overlap-sites <= 0 every locus is hit (:277-286)
+  a.loc_forward = forward && p->min_overlap_sites > 0;
   a.n_pairs = NP;
   a.n_loci = NL;
   a.n_sites = S;
@@ -680,6 +702,8 @@ int wf_timing_enable(wf_ctx* ctx, int on) {
   ctx->ev_lds.clear();
   ctx->launches = 0;
   ctx->timing = on != 0;
+  if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
+  wf::staged_timing(ctx->staged, ctx->timing);
   return WF_OK;
 }
 
@@ -695,6 +719,8 @@ int wf_timing_read(wf_ctx* ctx, wf_timing* out) {
   }
   out->pass_ms = total;
   out->passes = (int64_t)ctx->ev_lds.size();
+  for (int i = 0; i < WF_N_PHASES; ++i) { out->phase_ms[i] = 0.0; out->phase_spans[i] = 0; }
+  if (ctx->staged) wf::staged_timing_read(ctx->staged, out->phase_ms, out->phase_spans, WF_N_PHASES);
   return WF_OK;
 }
 

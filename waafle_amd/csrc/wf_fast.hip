@@ -1079,10 +1079,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
   }
 }
 
+// Resident k_wave workgroups per CU.  One value per process (every device is a gfx950 with
+// the same kernel image); the static's initialisation is thread-safe (C++11), so contexts on
+// several host threads may call this concurrently.
 template <int CAP, bool FULL>
 int blocks_per_cu() {
-  static int n = -1;                                   // per process: one kernel image
-  if (n < 0) {
+  static const int n = [] {
     const int bytes = (int)sizeof(WaveSmem<CAP, FULL>);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wave<CAP, FULL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
@@ -1090,8 +1092,8 @@ int blocks_per_cu() {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_wave<CAP, FULL>), 64,
                                                      bytes) != hipSuccess || b < 1)
       b = 1;
-    n = b;
-  }
+    return b;
+  }();
   return n;
 }
 

@@ -65,6 +65,7 @@ struct SArgs {
   int32_t* act_next; int64_t* act_base_next;      // raised contigs (next level)
   unsigned long long* counters;  // [0] next active << 40 | next attachments, [2] big count
   int32_t* big_list;             // contigs whose decision state needs an HBM slot
+  int32_t* big2_list;            // ... of those, the ones k_big_sparse declines (counters[1])
   int32_t* two_list;             // (rank, contig) pairs that need explain_two (counters[5])
   int32_t* one_list;             // (rank, contig) pairs for the dense explain_one workgroup
                                  // (counters[6]); null: every active contig goes there
@@ -94,6 +95,7 @@ struct SArgs {
   const int4* lut;               // (start, length, parent adds) per leaf
   int64_t dec_lds_bytes;         // LDS arena of the decision workgroup
   int sort_cap;                  // per-contig LDS sort capacity (power of 2; 0: device radix sort)
+  int force_big;                 // WF_OPT_SPARSE_BIG 2: every staged decision to k_big_sparse
   const unsigned long long* in_counts;   // this level's counts on the device (null: the
                                          // kernel arguments are exact)
 };
@@ -112,7 +114,8 @@ hipError_t launch_genecall(const GcArgs& a, int cus, hipStream_t s);
 // waafle_junctions (wf_junctions.hip): read-pair coverage and junction support
 struct JnArgs {
   int n_contigs;
-  int loc_forward;                         // every locus has start <= end (early exit ok)
+  int loc_forward;                         // every locus has start <= end and min_sites > 0
+                                           // (early exit past the pair's right end ok)
   int64_t n_pairs, n_loci, n_sites;        // n_sites = sum of (contig length + 1)
   int64_t min_sites;                       // --min-overlap-sites
   const int64_t* site_off;                 // [n_contigs + 1]
@@ -162,10 +165,17 @@ hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t
 StagedState* staged_create(int device);
 void staged_destroy(StagedState* st);
 void staged_set_lds(StagedState* st, int64_t bytes);
+// context options (include/waafle_hip.h wf_option): the segment-table decision for contigs
+// that outgrow the LDS arena, and the attachments one call accepts (more: WF_E_TOOBIG)
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit);
+// per-phase timing (wf_phase): HIP events around each phase of each level, read back at the
+// end of every staged_score call into the accumulators (reset by staged_timing(st, on))
+void staged_timing(StagedState* st, bool on);
+void staged_timing_read(const StagedState* st, double* ms, int64_t* spans, int n);
 // wave kernels (wf_fast.hip) first; rollup: they also carry the roll-up levels
 void staged_set_level0(StagedState* st, bool on, bool rollup);
-// Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2 with
-// the message in *err (-1 bad input, -2 HIP failure).
+// Runs the staged path for one batch on stream `s` (synchronises on it); 0 or -1/-2/-7
+// with the message in *err (-1 bad input, -2 HIP failure, -7 WF_E_TOOBIG).
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t n_hits,
                  int64_t n_loci, hipStream_t s, std::string* err, DetailsSink* det = nullptr);
 

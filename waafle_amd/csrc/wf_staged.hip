@@ -754,158 +754,6 @@ __global__ void k_seg_combine(const SArgs S, int64_t n_keys) {
 }
 
 
-// ---- flat explain_one (orgscorer.py:407-429, 585-597, 621-631) -------------------------
-// For --weak-loci ignore/penalize and <= 64 loci, the one-clade search needs no per-contig
-// workgroup: per-locus maxes are atomics over segments, each clade run (the clade's
-// segments, sorted by locus) scores itself, the best rank is an atomic max of its bits
-// (ranks are >= 0) and ties go to the larger clade id, like the sorted-order policy.
-__global__ void k_flat_maxes(const SArgs S, int64_t n_keys) {
-  const KArgs& K = S.k;
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= seg_count(S, n_keys)) return;
-  const int2 cg = S.seg_cg[s];
-  if (cg.x == K.unknown) return;
-  const double v = S.seg_mean[s];
-  if (!(v > 0.0)) return;
-  const int cr = S.seg_crank[s];
-  const int c = S.act ? S.act[cr] : cr;
-  atomicMax(reinterpret_cast<unsigned long long*>(&S.lmax[K.loc_off[c] + cg.y]), dbits(v));
-}
-
-__global__ void k_flat_prep(const SArgs S, int n_act, int level) {
-  const KArgs& K = S.k;
-  const int cr = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cr >= n_act) return;
-  const int c = S.act ? S.act[cr] : cr;
-  const int64_t l0 = K.loc_off[c];
-  const int G = (int)(K.loc_off[c + 1] - l0);
-  const int H = (int)(K.hit_off[c + 1] - K.hit_off[c]);
-  S.c_best[cr] = 0;
-  S.c_bestcl[cr] = -1;
-  S.c_nopt[cr] = 0;
-  if (H == 0 || G == 0) { S.c_gu[cr] = -1; return; }   // never evaluated (orgscorer.py:959)
-  uint64_t um = 0;
-  for (int g = 0; g < G; ++g) {
-    const double m = __longlong_as_double((long long)S.lmax[l0 + g]);
-    if (K.p.weak != 0 || m >= K.p.kmin) um |= 1ull << g;
-  }
-  const int Gu = __popcll(um);
-  S.c_umask[cr] = um;
-  if (Gu == 0) {
-    S.c_gu[cr] = -1;
-    if (level > 0) {                                     // np.min of an empty array upstream
-      K.iters[c] = (int16_t)min(level + 1, 32767);
-      K.status[c] = WF_E_EMPTYMASK;
-    }                                                    // level 0: skipped contig
-    return;
-  }
-  S.c_gu[cr] = Gu;
-}
-
-
-__device__ __forceinline__ bool run_start(const SArgs& S, int s) {
-  return s == 0 || S.seg_crank[s] != S.seg_crank[s - 1] || S.seg_cg[s].x != S.seg_cg[s - 1].x;
-}
-
-// pass 0: crit/rank of each clade run (Contig.score, orgscorer.py:447-461), best rank;
-// pass 1: best clade (ties -> larger id) and the options within --range (meld members)
-__global__ void k_flat_runs(const SArgs S, int64_t n_keys, int pass) {
-  const KArgs& K = S.k;
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ns = seg_count(S, n_keys);
-  if (s >= ns || !run_start(S, s)) return;
-  const int cr = S.seg_crank[s];
-  const int Gu = S.c_gu[cr];
-  if (Gu <= 0) return;
-  const int clade = S.seg_cg[s].x;
-  double crit, rank;
-  if (pass == 0) {
-    uint64_t um = S.c_umask[cr];
-    int t = s;
-    crit = 0.0;
-    bool firstv = true;
-    auto next = [&]() -> double {
-      const int g = __builtin_ctzll(um);
-      um &= um - 1;
-      while (t < ns && S.seg_crank[t] == cr && S.seg_cg[t].x == clade && S.seg_cg[t].y < g) ++t;
-      const double v = (t < ns && S.seg_crank[t] == cr && S.seg_cg[t].x == clade && S.seg_cg[t].y == g)
-                           ? S.seg_mean[t] : 0.0;
-      crit = (firstv || v < crit) ? v : crit;
-      firstv = false;
-      return v;
-    };
-    rank = np_sum_seq(Gu, next) / (double)Gu;
-    S.run_crit[s] = crit;
-    S.run_rank[s] = rank;
-    if (crit >= K.p.k1) atomicMax(&S.c_best[cr], dbits(rank) + 1ull);
-    return;
-  }
-  crit = S.run_crit[s];
-  rank = S.run_rank[s];
-  if (!(crit >= K.p.k1)) return;
-  const unsigned long long b = S.c_best[cr];
-  if (dbits(rank) + 1ull == b) atomicMax(&S.c_bestcl[cr], clade);
-  if (K.p.dis1 == 1) {
-    const double br = __longlong_as_double((long long)(b - 1ull));
-    if ((br - rank) <= K.p.range) {
-      const int c = S.act ? S.act[cr] : cr;
-      const int slot = atomicAdd(&S.c_nopt[cr], 1);
-      K.meld[2 * K.hit_off[c] + 2 * (int64_t)c + slot] = clade;
-    }
-  }
-}
-
-// One thread per contig: the result of a one-clade explanation, or hand-off to explain_two.
-__global__ void k_flat_finish(const SArgs S, int n_act, int level, int64_t n_keys) {
-  const KArgs& K = S.k;
-  const int cr = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cr >= n_act || S.c_gu[cr] <= 0) return;
-  const int c = S.act ? S.act[cr] : cr;
-  const int best = S.c_bestcl[cr];
-  if (best < 0) {                                       // no one-clade option: explain_two
-    const int slot = (int)atomicAdd(&S.counters[5], 1ull);
-    S.two_list[2 * slot] = cr;
-    S.two_list[2 * slot + 1] = c;
-    return;
-  }
-  const int m = K.p.dis1 == 1 ? S.c_nopt[cr] : 0;
-  const int64_t mbase = 2 * K.hit_off[c] + 2 * (int64_t)c;
-  if (K.p.dis1 == 1 && m == 0) {                        // negative --range upstream crash
-    K.status[c] = WF_E_BADINPUT;
-    return;
-  }
-  int lca = best;
-  if (K.p.dis1 == 1) {
-    lca = -1;
-    for (int i = 0; i < m; ++i) lca = lca2(K, lca, K.meld[mbase + i]);
-  }
-  // the best clade's run: binary search by clade among this contig's segments
-  int lo = S.crank_first[cr], hi = S.crank_first[cr + 1];
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (S.seg_cg[mid].x < best) lo = mid + 1; else hi = mid;
-  }
-  const int rs = lo;
-  const int64_t l0 = K.loc_off[c];
-  const int G = (int)(K.loc_off[c + 1] - l0);
-  const uint64_t um = S.c_umask[cr];
-  int t = rs;
-  const int se = S.crank_first[cr + 1];
-  for (int g = 0; g < G; ++g) {                         // set_synteny_one (:495-509)
-    while (t < se && S.seg_cg[t].x == best && S.seg_cg[t].y < g) ++t;
-    const double v = (t < se && S.seg_cg[t].x == best && S.seg_cg[t].y == g) ? S.seg_mean[t] : 0.0;
-    K.syn[l0 + g] = !((um >> g) & 1ull) ? '~' : (v >= K.p.k1 ? 'A' : '!');
-  }
-  K.call[c] = WF_CALL_NO_LGT;
-  K.crit[c] = S.run_crit[rs];
-  K.rank[c] = S.run_rank[rs];
-  K.c1[c] = lca;
-  K.c2[c] = -1;
-  K.nm1[c] = m;
-  K.iters[c] = (int16_t)(level + 1);
-  K.pair_evals[c] = level == 0 ? 0 : K.pair_evals[c];
-}
-
 // ---- explain_one, one wave per contig (orgscorer.py:407-429, 585-597, 621-631) ---------
 // The common case needs no gene-score matrix: the contig's segments (sorted by clade, then
 // locus) are staged in LDS, per-locus maxes are LDS atomics, and each clade run scores
@@ -937,7 +785,7 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
     if (K.hit_off[c + 1] == h0 || G == 0) continue;       // never evaluated (orgscorer.py:959)
     const int so = n_keys > 0 ? S.crank_first[cr] : 0;
     const int ns = (n_keys > 0 ? S.crank_first[cr + 1] : 0) - so;
-    if (ns > kOneCap || G > 64 || P.weak == 2) {
+    if (ns > kOneCap || G > 64 || P.weak == 2 || S.force_big) {
       if (lane == 0) {
         const int slot = (int)atomicAdd(&S.counters[6], 1ull);
         S.one_list[2 * slot] = cr;
@@ -1058,7 +906,7 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
 // one-clade explanation are queued for phase 2; 2: prologue + explain_two + roll-up.
 template <int NT, int PHASE>
 __device__ __forceinline__ bool decide_contig(const SArgs& S, int c, int cr, int level, char* abase, int64_t acap,
-                              Ctl& ctl, int64_t n_keys) {
+                              Ctl& ctl, int64_t n_keys, bool in_lds = true) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const int tid = threadIdx.x;
@@ -1103,7 +951,7 @@ __device__ __forceinline__ bool decide_contig(const SArgs& S, int c, int cr, int
     C.xcap = cls_bytes(Pmax);
     C.xws = ar.take<char>(C.xcap);
   }
-  if (!ar.fits()) {
+  if (!ar.fits() || (in_lds && S.force_big)) {
     if (tid == 0) K.need[c] = ar.used + 4096;
     __syncthreads();
     return false;
@@ -1264,20 +1112,25 @@ __global__ __launch_bounds__(NT, 2) void k_decide(const SArgs S, int n_act,
   }
 }
 
+// The dense decision in an HBM slot: the contigs k_big_sparse declined (big2_list,
+// counters[1]), or every contig of big_list (counters[2]) when the sparse form is off.
 __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int level,
-                                                          int64_t n_keys, int count) {
+                                                          int64_t n_keys, int use2) {
   int n_act_ = 0;
   lvl_counts(S, n_act_, n_keys);
-  count = (int)S.counters[2];
+  const int count = (int)S.counters[use2 ? 1 : 2];
+  const int32_t* list = use2 ? S.big2_list : S.big_list;
   __shared__ Ctl ctl;
   char* base = S.k.big_ws + (int64_t)blockIdx.x * S.k.slot_bytes;
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
-    const int cr = S.big_list[2 * i], c = S.big_list[2 * i + 1];
-    const bool ok = decide_contig<kBlock, 0>(S, c, cr, level, base, S.k.slot_bytes, ctl, n_keys);
+    const int cr = list[2 * i], c = list[2 * i + 1];
+    const bool ok = decide_contig<kBlock, 0>(S, c, cr, level, base, S.k.slot_bytes, ctl, n_keys, false);
     if (!ok && threadIdx.x == 0) S.k.status[c] = WF_E_NOMEM;
     __syncthreads();
   }
 }
+
+#include "wf_sparse.h"
 
 // Upper bound of decide_contig's arena for P clade rows (segments + 1) and G loci: every
 // take() of decide_contig with its 16-byte alignment, plus the mask-class workspace.
@@ -1337,9 +1190,17 @@ struct StagedState {
   Buf span_cnt, spans;                              // --write-details only
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
-  int big_slots = 512;
-  Buf lmax, c_gu, c_umask, c_best, c_bestcl, c_nopt, run_crit, run_rank;
-  Buf act0, act1, base0, base1, big_list, two_list, one_list, big_ws, tmp, pend, act_l0;
+  int sparse_big = 1;                // k_big_sparse before the HBM-slot decision (2: always)
+  int sparse_res = -1;               // resident k_big_sparse waves per CU
+  int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
+  // per-phase timing (wf_phase): event pool, this call's spans (phase, begin, end)
+  bool timing = false;
+  std::vector<hipEvent_t> tev;
+  int tev_used = 0;
+  std::vector<int> tspans;
+  double phase_ms[8] = {0};
+  int64_t phase_n[8] = {0};
+  Buf act0, act1, base0, base1, big_list, big2_list, two_list, one_list, big_ws, tmp, pend, act_l0;
   bool level0 = true;               // wave kernels (wf_fast.hip) before the staged kernels
   bool rollup = false;              // ... carrying the roll-up levels too
   bool lut_ready = false;
@@ -1353,6 +1214,7 @@ struct StagedState {
   unsigned long long* mbox_dev = nullptr;
   unsigned long long mbox_seq = 0;
   ~StagedState() {
+    for (hipEvent_t e : tev) (void)hipEventDestroy(e);
     if (mbox) (void)hipHostFree(mbox);
     if (host_counters) (void)hipHostFree(host_counters);
     if (host_lvl) (void)hipHostFree(host_lvl);
@@ -1393,6 +1255,56 @@ void staged_set_level0(StagedState* st, bool on, bool rollup) {
 void staged_set_lds(StagedState* st, int64_t bytes) {
   st->dec_lds = bytes;
   st->dec_lds_fixed = true;
+}
+
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit) {
+  st->sparse_big = sparse_big;
+  st->att_limit = att_limit;
+}
+
+void staged_timing(StagedState* st, bool on) {
+  st->timing = on;
+  for (int i = 0; i < 8; ++i) { st->phase_ms[i] = 0.0; st->phase_n[i] = 0; }
+}
+
+void staged_timing_read(const StagedState* st, double* ms, int64_t* spans, int n) {
+  for (int i = 0; i < n && i < 8; ++i) { ms[i] = st->phase_ms[i]; spans[i] = st->phase_n[i]; }
+}
+
+// An event recorded on `s` (from the context's pool); -1 when timing is off or it failed.
+static int t_mark(StagedState* st, hipStream_t s) {
+  if (!st->timing) return -1;
+  if (st->tev_used == (int)st->tev.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return -1;
+    st->tev.push_back(e);
+  }
+  const int i = st->tev_used;
+  if (hipEventRecord(st->tev[i], s) != hipSuccess) return -1;
+  ++st->tev_used;
+  return i;
+}
+
+static void t_span(StagedState* st, int phase, int b, int e) {
+  if (b < 0 || e < 0) return;
+  st->tspans.push_back(phase);
+  st->tspans.push_back(b);
+  st->tspans.push_back(e);
+}
+
+// this call's spans into the accumulators (the events are complete once the stream is)
+static hipError_t t_collect(StagedState* st, hipStream_t s) {
+  if (st->tspans.empty()) { st->tev_used = 0; return hipSuccess; }
+  hipError_t e = hipStreamSynchronize(s);
+  for (size_t i = 0; e == hipSuccess && i + 2 < st->tspans.size(); i += 3) {
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, st->tev[st->tspans[i + 1]], st->tev[st->tspans[i + 2]]);
+    st->phase_ms[st->tspans[i]] += ms;
+    st->phase_n[st->tspans[i]] += 1;
+  }
+  st->tspans.clear();
+  st->tev_used = 0;
+  return e;
 }
 
 #define ST_TRY(x)                                                                        \
@@ -1604,8 +1516,8 @@ static hipError_t select_list(StagedState* st, hipStream_t s, Flags flags, int32
                                        count, n, s);
 }
 
-int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t NH, int64_t NL,
-                 hipStream_t s, std::string* err, DetailsSink* det) {
+static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t NH,
+                      int64_t NL, hipStream_t s, std::string* err, DetailsSink* det) {
   const int N = k.n_contigs;
   if (N <= 0) return 0;
   if (!st->host_counters || !st->host_lvl || !st->lvl_ev[0] || !st->lvl_ev[1]) {
@@ -1624,10 +1536,8 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   sa.key_tb = bits_for(std::max(n_tax, 1));
   sa.lut_off = st->lut_off.as<int32_t>();
   sa.lut = st->lut.as<int4>();
-  // WF_DEC_LDS (measurement aid) fixes the arena like wf_set_lds_bytes; read before the
-  // kernels' copy of the arena size is taken, so the two always agree
-  if (const char* dl = getenv("WF_DEC_LDS")) { st->dec_lds = atoll(dl); st->dec_lds_fixed = true; }
   sa.dec_lds_bytes = st->dec_lds;
+  sa.force_big = st->sparse_big == 2 ? 1 : 0;
   // kernels take SArgs by value (kernarg segment): no argument uploads, and the pointers
   // loaded from it are known to be global (global_* instead of flat_* memory operations)
   ST_TRY(st->counters.ensure(s, 8 * sizeof(unsigned long long)));
@@ -1639,17 +1549,16 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   ST_TRY(st->att_off.ensure(s, (size_t)(N + 1) * sizeof(int64_t)));
   ST_TRY(st->red.ensure(s, 8 * sizeof(int64_t)));
   sa.catt_off = st->att_off.as<int64_t>();
-  static const char* ag_env = getenv("WF_ATT_GRID");        // blocks per CU (measurement aid)
-  const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * (ag_env ? atoi(ag_env) : 32));
+  const unsigned agrid = (unsigned)std::min<int64_t>(N, (int64_t)st->cus * 32);   // waves per CU
   ST_TRY(hipMemsetAsync(st->red.p, 0, 8 * sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt.as<int64_t>() + N, 0, sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt_leaves.as<int64_t>() + N, 0, sizeof(int64_t), s));
   // Fused level 0 (wf_fast.hip) unless --write-details (per-level records of every contig),
   // --weak-loci assign-unknown (virtual "Unknown" row) or HBM annotation slots are needed.
-  static const char* l0_env = getenv("WF_LEVEL0");          // 0: staged only (measurement aid)
   // (the wave kernels' 32-bit keys hold clade ids below 2^17)
   const bool level0 = st->level0 && !det && k.p.weak != 2 && (int64_t)max_loci * k.n_sys <= kAnnSlots &&
-                      sa.key_tb <= 17 && !(l0_env && l0_env[0] == '0');
+                      sa.key_tb <= 17;
+  const int t_waves = level0 ? t_mark(st, s) : -1;
   hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, sa.k);
   if (level0) {
     ST_TRY(st->pend.ensure(s, (size_t)N * 4));
@@ -1657,19 +1566,18 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     ST_TRY(launch_fast(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
                        st->cus, s));
     // the contigs it handed over (explain_two, roll-up) through the second wave form, its
-    // list and count built on the device (WF_FULL=0: straight to the staged kernels)
-    static const char* full_env = getenv("WF_FULL");
-    if (!(full_env && full_env[0] == '0')) {
-      ST_TRY(select_list(st, s, st->pend.as<int32_t>(), st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, N));
-      ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
-                         st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
-    }
+    // list and count built on the device
+    ST_TRY(select_list(st, s, st->pend.as<int32_t>(), st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, N));
+    ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
+                       st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
   } else {
     hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
                        st->cnt_leaves.as<int64_t>(),
                        reinterpret_cast<unsigned long long*>(st->red.as<int64_t>() + 1), nullptr, N);
   }
   ST_TRY(hipGetLastError());
+  t_span(st, WF_PHASE_WAVES, t_waves, t_mark(st, s));
+  const int t_attach = t_mark(st, s);
   {
     size_t t1 = 0, t2 = 0;
     ST_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, st->cnt.as<int64_t>(),
@@ -1719,8 +1627,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     hipLaunchKernelGGL(k_seed_info, dim3(1), dim3(64), 0, s, red, st->base0.as<int64_t>(), st->base1.as<int64_t>(), N);
     ST_TRY(hipGetLastError());
   }
-  static const char* mb_env = getenv("WF_MAILBOX");         // 0: copy + event (measurement aid)
-  const bool mailbox = st->mbox && !(mb_env && mb_env[0] == '0');
+  const bool mailbox = st->mbox != nullptr;
   if (mailbox) {
     ST_TRY(publish_sync(st, s, st->att_off.as<int64_t>() + N, 1, st->red.p, 8,
                         reinterpret_cast<unsigned long long*>(&hc[2])));
@@ -1734,17 +1641,16 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   if (n_first == 0) return 0;                       // the wave kernels finished every contig
   const int n_l0 = level0 ? (int)hc[7] : N, n_seed = level0 ? (int)hc[8] : 0;
   const int64_t keys_l0 = level0 ? hc[9] : hc[2], keys_seed = level0 ? hc[10] : 0;
-  // per-contig LDS sort when every contig's attachments fit one workgroup's LDS
-  // (WF_LDS_SORT=0: device radix sort of the whole level; measurement aid)
-  static const char* ls_env = getenv("WF_LDS_SORT");
+  // per-contig LDS sort when every contig's attachments fit one workgroup's LDS (else a
+  // device radix sort of the whole level)
   sa.sort_cap = 0;
-  if (!(ls_env && ls_env[0] == '0') && max_att <= kSortMax) {
+  if (max_att <= kSortMax) {
     sa.sort_cap = 2;
     while (sa.sort_cap < max_att) sa.sort_cap <<= 1;
   }
-  if (A >= (int64_t(1) << 31) - 1 || TLB >= (int64_t(1) << 31) - 1) {
+  if (A >= st->att_limit || TLB >= (int64_t(1) << 31) - 1) {
     *err = "too many hit-locus attachments for one batch (split it)";
-    return -1;
+    return WF_E_TOOBIG;
   }
   const size_t A1 = (size_t)std::max<int64_t>(A, 1), T1 = (size_t)std::max<int64_t>(TLB, 1);
   ST_TRY(st->att_lo.ensure(s, A1 * 4)); ST_TRY(st->att_hi.ensure(s, A1 * 4));
@@ -1761,15 +1667,11 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   ST_TRY(st->wave_list.ensure(s, A1 * 4));
   ST_TRY(st->crank_first.ensure(s, ((size_t)N + 1) * 4));
   ST_TRY(st->seg_cnt.ensure(s, ((size_t)N + 1) * 4));
-  ST_TRY(st->lmax.ensure(s, (size_t)std::max<int64_t>(NL, 1) * 8));
-  ST_TRY(st->c_gu.ensure(s, (size_t)N * 4)); ST_TRY(st->c_umask.ensure(s, (size_t)N * 8));
-  ST_TRY(st->c_best.ensure(s, (size_t)N * 8)); ST_TRY(st->c_bestcl.ensure(s, (size_t)N * 4));
-  ST_TRY(st->c_nopt.ensure(s, (size_t)N * 4));
-  ST_TRY(st->run_crit.ensure(s, A1 * 8)); ST_TRY(st->run_rank.ensure(s, A1 * 8));
   ST_TRY(st->satt_lohi.ensure(s, A1 * 8)); ST_TRY(st->satt_sc.ensure(s, A1 * 8));
   ST_TRY(st->act0.ensure(s, (size_t)N * 4)); ST_TRY(st->act1.ensure(s, (size_t)N * 4));
   ST_TRY(st->base0.ensure(s, (size_t)(N + 1) * 8)); ST_TRY(st->base1.ensure(s, (size_t)(N + 1) * 8));
   ST_TRY(st->big_list.ensure(s, (size_t)N * 8));
+  ST_TRY(st->big2_list.ensure(s, (size_t)N * 8));
   ST_TRY(st->two_list.ensure(s, (size_t)N * 8));
   ST_TRY(st->one_list.ensure(s, (size_t)N * 8));
   const int64_t n_annot = NL * k.n_sys;
@@ -1804,14 +1706,10 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   sa.seg_cnt = st->seg_cnt.as<int32_t>();
   ST_TRY(st->seg_len.ensure(s, A1 * 4));
   sa.seg_len = sa.sort_cap > 0 ? st->seg_len.as<int32_t>() : nullptr;   // set by k_seg_build
-  sa.lmax = st->lmax.as<uint64_t>();
-  sa.c_gu = st->c_gu.as<int32_t>(); sa.c_umask = st->c_umask.as<uint64_t>();
-  sa.c_best = st->c_best.as<unsigned long long>(); sa.c_bestcl = st->c_bestcl.as<int32_t>();
-  sa.c_nopt = st->c_nopt.as<int32_t>();
-  sa.run_crit = st->run_crit.as<double>(); sa.run_rank = st->run_rank.as<double>();
   sa.satt_lohi = st->satt_lohi.as<int2>(); sa.satt_sc = st->satt_sc.as<double>();
   sa.annot_best = st->annot_best.as<uint64_t>();
   sa.big_list = st->big_list.as<int32_t>();
+  sa.big2_list = st->big2_list.as<int32_t>();
   sa.two_list = st->two_list.as<int32_t>();
   sa.wave_list = st->wave_list.as<int32_t>();
   if (n_annot > 0 && (int64_t)max_loci * k.n_sys > kAnnSlots) {   // HBM annotation slots
@@ -1821,43 +1719,22 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   hipLaunchKernelGGL(k_att_contig<1>, dim3(std::min<unsigned>(agrid, (unsigned)n_first)), dim3(kAttNT), 0, s, sa,
                      nullptr, nullptr, nullptr, level0 ? st->act0.as<int32_t>() : nullptr, n_first);
   ST_TRY(hipGetLastError());
+  t_span(st, WF_PHASE_ATTACH, t_attach, t_mark(st, s));
 
-  // flat explain_one applies to --weak-loci ignore/penalize and <= 64 loci per contig
-  // (WF_FLAT_ONE=0 forces the per-contig workgroup form; measurement aid)
-  // (WF_FLAT_ONE=1 selects it; by default explain_one runs in the per-contig workgroup,
-  // which measured faster on cfg2/cfg3 once its arena is sized to the data)
-  static const char* flat_env = getenv("WF_FLAT_ONE");
-  const bool flat_one = k.p.weak != 2 && max_loci <= 64 && flat_env && flat_env[0] == '1';
-  // explain_one by one wave per contig (k_one), the dense workgroup only for the contigs it
-  // hands over (WF_ONE_FAST=0: dense workgroup for every contig; measurement aid)
-  static const char* one_env = getenv("WF_ONE_FAST");
-  const bool one_fast = !flat_one && !(one_env && one_env[0] == '0');
-  sa.one_list = one_fast ? st->one_list.as<int32_t>() : nullptr;
-  // short segments' means by one thread each in k_seg_rec (WF_THREAD_MEAN=0: every segment
-  // through the leaf kernels; measurement aid)
-  static const char* tm_env = getenv("WF_THREAD_MEAN");
-  const bool thread_mean = !(tm_env && tm_env[0] == '0');
+  // explain_one by one wave per contig (k_one); the dense workgroup (k_decide<3>) gets the
+  // contigs it hands over and the ones it leaves open (explain_two)
+  sa.one_list = st->one_list.as<int32_t>();
   // roll-up levels
   Buf* act[2] = {&st->act0, &st->act1};
   Buf* base[2] = {&st->base0, &st->base1};
-  // k_leaf grid: blocks per CU (WF_LEAF_GRID overrides; measurement aid)
-  static const char* lg_env = getenv("WF_LEAF_GRID");
-  const unsigned persistent = (unsigned)st->cus * (lg_env ? (unsigned)atoi(lg_env) : 8u);
-  // Level counters: level L counts into block L; level L+1 reads block L's word 0.  Level 0
-  // and the radix-sort path run synchronously (the host reads the counts after each level).
-  // Optionally, with the per-contig sort, levels >= 1 are pipelined: the host enqueues level L+1 with
-  // upper-bound grids (active sets only shrink) and the kernels read the real counts on the
-  // device, while the host waits for level L-1's count word -- the GPU never idles on a
-  // host round trip, and one empty level is enqueued at the end.
+  const unsigned leaf_grid = (unsigned)st->cus * 8u;   // k_leaf: persistent, 8 blocks per CU
+  // Level counters: level L counts into block L of lvl_ctr; the host reads them after each
+  // level through the mailbox
   const int n_lv = kMaxIter + 2;
   ST_TRY(st->lvl_ctr.ensure(s, (size_t)n_lv * 8 * sizeof(unsigned long long)));
   ST_TRY(hipMemsetAsync(st->lvl_ctr.p, 0, (size_t)n_lv * 8 * sizeof(unsigned long long), s));
   unsigned long long* lvl_ctr = st->lvl_ctr.as<unsigned long long>();
-  // Measured on cfg2: the host round trips it removes (~0.1 ms per pass) are paid back by
-  // the trailing empty level and the always-launched HBM-slot kernel, so it is opt-in
-  // (WF_PIPELINE=1) until a level has fewer launches.
-  static const char* pipe_env = getenv("WF_PIPELINE");
-  const bool pipelined = sa.sort_cap > 0 && !flat_one && !det && pipe_env && pipe_env[0] == '1' && n_l0 > 0;
+  sa.in_counts = nullptr;
   int n_act = n_l0;
   int64_t n_keys = keys_l0;
   int start = 0;
@@ -1878,10 +1755,19 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     ST_TRY(st->span_cnt.ensure(s, A1 * 4));
     ST_TRY(st->spans.ensure(s, A1 * 8));
   }
+  if (st->dec_lds > 64 * 1024) {
+    // per process, thread-safe initialisation (C++11 statics); every device is a gfx950
+    static const hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        160 * 1024 - 1024);
+    static const hipError_t attr5 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3, 256>),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                        160 * 1024 - 1024);
+    ST_TRY(attr3);
+    ST_TRY(attr5);
+  }
   for (int level = start; n_act > 0 && level <= kMaxIter; ++level) {
-    const bool async = pipelined && level >= 1;
     sa.counters = lvl_ctr + 8 * level;
-    sa.in_counts = async ? lvl_ctr + 8 * (level - 1) : nullptr;
     const int cur = level & 1;
     sa.act = level == 0 ? (level0 ? st->act_l0.as<int32_t>() : nullptr) : act[cur]->as<int32_t>();
     sa.act_base = level == 0 && !level0 ? nullptr : base[cur]->as<int64_t>();
@@ -1894,17 +1780,18 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
     hipcub::DoubleBuffer<int32_t> vbuf(st->vals0.as<int32_t>(), st->vals1.as<int32_t>());
     sa.keys = nullptr;
     sa.vals = nullptr;
+    const int t_seg = t_mark(st, s);
     if (n_keys > 0) {
       size_t need = st->tmp.n;
       if (sa.sort_cap > 0) {
         const size_t lds = (size_t)sa.sort_cap * 12;
         if (lds > 64 * 1024) {
-          static hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<64>),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)(kSortMax * 12));
-          static hipError_t attr4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<256>),
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        (int)(kSortMax * 12));
+          static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<64>),
+                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                             (int)(kSortMax * 12));
+          static const hipError_t attr4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<256>),
+                                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                              (int)(kSortMax * 12));
           ST_TRY(attr);
           ST_TRY(attr4);
         }
@@ -1928,8 +1815,7 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
       sa.vals = vbuf.Current();
       if (sa.sort_cap > 0) {
         need = st->tmp.n;
-        static const char* ss_env = getenv("WF_SMALL_SCAN");   // 0: device scan (measurement aid)
-        if (!(ss_env && ss_env[0] == '0') && n_act < 32 * kScanNT)   // <= 32 items a thread
+        if (n_act < 32 * kScanNT)        // <= 32 items a thread: one workgroup
           hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanNT), 0, s, sa.seg_cnt, sa.crank_first, n_act + 1);
         else
           ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_cnt, sa.crank_first, n_act + 1, s));
@@ -1946,73 +1832,37 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
       if (det)
         hipLaunchKernelGGL(k_seg_spans, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys,
                            st->span_cnt.as<int32_t>(), st->spans.as<int32_t>());
-      if (thread_mean) {
-        hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
-        // one wave per segment, a serial envelope sweep (shuffle chains): as many waves as
-        // fit (62 VGPRs, 2.8 KB LDS -> 32 per CU); roll-up levels have ~10^5 such segments
-        static const char* sw_env = getenv("WF_SEGWAVE_PER_CU");   // measurement aid
-        hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * (sw_env ? atoi(sw_env) : 32)), dim3(64), 0, s, sa);
-      }
-      else
-        hipLaunchKernelGGL(k_seg_rec<false>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
+      // short segments' means by one thread each; one wave per multi-attachment segment, a
+      // serial envelope sweep (62 VGPRs, 2.8 KB LDS -> 32 waves per CU; roll-up levels have
+      // ~10^5 such segments); the rest through the leaf kernels
+      hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 32), dim3(64), 0, s, sa);
       need = st->tmp.n;
       ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_nleaf, sa.leaf_off,
                                               (int)n_keys + 1, s));
       hipLaunchKernelGGL(k_leaf_expand, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
-      hipLaunchKernelGGL(k_leaf, dim3(persistent), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_leaf, dim3(leaf_grid), dim3(256), 0, s, sa, n_keys);
       hipLaunchKernelGGL(k_seg_combine, dim3(st->cus * 4), dim3(256), 0, s, sa, n_keys);
       ST_TRY(hipGetLastError());
     } else {
       sa.keys = kbuf.Current();
       sa.vals = vbuf.Current();
     }
-    if (st->dec_lds > 64 * 1024) {
-      static hipError_t attr1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<1>),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    160 * 1024 - 1024);
-      static hipError_t attr2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<2>),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    160 * 1024 - 1024);
-      static hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3>),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    160 * 1024 - 1024);
-      static hipError_t attr5 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3, 256>),
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                    160 * 1024 - 1024);
-      ST_TRY(attr1);
-      ST_TRY(attr2);
-      ST_TRY(attr3);
-      ST_TRY(attr5);
-    }
+    t_span(st, WF_PHASE_SEGMENTS, t_seg, t_mark(st, s));
     if (det) ST_TRY(details_level(st, sa, level, n_act, n_keys, s, det));
+    const int t_dec = t_mark(st, s);
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
-    if (flat_one) {
-      ST_TRY(hipMemsetAsync(sa.lmax, 0, (size_t)std::max<int64_t>(NL, 1) * 8, s));
-      hipLaunchKernelGGL(k_flat_maxes, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
-      hipLaunchKernelGGL(k_flat_prep, dim3(grid_for(n_act)), dim3(256), 0, s, sa, n_act, level);
-      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys, 0);
-      hipLaunchKernelGGL(k_flat_runs, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys, 1);
-      hipLaunchKernelGGL(k_flat_finish, dim3(grid_for(n_act)), dim3(256), 0, s, sa, n_act, level, n_keys);
-    } else if (one_fast) {
-      hipLaunchKernelGGL(k_one, dim3(std::min<int64_t>(n_act, (int64_t)st->cus * 32)), dim3(64), 0, s, sa,
-                         n_act, level, n_keys);
-    } else {
-      hipLaunchKernelGGL(k_decide<1>, dim3(dgrid), dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act,
-                         level, n_keys);
-    }
-    // explain_two for the contigs phase 1 left open (count on the device: a grid of
-    // rank-independent size, idle blocks exit at once)
+    hipLaunchKernelGGL(k_one, dim3(std::min<int64_t>(n_act, (int64_t)st->cus * 32)), dim3(64), 0, s, sa,
+                       n_act, level, n_keys);
+    // explain_two for the contigs k_one left open and the whole level for the ones it handed
+    // over (counts on the device: a grid of rank-independent size, idle blocks exit at once)
     // as many one-wave decision workgroups as the arena and 3 waves/SIMD (VGPRs) allow: the
     // explain_two contigs are latency chains, so they should all be in flight at once
     const unsigned dec_per_cu =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>(12, (160 * 1024) / std::max<int64_t>(st->dec_lds, 1)));
-    // above WF_DEC_WIDE_MAX active contigs a level's explain_two runs one wave per contig
-    // (more contigs in flight) instead of four (measurement aid; default: always four)
-    static const char* dw_env = getenv("WF_DEC_WIDE_MAX");
-    const bool wide = !dw_env || n_act <= atoi(dw_env);
-    // the four-wave form gets at most the workgroups resident at once (VGPRs allow 3 per
-    // CU at 137): each workgroup walks its contigs grid-stride, so a second, partial round
-    // of workgroups only lengthens the tail (WF_DEC_WIDE_PER_CU overrides; measurement aid)
+    // the four-wave form (roll-up levels: few open contigs, four waves each) gets at most the
+    // workgroups resident at once (VGPRs allow 3 per CU at 137): each workgroup walks its
+    // contigs grid-stride, so a second, partial round only lengthens the tail
     if (st->wide_res_lds != st->dec_lds) {           // per context: no shared host state
       int b = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_decide<3, 256>), 256,
@@ -2021,32 +1871,15 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
       st->wide_res = b;
       st->wide_res_lds = st->dec_lds;
     }
-    static const char* wp_env = getenv("WF_DEC_WIDE_PER_CU");
-    const unsigned wide_per_cu = wp_env ? (unsigned)std::max(1, atoi(wp_env))
-                                        : std::min<unsigned>(dec_per_cu, (unsigned)st->wide_res);
-    if (one_fast && level > 0 && wide)  // few open contigs: four waves each
+    const unsigned wide_per_cu = std::min<unsigned>(dec_per_cu, (unsigned)st->wide_res);
+    if (level > 0)
       hipLaunchKernelGGL((k_decide<3, 256>), dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * wide_per_cu)),
                          dim3(256), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
-    else if (one_fast)                  // k_one's overflow list and its open contigs
+    else
       hipLaunchKernelGGL(k_decide<3>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
                          dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
-    else
-      hipLaunchKernelGGL(k_decide<2>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
-                         dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     ST_TRY(hipGetLastError());
-    if (async) {
-      // HBM-slot decisions on the device count (slots sized for the largest contig)
-      hipLaunchKernelGGL(k_decide_big, dim3(st->big_slots), dim3(kBlock), 0, s, sa, level, n_keys, 0);
-      ST_TRY(hipGetLastError());
-      ST_TRY(hipMemcpyAsync(st->host_lvl + level, sa.counters, sizeof(unsigned long long),
-                            hipMemcpyDeviceToHost, s));
-      ST_TRY(hipEventRecord(st->lvl_ev[level & 1], s));
-      if (level >= 2) {                 // level `level`'s own count, produced by level - 1
-        ST_TRY(hipEventSynchronize(st->lvl_ev[(level - 1) & 1]));
-        if ((st->host_lvl[level - 1] >> 40) == 0) break;   // this level was empty: done
-      }
-      continue;                         // n_act / n_keys stay the upper bounds
-    }
+    t_span(st, WF_PHASE_DECIDE, t_dec, t_mark(st, s));
     if (mailbox) {
       ST_TRY(publish_sync(st, s, sa.counters, 4, nullptr, 0, st->host_counters));
     } else {
@@ -2055,38 +1888,68 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
       ST_TRY(spin_sync(s, st->lvl_ev[0]));
     }
     const int n_big = (int)st->host_counters[2];
-    if (n_big > 0) {
+    int n_dense = 0;                    // contigs that need the dense decision in an HBM slot
+    const int t_big = n_big > 0 ? t_mark(st, s) : -1;
+    if (n_big > 0 && st->sparse_big) {
+      // the decision from the segment table, one wave per contig (wf_sparse.h): as many
+      // waves as are resident at once (LDS-bound)
+      if (st->sparse_res < 0) {
+        int b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_big_sparse), 64, 0) !=
+                hipSuccess || b < 1)
+          b = 8;
+        st->sparse_res = b;
+      }
+      const int grid = std::min(n_big, st->cus * st->sparse_res);
+      hipLaunchKernelGGL(k_big_sparse, dim3(grid), dim3(64), 0, s, sa, level, n_keys);
+      ST_TRY(hipGetLastError());
+      if (mailbox) {
+        ST_TRY(publish_sync(st, s, sa.counters, 4, nullptr, 0, st->host_counters));
+      } else {
+        ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost, s));
+        ST_TRY(spin_sync(s, st->lvl_ev[0]));
+      }
+      n_dense = (int)st->host_counters[1];
+    } else {
+      n_dense = n_big;
+    }
+    if (n_dense > 0) {
       const int64_t slot = ((int64_t)st->host_counters[3] + 255) & ~int64_t(255);
       // HBM-slot workgroups: as many as are resident at once (135 VGPRs: 3 four-wave
-      // workgroups per CU); cfg5 (30 k stress contigs) measured 234.7 ms/pass at 2 per CU,
-      // 222.8 at 3, 264.5 at 4 (a second, partial round), 230.2 at 8.  WF_BIG_PER_CU
-      // overrides (measurement aid)
-      static const char* bp_env = getenv("WF_BIG_PER_CU");
-      const int slots = std::min(n_big, st->cus * (bp_env ? std::max(1, atoi(bp_env)) : 3));
+      // workgroups per CU); cfg5 (30 k stress contigs, round 2) measured 234.7 ms/pass at 2
+      // per CU, 222.8 at 3, 264.5 at 4 (a second, partial round), 230.2 at 8
+      const int slots = std::min(n_dense, st->cus * 3);
       ST_TRY(st->big_ws.ensure(s, (size_t)slot * slots));
       sa.k.big_ws = st->big_ws.as<char>();
       sa.k.slot_bytes = slot;
-      hipLaunchKernelGGL(k_decide_big, dim3(slots), dim3(kBlock), 0, s, sa, level, n_keys, n_big);
+      hipLaunchKernelGGL(k_decide_big, dim3(slots), dim3(kBlock), 0, s, sa, level, n_keys,
+                         (n_big > 0 && st->sparse_big) ? 1 : 0);
       ST_TRY(hipGetLastError());
       ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, s));
       ST_TRY(spin_sync(s, st->lvl_ev[0]));
     }
-    if (level == start && !st->dec_lds_fixed && n_big * 50 > n_act && st->dec_lds < 48 * 1024)
+    if (n_big > 0) t_span(st, WF_PHASE_BIG, t_big, t_mark(st, s));
+    if (level == start && !st->dec_lds_fixed && n_dense * 50 > n_act && st->dec_lds < 48 * 1024)
       st->dec_lds += 8 * 1024;   // adaptive arena: grows while > 2% of a first level overflow
     n_act = (int)(st->host_counters[0] >> 40);
     n_keys = (int64_t)(st->host_counters[0] & ((1ull << 40) - 1));
-    if (pipelined && level == 0 && n_act > 0) {
-      // HBM decision slots for the pipelined levels, sized for the largest possible contig
-      const int64_t slot = (arena_bound(max_att + 2, max_loci) + 255) & ~int64_t(255);
-      st->big_slots = st->cus * 2;
-      ST_TRY(st->big_ws.ensure(s, (size_t)slot * st->big_slots));
-      sa.k.big_ws = st->big_ws.as<char>();
-      sa.k.slot_bytes = slot;
-    }
   }
-  if (pipelined) ST_TRY(hipStreamSynchronize(s));
   return 0;
+}
+
+int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t NH, int64_t NL,
+                 hipStream_t s, std::string* err, DetailsSink* det) {
+  st->tspans.clear();
+  st->tev_used = 0;
+  int rc = staged_run(st, k, n_tax, max_loci, max_hits, NH, NL, s, err, det);
+  const hipError_t e = t_collect(st, s);
+  if (rc == 0 && e != hipSuccess) {
+    *err = std::string("phase timing: ") + hipGetErrorString(e);
+    rc = -2;
+  }
+  return rc;
 }
 
 #ifdef WF_STAMPS

@@ -101,13 +101,20 @@ def taxonomy_struct(t):
                         root=t.root, unknown=t.unknown)
 
 
-SPLIT_MSG = "too many hit-locus attachments for one batch"   # wf_staged.hip staged_score
+def rebase_error(err, first):
+    """A failure of a sub-batch starting at contig `first`: its failing-contig indices
+    (WaafleHipError.contigs, relative to the sub-batch) made relative to the whole batch."""
+    bad = getattr(err, "contigs", None)
+    if bad is not None and len(bad):
+        err.contigs = np.asarray(bad) + int(first)
+    return err
 
 
 class GpuScorer:
-    """One libwaafle_hip context on one device."""
+    """One libwaafle_hip context on one device.  `options`: {wf_option: value}
+    (lib.OPT_*), e.g. {lib.OPT_ATT_LIMIT: n} to make wf_score split smaller batches."""
 
-    def __init__(self, device=0, lds_bytes=None, mode=None):
+    def __init__(self, device=0, lds_bytes=None, mode=None, options=None):
         self.lib = L.load()
         h = C.c_void_p()
         rc = self.lib.wf_init(int(device), C.byref(h))
@@ -119,6 +126,8 @@ class GpuScorer:
             self._check(self.lib.wf_set_mode(self.h, MODES[mode] if isinstance(mode, str) else int(mode)))
         if lds_bytes:
             self._check(self.lib.wf_set_lds_bytes(self.h, int(lds_bytes)))
+        for opt, val in (options or {}).items():
+            self._check(self.lib.wf_set_option(self.h, int(opt), int(val)))
 
     def _check(self, rc):
         if rc != L.WF_OK:
@@ -129,17 +138,22 @@ class GpuScorer:
         self._check(self.lib.wf_set_taxonomy(self.h, C.byref(self._tax)))
 
     def score(self, batch, params):
-        """wf_score over the batch.  A batch whose hit-locus attachments (or their leaves)
-        overflow the device's 32-bit work indices is scored in contig halves (contigs are
-        independent, so the records are the same)."""
+        """wf_score over the batch.  A batch whose hit-locus attachments exceed one call's
+        limit (WF_E_TOOBIG: the device's 32-bit work indices, or WF_OPT_ATT_LIMIT) is
+        scored in contig halves (contigs are independent, so the records are the same);
+        a failing half reports its contigs relative to this batch."""
         try:
             return self._score_once(batch, params)
         except L.WaafleHipError as err:
-            if SPLIT_MSG not in str(err) or batch.n_contigs < 2:
+            if err.code != L.WF_E_TOOBIG or batch.n_contigs < 2:
                 raise
         mid = batch.n_contigs // 2
-        parts = [self.score(batch.slice(0, mid), params),
-                 self.score(batch.slice(mid, batch.n_contigs), params)]
+        parts = []
+        for a, b in ((0, mid), (mid, batch.n_contigs)):
+            try:
+                parts.append(self.score(batch.slice(a, b), params))
+            except L.WaafleHipError as err:
+                raise rebase_error(err, a)
         return Results.concat(parts, [0, int(batch.hit_off[mid])])
 
     def _score_once(self, batch, params):
@@ -268,8 +282,10 @@ def score(batch, tax, params, gpus=1, lds_bytes=None, devices=None):
                 parts[k] = s.score(batch.slice(a, b), params)
             finally:
                 s.close()
-        except Exception as exc:   # re-raised on the main thread
-            errors.append(exc)
+        except L.WaafleHipError as exc:   # re-raised on the main thread, batch-relative
+            errors.append((k, rebase_error(exc, a)))
+        except Exception as exc:
+            errors.append((k, exc))
 
     threads = [threading.Thread(target=work, args=(k, a, b)) for k, (a, b) in enumerate(bounds)]
     for t in threads:
@@ -277,5 +293,5 @@ def score(batch, tax, params, gpus=1, lds_bytes=None, devices=None):
     for t in threads:
         t.join()
     if errors:
-        raise errors[0]
+        raise min(errors, key=lambda e: e[0])[1]   # the first failing shard
     return Results.concat(parts, [int(batch.hit_off[a]) for a, _ in bounds])

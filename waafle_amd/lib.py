@@ -9,12 +9,16 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libwaafle_hip.so")
 
-WF_OK, WF_E_BADINPUT, WF_E_HIP, WF_E_RUNAWAY, WF_E_NOMEM, WF_E_STATE, WF_E_EMPTYMASK = \
-    0, -1, -2, -3, -4, -5, -6
+WF_OK, WF_E_BADINPUT, WF_E_HIP, WF_E_RUNAWAY, WF_E_NOMEM, WF_E_STATE, WF_E_EMPTYMASK, WF_E_TOOBIG = \
+    0, -1, -2, -3, -4, -5, -6, -7
 CALL_UNCLASSIFIED, CALL_NO_LGT, CALL_LGT = 0, 1, 2
 MODE_STAGED = 0
 MODE_LEVEL0 = 2
 MODE_WAVES = 3
+OPT_SPARSE_BIG, OPT_ATT_LIMIT = 1, 2           # wf_set_option
+PHASES = ("waves", "attach", "segments", "decide", "big")   # wf_phase 0..4
+N_PHASES = 8
+ABI_VERSION = 3
 
 _P = C.c_void_p
 
@@ -52,7 +56,12 @@ class WfResult(C.Structure):
 
 
 class WfTiming(C.Structure):
-    _fields_ = [("pass_ms", C.c_double), ("passes", C.c_int64)]
+    _fields_ = [("pass_ms", C.c_double), ("passes", C.c_int64),
+                ("phase_ms", C.c_double * N_PHASES), ("phase_spans", C.c_int64 * N_PHASES)]
+
+    def phases(self):
+        """{phase name: (ms summed over the timed passes, timed spans)}"""
+        return {n: (float(self.phase_ms[i]), int(self.phase_spans[i])) for i, n in enumerate(PHASES)}
 
 
 class WfGcBatch(C.Structure):
@@ -104,6 +113,7 @@ SIGNATURES = {
     "wf_set_stream": (C.c_int, [C.c_void_p, C.c_void_p]),
     "wf_set_lds_bytes": (C.c_int, [C.c_void_p, C.c_int64]),
     "wf_set_mode": (C.c_int, [C.c_void_p, C.c_int]),
+    "wf_set_option": (C.c_int, [C.c_void_p, C.c_int, C.c_int64]),
     "wf_set_taxonomy": (C.c_int, [C.c_void_p, C.POINTER(WfTaxonomy)]),
     "wf_score": (C.c_int, [C.c_void_p, C.POINTER(WfBatch), C.POINTER(WfParams),
                            C.POINTER(WfResult)]),
@@ -146,7 +156,7 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.wf_abi_version() != 2:
+    if lib.wf_abi_version() != ABI_VERSION:
         raise ImportError("libwaafle_hip ABI mismatch")
     _lib = lib
     return lib

@@ -413,3 +413,54 @@ def to_batch(data, min_gene_length=200.0, with_codes=True):
         loc_codes=codes, systems=["UniProt"], annot_value_ids=value_ids,
         annot_values=[values], hit_row=np.arange(data.n_hits, dtype=np.int64))
     return batch, tax
+
+
+def _write_chunk(args):
+    """Worker: chunk k of a chunked config rendered as text part files."""
+    name, k, outdir = args
+    write_text(generate_chunk(name, k), outdir, "part{:06d}".format(k))
+    return k
+
+
+def write_text_chunked(name, outdir, basename="synth", workers=None):
+    """Text rendering of a whole chunked config (the 4 files of write_text), its chunks
+    generated and written in parallel worker processes and concatenated in contig order.
+    Returns (paths, contigs, hits)."""
+    import shutil
+    spec = CONFIGS[name]
+    chunk = chunk_size(name)
+    ks = list(range((spec["n"] + chunk - 1) // chunk))
+    parts = os.path.join(outdir, basename + ".parts")
+    os.makedirs(parts, exist_ok=True)
+    if workers is None:
+        workers = min(16, len(os.sched_getaffinity(0)), len(ks))
+    jobs = [(name, k, parts) for k in ks]
+    if workers > 1:
+        import multiprocessing as mp
+        pool = mp.get_context("fork").Pool(workers)     # close + join (see generate_batch)
+        try:
+            pool.map(_write_chunk, jobs, chunksize=1)
+        finally:
+            pool.close()
+            pool.join()
+    else:
+        for j in jobs:
+            _write_chunk(j)
+    exts = (".fna", ".blastout", ".gff", ".taxonomy.tsv")
+    paths = [os.path.join(outdir, basename + e) for e in exts]
+    hits = 0
+    for e, dest in zip(exts, paths):
+        srcs = [os.path.join(parts, "part{:06d}{}".format(k, e)) for k in ks]
+        if e == ".taxonomy.tsv":
+            srcs = srcs[:1]                       # every chunk shares the config's taxonomy
+        with open(dest, "wb") as out:
+            for src in srcs:
+                with open(src, "rb") as fh:
+                    if e == ".blastout":
+                        data = fh.read()
+                        hits += data.count(b"\n")
+                        out.write(data)
+                    else:
+                        shutil.copyfileobj(fh, out)
+    shutil.rmtree(parts)
+    return paths, spec["n"], hits
