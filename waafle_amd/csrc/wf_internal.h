@@ -66,6 +66,7 @@ struct SArgs {
   unsigned long long* counters;  // [0] next active << 40 | next attachments, [2] big count
   int32_t* big_list;             // contigs whose decision state needs an HBM slot
   int32_t* big2_list;            // ... of those, the ones k_big_sparse declines (counters[1])
+  char* sp_ws;                   // k_big_sparse: HBM scratch, kSpSlot bytes per wave
   int32_t* two_list;             // (rank, contig) pairs that need explain_two (counters[5])
   int32_t* one_list;             // (rank, contig) pairs for the dense explain_one workgroup
                                  // (counters[6]); null: every active contig goes there

@@ -16,41 +16,60 @@
 //           potential clades (max over all loci >= k2, :603-605) counted in order and their
 //           ">= k2 on kept loci" masks entered into a class table in LDS
 //   classes crit(c1,c2) >= k2 <=> (m1 | m2) == keep: the test runs on class pairs; the
-//           classes that pass with some class hold the only clades that can form an option
-//   pass 3  row-parallel: those clades ("members": potential index, run start, mask,
-//           sister mask) into LDS
-//   pass 4  row-parallel, --sister-penalty on: for every parent of a member, the OR of the
-//           sister masks (score >= threshold, :717-744) of the present clades listed under
-//           it that are not members; member sisters are added per pair (the pair itself is
-//           excluded, as get_sisters(clade1) - {clade2} does)
-//   pairs   member pairs whose masks pass: rank (numpy order), best by (rank, pair index),
-//           eval_two and meld_two exactly as decide_two, rows read from the runs
+//           passing class pairs hold exactly the reference's candidate pairs
+//   pass 3  row-parallel: the clades of those classes ("members": potential index, run
+//           start, sister mask, listed parent) into the wave's HBM scratch, grouped by class
+//   pass 4  row-parallel, --sister-penalty on: for every parent of a member, per locus, how
+//           many present clades listed under it score >= the threshold (saturating at 3:
+//           one pair removes at most its two clades, get_sisters(c1) - {c2}, :717-744)
+//   pairs   the passing class pairs' members: rank (numpy order), best by (rank, pair
+//           index), eval_two and meld_two exactly as decide_two, rows read from the runs
 //
-// A contig whose classes, members or member parents outgrow the LDS tables, with > 63 loci
-// or with --weak-loci assign-unknown goes on to the dense decision (k_decide_big) instead.
-constexpr int kSpCls = 256;      // mask-class hash slots
-constexpr int kSpMem = 256;      // member clades
-constexpr int kSpPar = 128;      // parents of member clades
+// The passes stage the contig's segments through LDS 256 at a time (plus 64 ahead: a run
+// has at most 63 segments), so a run is walked in LDS and each step of a pass waits on one
+// batch of coalesced loads.  A contig whose classes or class pairs outgrow the LDS tables,
+// whose members outgrow the scratch, with > 63 loci or with --weak-loci assign-unknown goes
+// on to the dense decision (k_decide_big) instead.
+constexpr int kSpCls = 128;      // mask-class hash slots (at most 3/4 used)
+constexpr int kSpPairs = 256;    // passing class pairs
+constexpr int kSpMemG = 2048;    // member clades per contig (HBM scratch)
+constexpr int kSpParG = 4096;    // parent hash slots (HBM scratch), >= 2 * members
+constexpr int kSpWin = 256;      // segments staged per step
 constexpr int kSpMaxG = 63;      // loci per contig (mask bits; ~0 marks an empty class slot)
 
+struct SpMember {                // 32 B
+  int rs, cl, pi, sp;            // run start, clade, potential index, listed parent
+  unsigned long long mask, hm;   // >= k2 on kept loci; >= the sister threshold, all loci
+};
+struct SpParent {                // 32 B: parent id (~0: empty), clades >= threshold at a
+  unsigned long long key, c1, c2, c3;   // locus: >= 1, >= 2, >= 3 (bit per locus)
+};
+constexpr int64_t kSpSlot = (int64_t)kSpMemG * sizeof(SpMember) + (int64_t)kSpParG * sizeof(SpParent);
+
 struct SpShared {
+  int2 wcg[kSpWin + 64];                     // staged segments: (clade, locus) ...
+  double wv[kSpWin + 64];                    // ... and gene score
   unsigned long long mx[64];                 // per-locus max score bits (known clades)
   unsigned long long ckey[kSpCls];           // class mask (~0: empty)
   int ccnt[kSpCls];                          // potential clades in the class
-  int cint[kSpCls];                          // class passes with some class
+  int cint[kSpCls];                          // class is in a passing pair
   int cls[kSpCls];                           // occupied slots, compacted
-  unsigned long long mmask[kSpMem], mhm[kSpMem];
-  int mrs[kSpMem], mcl[kSpMem], mpi[kSpMem], msp[kSpMem];
-  int pkey[kSpPar];
-  unsigned long long por[kSpPar];
+  int coff[kSpCls], cfill[kSpCls];           // members of the class: first, filled
+  int pair[kSpPairs];                        // passing class pairs: a | b << 16 (a <= b)
+  int pref[kSpPairs + 1];                    // candidate-pair prefix
   double row[64];                            // one dense row (explain_one's best)
   int len[64];                               // locus lengths (ambiguous fraction)
   uint8_t syn[64];                           // best option's synteny
-  unsigned bm1[kSpMem / 32], bm2[kSpMem / 32];
-  int n_used, n_mem, n_par, n_in, all_ok, all_same, cnt;
+  unsigned bm1[kSpMemG / 32], bm2[kSpMemG / 32];   // members melded as clade 1 / 2
+  int n_used, n_pairs, n_in, all_ok, all_same, cnt, over;
 };
 
-// Value of clade run `cl` at locus g (0 without a segment); calls in ascending g.
+__device__ __forceinline__ int sp_hash(uint64_t m, int cap) {
+  return (int)((m * 0x9E3779B97F4A7C15ull) >> 40) & (cap - 1);
+}
+
+// Value of clade run `cl` at locus g (0 without a segment), from the segment table in HBM;
+// calls in ascending g.
 struct SpCursor {
   int t, cl, se;
   __device__ __forceinline__ double at(const SArgs& S, int g) {
@@ -67,20 +86,17 @@ struct SpCursor {
   }
 };
 
-// Bit summary of one clade run: loci at or above k1 / k2 / the sister threshold (a locus
-// without a segment scores 0.0 and is compared as such).
+// Bit summary of the run staged at window index w: loci at or above k1 / k2 / the sister
+// threshold (a locus without a segment scores 0.0 and is compared as such).
 struct SpRow {
   uint64_t mk1, mk2, mhs;
 };
 
-__device__ __forceinline__ SpRow sp_row(const SArgs& S, const DevParams& P, int rs, int se, int cl,
-                                        uint64_t allg) {
+__device__ __forceinline__ SpRow sp_row(const SpShared& sh, const DevParams& P, int w, int cl, uint64_t allg) {
   uint64_t cov = 0, k1 = 0, k2 = 0, hs = 0;
-  for (int t = rs; t < se; ++t) {
-    const int2 cg = S.seg_cg[t];
-    if (cg.x != cl) break;
-    const double v = S.seg_mean[t];
-    const uint64_t bit = 1ull << cg.y;
+  for (; sh.wcg[w].x == cl; ++w) {
+    const double v = sh.wv[w];
+    const uint64_t bit = 1ull << sh.wcg[w].y;
     cov |= bit;
     if (v >= P.k1) k1 |= bit;
     if (v >= P.k2) k2 |= bit;
@@ -94,25 +110,56 @@ __device__ __forceinline__ SpRow sp_row(const SArgs& S, const DevParams& P, int 
   return r;
 }
 
-// Runs of the contig's segments [so, se) in clade order, one per lane: f(is_start, t, clade)
+// numpy-order mean over the kept loci of the run staged at w (Contig.score, :447-461)
+__device__ __forceinline__ double sp_rank_w(const SpShared& sh, int w, int cl, uint64_t keep, int Gu) {
+  uint64_t m = keep;
+  auto next = [&]() -> double {
+    const int g = __builtin_ctzll(m);
+    m &= m - 1;
+    while (sh.wcg[w].x == cl && sh.wcg[w].y < g) ++w;
+    return (sh.wcg[w].x == cl && sh.wcg[w].y == g) ? sh.wv[w] : 0.0;
+  };
+  return (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+}
+
+// Runs of the contig's segments [so, se) in clade order, one per lane: f(is_start, t, w, cl)
 // is called by every lane of the wave for each 64-segment chunk (is_start false on lanes
-// that hold no run start), so f may use wave operations.
+// that hold no run start; t the segment, w its window index), so f may use wave operations.
+// The window holds kSpWin segments plus 64 ahead (clade -2 past the contig's end).
 template <class F>
-__device__ __forceinline__ void sp_rows(const SArgs& S, int so, int se, F f) {
+__device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, int se, F f) {
   const int lane = threadIdx.x & 63;
   int carry = -1;
-  for (int base = so; base < se; base += 64) {
-    const int t = base + lane;
-    const int cl = t < se ? S.seg_cg[t].x : -2;
-    int prev = __shfl_up(cl, 1, 64);
-    if (lane == 0) prev = carry;
-    carry = __shfl(cl, 63, 64);
-    f(t < se && cl != prev, t, cl);
+  for (int base = so; base < se; base += kSpWin) {
+    int2 cg[5];
+    double v[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int t = base + 64 * j + lane;
+      cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
+      v[j] = t < se ? S.seg_mean[t] : 0.0;
+    }
+    __syncthreads();                                 // the previous window is consumed
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      sh.wcg[64 * j + lane] = cg[j];
+      sh.wv[64 * j + lane] = v[j];
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int j = 0; j < kSpWin / 64; ++j) {
+      const int w = 64 * j + lane;
+      const int cl = sh.wcg[w].x;
+      const int prev = w == 0 ? carry : sh.wcg[w - 1].x;
+      f(base + w < se && cl != prev, base + w, w, cl);
+    }
+    carry = sh.wcg[kSpWin - 1].x;
   }
+  __syncthreads();
 }
 
 // (rank, crit) of a clade pair over the kept loci: numpy-order mean and min of the
-// per-locus max (orgscorer.py:447-461).
+// per-locus max (orgscorer.py:447-461), rows read from the segment table.
 __device__ __forceinline__ double sp_pair_rank(const SArgs& S, int ra, int ca, int rb, int cb, int se,
                                                uint64_t keep, int Gu) {
   SpCursor a{ra, ca, se}, b{rb, cb, se};
@@ -141,21 +188,35 @@ __device__ __forceinline__ double sp_pair_crit(const SArgs& S, int ra, int ca, i
   return m;
 }
 
-__device__ __forceinline__ int sp_par_slot(const SpShared& sh, int p) {
-  for (int i = 0; i < sh.n_par; ++i)
-    if (sh.pkey[i] == p) return i;
-  return -1;
+// parent table (open addressing, capacity pcap, a power of 2)
+__device__ __forceinline__ const SpParent* sp_par_find(const SpParent* tab, int pcap, int p) {
+  for (int h = sp_hash((uint64_t)p, pcap), n = 0; n < pcap; h = (h + 1) & (pcap - 1), ++n) {
+    const unsigned long long k = tab[h].key;
+    if (k == (unsigned long long)p) return &tab[h];
+    if (k == ~0ull) return nullptr;
+  }
+  return nullptr;
 }
 
-// eval_two (wf_device.h, G <= 64 form) for members u, v (u's potential index < v's): the
-// synteny masks from the two runs, swap rule, direction, LGT filters, sister penalty.
-__device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& sh, int u, int v, int se,
-                                               int G, uint64_t ign, bool cmp, uint8_t* out, int& same) {
+// Loci where a clade listed under parent entry e, other than clades X and Y, scores >= the
+// sister threshold: the saturating counts minus X's and Y's own contributions.
+__device__ __forceinline__ uint64_t sp_sisters(const SpParent* e, int p, const SpMember& X, const SpMember& Y) {
+  if (!e) return 0ull;
+  const uint64_t dx = X.sp == p ? X.hm : 0ull, dy = Y.sp == p ? Y.hm : 0ull;
+  const uint64_t sub2 = dx & dy, sub1 = dx ^ dy;
+  return e->c3 | (e->c2 & ~sub2) | (e->c1 & ~sub1 & ~sub2);
+}
+
+// eval_two (wf_device.h, G <= 64 form) for members A (potential index i) and B (j > i):
+// the synteny masks from the two runs, swap rule, direction, LGT filters, sister penalty.
+// c1p / c2p of the result are 0 (A) or 1 (B).
+__device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& sh, const SpMember& A,
+                                               const SpMember& B, const SpParent* par, int pcap, int se,
+                                               int G, uint64_t ign, bool cmp, uint8_t* out) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
-  const int ca = sh.mcl[u], cb = sh.mcl[v];
-  const bool unk = ca == K.unknown || cb == K.unknown;
-  SpCursor a{sh.mrs[u], ca, se}, b{sh.mrs[v], cb, se};
+  const bool unk = A.cl == K.unknown || B.cl == K.unknown;
+  SpCursor a{A.rs, A.cl, se}, b{B.rs, B.cl, se};
   uint64_t mm = 0, ma = 0, mb = 0;
   for (int g = 0; g < G; ++g) {
     const uint64_t bit = 1ull << g;
@@ -170,7 +231,7 @@ __device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& s
   const uint64_t ab = ma | mb;                     // "^[^A]*B" -> swap (:537-540)
   e.swapped = (ab && ((mb >> __builtin_ctzll(ab)) & 1ull)) ? 1 : 0;
   const uint64_t mA = e.swapped ? mb : ma, mB = e.swapped ? ma : mb;
-  same = 1;
+  e.same = 1;
   int64_t tot = 0, amb = 0;
   int state = 0;
   bool dir_ok = true;
@@ -178,7 +239,7 @@ __device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& s
     const uint64_t bit = 1ull << g;
     const uint8_t c = (ign & bit) ? '~' : (mm & bit) ? '*' : (mA & bit) ? 'A' : (mB & bit) ? 'B' : '!';
     if (out) out[g] = c;
-    if (cmp && sh.syn[g] != c) same = 0;
+    if (cmp && sh.syn[g] != c) e.same = 0;
     if (c == 'A' || c == 'B' || c == '*') {
       tot += sh.len[g];
       if (c == '*') amb += sh.len[g];
@@ -192,49 +253,61 @@ __device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& s
   }
   const int nA = __popcll(mA), nB = __popcll(mB);
   e.dir = (dir_ok && state == 3) ? 1 : 0;
-  e.c1p = e.swapped ? v : u;                       // member slots
-  e.c2p = e.swapped ? u : v;
-  e.same = same;
+  e.c1p = e.swapped ? 1 : 0;
+  e.c2p = e.swapped ? 0 : 1;
   e.ok = 1;
   if ((double)amb / (double)tot > P.amb_frac) e.ok = 0;           // :693-702
   if (P.clade_genes >= 0 && min(nA, nB) < P.clade_genes) e.ok = 0; // :704-708
-  const int X = sh.mcl[e.c1p], Y = sh.mcl[e.c2p];
+  const SpMember& X = e.swapped ? B : A;
+  const SpMember& Y = e.swapped ? A : B;
   if (P.clade_leaves >= 0) {                                       // :710-715
-    const int64_t lc = e.dir ? K.leaves[Y] : min(K.leaves[X], K.leaves[Y]);
+    const int64_t lc = e.dir ? K.leaves[Y.cl] : min(K.leaves[X.cl], K.leaves[Y.cl]);
     if (lc < P.clade_leaves) e.ok = 0;
   }
   if (P.sister_on && e.ok) {                                       // :717-744
-    const int px = K.parent[X], py = K.parent[Y];
-    const int sx = sp_par_slot(sh, px), sy = sp_par_slot(sh, py);
-    uint64_t fb = sx >= 0 ? sh.por[sx] : 0ull, fa = sy >= 0 ? sh.por[sy] : 0ull;
-    for (int q = 0; q < sh.n_mem; ++q) {
-      const int sp = sh.msp[q];
-      if (sp != px && sp != py) continue;
-      const int s = sh.mcl[q];
-      if (s == X || s == Y) continue;
-      if (sp == px) fb |= sh.mhm[q];
-      if (sp == py) fa |= sh.mhm[q];
-    }
+    const int px = K.parent[X.cl], py = K.parent[Y.cl];
+    const uint64_t fb = sp_sisters(sp_par_find(par, pcap, px), px, X, Y);   // sisters of X
+    const uint64_t fa = sp_sisters(sp_par_find(par, pcap, py), py, X, Y);   // sisters of Y
     if ((fb & mB) || (!e.dir && (fa & mA))) e.ok = 0;
   }
   return e;
 }
 
-// Member pairs (u, v), u < v in potential order, whose masks pass: f(u, v, i, j) on the lane
-// that owns the pair (i, j: potential indices, i < j).
+// Every candidate pair (the members of each passing class pair): f(u, v, mu, mv) on the
+// lane that owns it, mu's potential index below mv's.
 template <class F>
-__device__ __forceinline__ void sp_for_pairs(const SpShared& sh, uint64_t keep, F f) {
+__device__ __forceinline__ void sp_for_cands(const SpShared& sh, const SpMember* mem, F f) {
   const int lane = threadIdx.x & 63;
-  const int M = sh.n_mem;
-  for (int a = 0; a < M - 1; ++a) {
-    const uint64_t ma = sh.mmask[a];
-    const int pa = sh.mpi[a];
-    for (int b = a + 1 + lane; b < M; b += 64) {
-      if ((ma | sh.mmask[b]) != keep) continue;
-      const int pb = sh.mpi[b];
-      if (pa < pb) f(a, b, pa, pb);
-      else f(b, a, pb, pa);
+  const int np = sh.n_pairs;
+  const int T = sh.pref[np];
+  for (int x = lane; x < T; x += 64) {
+    int lo = 0, hi = np - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sh.pref[mid] <= x) lo = mid; else hi = mid - 1;
     }
+    const int a = sh.pair[lo] & 0xFFFF, b = sh.pair[lo] >> 16;
+    const int y = x - sh.pref[lo];
+    const int a0 = sh.coff[a], na = sh.ccnt[a];
+    int u, v;
+    if (a == b) {
+      // y-th (p, q), p < q, in row-major order: row p starts at p*(2na-p-1)/2
+      int plo = 0, phi = na - 2;
+      while (plo < phi) {
+        const int mid = (plo + phi + 1) >> 1;
+        if ((long long)mid * (2 * na - mid - 1) / 2 <= y) plo = mid; else phi = mid - 1;
+      }
+      const int rs = (int)((long long)plo * (2 * na - plo - 1) / 2);
+      u = a0 + plo;
+      v = a0 + plo + 1 + (y - rs);
+    } else {
+      const int nb = sh.ccnt[b];
+      u = a0 + y / nb;
+      v = sh.coff[b] + y % nb;
+    }
+    const SpMember mu = mem[u], mv = mem[v];
+    if (mu.pi < mv.pi) f(u, v, mu, mv);
+    else f(v, u, mv, mu);
   }
 }
 
@@ -268,10 +341,13 @@ __device__ __forceinline__ void sp_raise(const SArgs& S, int c, int64_t pair_eva
 }
 
 // Returns false when the contig must go to the dense decision (nothing written then).
-__device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, int cr, int level, int64_t n_keys) {
+// `ws`: this wave's HBM scratch (kSpSlot bytes).
+__device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws, int c, int cr, int level,
+                                         int64_t n_keys) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
   const int64_t h0 = K.hit_off[c];
   const int64_t l0 = K.loc_off[c];
   const int G = (int)(K.loc_off[c + 1] - l0);
@@ -283,6 +359,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
   const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
   const int iteration = level + 1;
   int64_t pair_evals = level == 0 ? 0 : K.pair_evals[c];
+  SpMember* mem = reinterpret_cast<SpMember*>(ws);
+  SpParent* par = reinterpret_cast<SpParent*>(ws + (int64_t)kSpMemG * sizeof(SpMember));
 
   // ---- pass 1: per-locus maxes over known clades, root present (:407-411) -------------
   sh.mx[lane] = 0;
@@ -290,15 +368,24 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
     const int ls = K.lstart[l0 + lane], le = K.lend[l0 + lane];
     sh.len[lane] = max(ls, le) - min(ls, le) + 1;
   }
-  for (int i = lane; i < kSpCls; i += 64) { sh.ckey[i] = ~0ull; sh.ccnt[i] = 0; sh.cint[i] = 0; }
-  if (lane == 0) { sh.n_used = 0; sh.n_mem = 0; sh.n_par = 0; sh.cnt = 0; }
+  for (int i = lane; i < kSpCls; i += 64) { sh.ckey[i] = ~0ull; sh.ccnt[i] = 0; sh.cint[i] = 0; sh.cfill[i] = 0; }
+  if (lane == 0) { sh.n_used = 0; sh.n_pairs = 0; sh.cnt = 0; sh.over = 0; }
   __syncthreads();
   bool root = false;
-  for (int t = so + lane; t < se; t += 64) {
-    const int2 cg = S.seg_cg[t];
-    const double v = S.seg_mean[t];
-    root |= cg.x == K.root;
-    if (cg.x != K.unknown && v > 0.0) atomicMax(&sh.mx[cg.y], dbits(v));
+  for (int base = so; base < se; base += 256) {
+    int2 cg[4];
+    double v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = base + 64 * j + lane;
+      cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
+      v[j] = t < se ? S.seg_mean[t] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      root |= cg[j].x == K.root;
+      if (cg[j].x >= 0 && cg[j].x != K.unknown && v[j] > 0.0) atomicMax(&sh.mx[cg[j].y], dbits(v[j]));
+    }
   }
   const bool root_present = __ballot(root) != 0ull;
   __syncthreads();
@@ -309,7 +396,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
   const int Gu = __popcll(keep);
   const bool no_rows = se == so;                    // Pn == 0
   if (level == 0 && keep == 0) return true;        // skipped contig (orgscorer.py:959)
-  if (Gu == 0) {                                  // np.min of an empty array upstream
+  if (Gu == 0) {                                    // np.min of an empty array upstream
     if (lane == 0) {
       K.iters[c] = (int16_t)min(iteration, 32767);
       K.pair_evals[c] = pair_evals;
@@ -323,20 +410,13 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
   long long bk = -1;
   int brs = -1;
   int Pp = 0;
-  sp_rows(S, so, se, [&](bool st, int t, int cl) {
+  sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
     bool pot = false;
     uint64_t cmask = 0;
     if (st) {
-      const SpRow r = sp_row(S, P, t, se, cl, allg);
+      const SpRow r = sp_row(sh, P, w, cl, allg);
       if ((r.mk1 & keep) == keep) {                 // crit >= k1 (:585-597)
-        SpCursor cur{t, cl, se};
-        uint64_t m = keep;
-        auto next = [&]() -> double {
-          const int g = __builtin_ctzll(m);
-          m &= m - 1;
-          return cur.at(S, g);
-        };
-        const double rank = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+        const double rank = sp_rank_w(sh, w, cl, keep, Gu);
         if (better(rank, cl, br, bk)) { br = rank; bk = cl; brs = t; }
       }
       pot = r.mk2 != 0ull;                          // max over all loci >= k2 (:603-605)
@@ -344,7 +424,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
     }
     Pp += __popcll(__ballot(pot));
     if (pot) {
-      int h = (int)(((cmask * 0x9E3779B97F4A7C15ull) >> 56) & (kSpCls - 1));
+      int h = sp_hash(cmask, kSpCls);
       for (int probe = 0; probe < kSpCls; ++probe) {
         const unsigned long long old = atomicCAS(&sh.ckey[h], ~0ull, (unsigned long long)cmask);
         if (old == ~0ull) atomicAdd(&sh.n_used, 1);
@@ -360,25 +440,17 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
     const int rs2 = __shfl_xor(brs, off, 64);
     if (better(r2, k2, br, bk)) { br = r2; bk = k2; brs = rs2; }
   }
-  __syncthreads();
 
   if (bk >= 0) {
     // meld_one (:621-631): options within --range of the best
     const int best = (int)bk;
     int acc = -1;
     if (P.dis1 == 1) {
-      sp_rows(S, so, se, [&](bool st, int t, int cl) {
+      sp_rows(S, sh, so, se, [&](bool st, int, int w, int cl) {
         if (!st) return;
-        const SpRow r = sp_row(S, P, t, se, cl, allg);
+        const SpRow r = sp_row(sh, P, w, cl, allg);
         if ((r.mk1 & keep) != keep) return;
-        SpCursor cur{t, cl, se};
-        uint64_t m = keep;
-        auto next = [&]() -> double {
-          const int g = __builtin_ctzll(m);
-          m &= m - 1;
-          return cur.at(S, g);
-        };
-        const double rank = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+        const double rank = sp_rank_w(sh, w, cl, keep, Gu);
         if ((br - rank) <= P.range) {
           K.meld[mbase + atomicAdd(&sh.cnt, 1)] = cl;
           acc = lca2(K, acc, cl);
@@ -387,7 +459,6 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc = lca2(K, acc, __shfl_xor(acc, off, 64));
     }
-    __syncthreads();
     const int m = sh.cnt;
     if (P.dis1 == 1 && m == 0) {                    // negative --range: get_lca() of nothing
       if (lane == 0) K.status[c] = WF_E_BADINPUT;
@@ -431,116 +502,121 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
   // ---- explain_two (:599-619) --------------------------------------------------------
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
   if (sh.n_used * 4 > kSpCls * 3) return false;    // too many classes for the table
-  // class pairs: a class passes when (ma | mb) == keep for some class b (itself: >= 2 clades)
+  // passing class pairs: (ma | mb) == keep (a == b: at least 2 clades)
   int U = 0;
   for (int base = 0; base < kSpCls; base += 64) {  // the occupied slots, compacted
     const int h = base + lane;
     const bool occ = sh.ckey[h] != ~0ull;
     const uint64_t w = __ballot(occ);
-    if (occ) sh.cls[U + __popcll(w & ((1ull << lane) - 1ull))] = h;
+    if (occ) sh.cls[U + __popcll(w & below)] = h;
     U += __popcll(w);
   }
   __syncthreads();
-  bool any = false;
   for (int ia = 0; ia < U; ++ia) {
     const int a = sh.cls[ia];
     const unsigned long long ma = sh.ckey[a];
-    bool pass = false;
-    for (int ib = lane; ib < U; ib += 64) {
+    for (int ib = ia + lane; ib < U; ib += 64) {
       const int b = sh.cls[ib];
-      if ((ma | sh.ckey[b]) != keep) continue;
-      if (a == b && sh.ccnt[a] < 2) continue;
-      pass = true;
-    }
-    if (__ballot(pass)) {
-      any = true;
-      if (lane == 0) sh.cint[a] = 1;
+      if ((ma | sh.ckey[b]) != keep || (a == b && sh.ccnt[a] < 2)) continue;
+      const int q = atomicAdd(&sh.n_pairs, 1);
+      if (q < kSpPairs) sh.pair[q] = min(a, b) | (max(a, b) << 16);
+      sh.cint[a] = 1;
+      sh.cint[b] = 1;
     }
   }
   __syncthreads();
   bool have_ok = false;
-  int M = 0;
-  if (any) {
-    int Mtot = 0;
-    for (int a = lane; a < kSpCls; a += 64) Mtot += sh.cint[a] ? sh.ccnt[a] : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) Mtot += __shfl_xor(Mtot, off, 64);
-    if (Mtot > kSpMem) return false;
-    // ---- pass 3: members (potential clades of passing classes), in potential order -----
+  if (sh.n_pairs > 0) {
+    if (sh.n_pairs > kSpPairs) return false;
+    // members of the passing classes, grouped by class (first member of each class)
+    if (lane == 0) {
+      int acc = 0;
+      for (int ia = 0; ia < U; ++ia) {
+        const int a = sh.cls[ia];
+        sh.coff[a] = acc;
+        if (sh.cint[a]) acc += sh.ccnt[a];
+      }
+      sh.cnt = acc;
+      int tot = 0;                                   // candidates per pair, prefix
+      for (int q = 0; q < sh.n_pairs; ++q) {
+        sh.pref[q] = tot;
+        const int a = sh.pair[q] & 0xFFFF, b = sh.pair[q] >> 16;
+        const long long n = a == b ? (long long)sh.ccnt[a] * (sh.ccnt[a] - 1) / 2
+                                   : (long long)sh.ccnt[a] * sh.ccnt[b];
+        tot = (int)min<long long>((long long)tot + n, 0x7FFFFFFF);
+      }
+      sh.pref[sh.n_pairs] = tot;
+    }
+    __syncthreads();
+    const int M = sh.cnt;
+    if (M > kSpMemG || sh.pref[sh.n_pairs] == 0x7FFFFFFF) return false;
+    // ---- pass 3: members (potential clades of passing classes) -------------------------
     int pbase = 0;
-    sp_rows(S, so, se, [&](bool st, int t, int cl) {
-      bool pot = false, mem = false;
+    sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
+      bool pot = false;
       SpRow r{0, 0, 0};
       if (st) {
-        r = sp_row(S, P, t, se, cl, allg);
+        r = sp_row(sh, P, w, cl, allg);
         pot = r.mk2 != 0ull;
-        if (pot) {
-          const uint64_t cmask = r.mk2 & keep;
-          int h = (int)(((cmask * 0x9E3779B97F4A7C15ull) >> 56) & (kSpCls - 1));
-          while (sh.ckey[h] != cmask) h = (h + 1) & (kSpCls - 1);
-          mem = sh.cint[h] != 0;
-        }
       }
       const uint64_t pb = __ballot(pot);
-      const int pi = pbase + __popcll(pb & ((1ull << lane) - 1ull));
+      const int pi = pbase + __popcll(pb & below);
       pbase += __popcll(pb);
-      if (mem) {
-        const int q = atomicAdd(&sh.n_mem, 1);
-        sh.mmask[q] = r.mk2 & keep;
-        sh.mhm[q] = r.mhs;
-        sh.mrs[q] = t;
-        sh.mcl[q] = cl;
-        sh.mpi[q] = pi;
-        sh.msp[q] = K.sibp[cl];
+      if (pot) {
+        const uint64_t cmask = r.mk2 & keep;
+        int h = sp_hash(cmask, kSpCls);
+        while (sh.ckey[h] != cmask) h = (h + 1) & (kSpCls - 1);
+        if (sh.cint[h]) {
+          SpMember m;
+          m.rs = t; m.cl = cl; m.pi = pi; m.sp = K.sibp[cl];
+          m.mask = cmask; m.hm = r.mhs;
+          mem[sh.coff[h] + atomicAdd(&sh.cfill[h], 1)] = m;
+        }
       }
     });
-    __syncthreads();
-    M = sh.n_mem;
+    // ---- pass 4: per parent of a member, clades listed under it scoring >= threshold ----
+    int pcap = 64;
+    while (pcap < 2 * M) pcap <<= 1;
     if (P.sister_on) {
-      // parents of the members (the parents whose listed children are their sisters)
-      if (lane == 0) {
-        int np = 0;
-        bool over = false;
-        for (int q = 0; q < M && !over; ++q) {
-          const int p = K.parent[sh.mcl[q]];
-          bool seen = false;
-          for (int i = 0; i < np; ++i) seen |= sh.pkey[i] == p;
-          if (seen) continue;
-          if (np == kSpPar) { over = true; break; }
-          sh.pkey[np] = p;
-          sh.por[np] = 0;
-          ++np;
-        }
-        sh.n_par = over ? -1 : np;
-      }
+      for (int h = lane; h < pcap; h += 64) par[h].key = ~0ull;
+      __threadfence_block();
       __syncthreads();
-      if (sh.n_par < 0) return false;
-      // ---- pass 4: sister masks of the non-member clades under those parents ----------
-      sp_rows(S, so, se, [&](bool st, int t, int cl) {
+      for (int q = lane; q < M; q += 64) {             // the members' parents
+        const int p = K.parent[mem[q].cl];
+        for (int h = sp_hash((uint64_t)p, pcap);; h = (h + 1) & (pcap - 1)) {
+          const unsigned long long old = atomicCAS(&par[h].key, ~0ull, (unsigned long long)p);
+          if (old == ~0ull) { par[h].c1 = 0; par[h].c2 = 0; par[h].c3 = 0; }
+          if (old == ~0ull || old == (unsigned long long)p) break;
+        }
+      }
+      __threadfence_block();
+      __syncthreads();
+      sp_rows(S, sh, so, se, [&](bool st, int, int w, int cl) {
         if (!st) return;
         const int sp = K.sibp[cl];
-        const int slot = sp >= 0 ? sp_par_slot(sh, sp) : -1;
-        if (slot < 0) return;
-        const SpRow r = sp_row(S, P, t, se, cl, allg);
-        if (r.mhs == 0ull) return;
-        if (r.mk2 != 0ull) {                        // a member itself? (added per pair)
-          const uint64_t cmask = r.mk2 & keep;
-          int h = (int)(((cmask * 0x9E3779B97F4A7C15ull) >> 56) & (kSpCls - 1));
-          while (sh.ckey[h] != cmask) h = (h + 1) & (kSpCls - 1);
-          if (sh.cint[h]) return;
+        const SpParent* e = sp >= 0 ? sp_par_find(par, pcap, sp) : nullptr;
+        if (!e) return;
+        const uint64_t hm = sp_row(sh, P, w, cl, allg).mhs;
+        if (!hm) return;
+        SpParent* x = const_cast<SpParent*>(e);
+        const uint64_t o1 = atomicOr(&x->c1, (unsigned long long)hm);   // saturating count
+        const uint64_t t2 = o1 & hm;
+        if (t2) {
+          const uint64_t o2 = atomicOr(&x->c2, (unsigned long long)t2);
+          if (o2 & t2) atomicOr(&x->c3, (unsigned long long)(o2 & t2));
         }
-        atomicOr(&sh.por[slot], (unsigned long long)r.mhs);
       });
-      __syncthreads();
+      __threadfence_block();
     }
+    __syncthreads();
 
-    // ---- pass 1 over the pairs: best by (rank, pair index) ----------------------------------
+    // ---- pass 1 over the candidates: best by (rank, pair index) ------------------------
     double pr = -__builtin_inf();
     long long pk = -1;
     int pu = -1, pv = -1;
-    sp_for_pairs(sh, keep, [&](int u, int v, int i, int j) {
-      const double r = sp_pair_rank(S, sh.mrs[u], sh.mcl[u], sh.mrs[v], sh.mcl[v], se, keep, Gu);
-      const long long key = (long long)i * Pp + j;
+    sp_for_cands(sh, mem, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
+      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu);
+      const long long key = (long long)mu.pi * Pp + mv.pi;
       if (better(r, key, pr, pk)) { pr = r; pk = key; pu = u; pv = v; }
     });
 #pragma unroll
@@ -550,29 +626,32 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
       const int u2 = __shfl_xor(pu, off, 64), v2 = __shfl_xor(pv, off, 64);
       if (better(r2, k2, pr, pk)) { pr = r2; pk = k2; pu = u2; pv = v2; }
     }
-    // every member is in some passing pair, so pk >= 0 here
-    int best_ok = 0, best_dir = 0, best_c1 = -1, best_c2 = -1;
+    // a passing class pair has at least one candidate, so pk >= 0 here
+    int best_ok = 0, best_dir = 0;
+    int best_c1 = -1, best_c2 = -1;
     double best_crit = 0.0;
     if (lane == 0) {
-      int same;
-      const OptEval e = sp_eval_two(S, sh, pu, pv, se, G, ign, false, sh.syn, same);
-      best_ok = e.ok; best_dir = e.dir; best_c1 = e.c1p; best_c2 = e.c2p;
-      best_crit = sp_pair_crit(S, sh.mrs[pu], sh.mcl[pu], sh.mrs[pv], sh.mcl[pv], se, keep);
+      const SpMember A = mem[pu], B = mem[pv];
+      const OptEval e = sp_eval_two(S, sh, A, B, par, pcap, se, G, ign, false, sh.syn);
+      best_ok = e.ok; best_dir = e.dir;
+      best_c1 = e.c1p ? pv : pu;
+      best_c2 = e.c2p ? pv : pu;
+      best_crit = sp_pair_crit(S, A.rs, A.cl, B.rs, B.cl, se, keep);
       sh.n_in = 0; sh.all_ok = 1; sh.all_same = 1;
     }
-    for (int i = lane; i < kSpMem / 32; i += 64) { sh.bm1[i] = 0; sh.bm2[i] = 0; }
+    for (int i = lane; i < kSpMemG / 32; i += 64) { sh.bm1[i] = 0; sh.bm2[i] = 0; }
     __syncthreads();
-    // ---- pass 2 over the pairs: options within --range get the LGT filters (:636-639) --
-    sp_for_pairs(sh, keep, [&](int u, int v, int, int) {
-      const double r = sp_pair_rank(S, sh.mrs[u], sh.mcl[u], sh.mrs[v], sh.mcl[v], se, keep, Gu);
-      if (!((pr - r) <= P.range)) return;
-      int same;
-      const OptEval e = sp_eval_two(S, sh, u, v, se, G, ign, true, nullptr, same);
+    // ---- pass 2 over the candidates: options within --range get the LGT filters --------
+    sp_for_cands(sh, mem, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
+      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu);
+      if (!((pr - r) <= P.range)) return;                       // (:636-639)
+      const OptEval e = sp_eval_two(S, sh, mu, mv, par, pcap, se, G, ign, true, nullptr);
       atomicAdd(&sh.n_in, 1);
       if (!e.ok) atomicAnd(&sh.all_ok, 0);
       if (!e.same) atomicAnd(&sh.all_same, 0);
-      atomicOr(&sh.bm1[e.c1p >> 5], 1u << (e.c1p & 31));
-      atomicOr(&sh.bm2[e.c2p >> 5], 1u << (e.c2p & 31));
+      const int q1 = e.c1p ? v : u, q2 = e.c2p ? v : u;
+      atomicOr(&sh.bm1[q1 >> 5], 1u << (q1 & 31));
+      atomicOr(&sh.bm2[q2 >> 5], 1u << (q2 & 31));
     });
     __syncthreads();
     // ---- meld_two (:640-669) ----------------------------------------------------------------
@@ -592,15 +671,16 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
       // the melded clades' LCAs (utils.py:401-411)
       int a1 = -1, a2 = -1;
       for (int q = lane; q < M; q += 64) {
-        if (in_bm(sh.bm1, q)) a1 = lca2(K, a1, sh.mcl[q]);
-        if (in_bm(sh.bm2, q)) a2 = lca2(K, a2, sh.mcl[q]);
+        if (in_bm(sh.bm1, q)) { a1 = lca2(K, a1, mem[q].cl); ++m1; }
+        if (in_bm(sh.bm2, q)) { a2 = lca2(K, a2, mem[q].cl); ++m2; }
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
         a1 = lca2(K, a1, __shfl_xor(a1, off, 64));
         a2 = lca2(K, a2, __shfl_xor(a2, off, 64));
+        m1 += __shfl_xor(m1, off, 64);
+        m2 += __shfl_xor(m2, off, 64);
       }
-      for (int w = 0; w < kSpMem / 32; ++w) { m1 += __popc(sh.bm1[w]); m2 += __popc(sh.bm2[w]); }
       lca1 = a1;
       lca2v = a2;
       bool keepit = true;
@@ -617,14 +697,13 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
     if (have_ok) {
       if (lane < G) K.syn[l0 + lane] = sh.syn[lane];
       if (kind == 2) {                               // melded clades, in member order
-        const uint64_t below = (1ull << lane) - 1ull;
         int o1 = 0, o2 = 0;
         for (int base = 0; base < M; base += 64) {
           const int q = base + lane;
           const bool in1 = in_bm(sh.bm1, q), in2 = in_bm(sh.bm2, q);
           const uint64_t w1 = __ballot(in1), w2 = __ballot(in2);
-          if (in1) K.meld[mbase + o1 + __popcll(w1 & below)] = sh.mcl[q];
-          if (in2) K.meld[mbase + m1 + o2 + __popcll(w2 & below)] = sh.mcl[q];
+          if (in1) K.meld[mbase + o1 + __popcll(w1 & below)] = mem[q].cl;
+          if (in2) K.meld[mbase + m1 + o2 + __popcll(w2 & below)] = mem[q].cl;
           o1 += __popcll(w1);
           o2 += __popcll(w2);
         }
@@ -634,8 +713,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
         K.crit[c] = best_crit;
         K.rank[c] = pr;
         K.dir[c] = (int8_t)best_dir;
-        K.c1[c] = (kind == 2) ? lca1 : sh.mcl[best_c1];
-        K.c2[c] = (kind == 2) ? lca2v : sh.mcl[best_c2];
+        K.c1[c] = (kind == 2) ? lca1 : mem[best_c1].cl;
+        K.c2[c] = (kind == 2) ? lca2v : mem[best_c2].cl;
         K.nm1[c] = (kind == 2) ? m1 : 0;
         K.nm2[c] = (kind == 2) ? m2 : 0;
         K.iters[c] = (int16_t)iteration;
@@ -659,13 +738,15 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, int c, in
 }
 
 // The contigs whose dense decision state outgrew the LDS arena (big_list, counters[2]):
-// one wave each; the ones sp_level declines go to big2_list (counters[1]) for k_decide_big.
+// one wave each with kSpSlot bytes of HBM scratch (S.sp_ws); the ones sp_level declines go
+// to big2_list (counters[1]) for k_decide_big.
 __global__ __launch_bounds__(64) void k_big_sparse(const SArgs S, int level, int64_t n_keys) {
   __shared__ SpShared sh;
+  char* ws = S.sp_ws + (int64_t)blockIdx.x * kSpSlot;
   const int count = (int)S.counters[2];
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const int cr = S.big_list[2 * i], c = S.big_list[2 * i + 1];
-    const bool ok = sp_level(S, sh, c, cr, level, n_keys);
+    const bool ok = sp_level(S, sh, ws, c, cr, level, n_keys);
     if (!ok && threadIdx.x == 0) {
       const int slot = (int)atomicAdd(&S.counters[1], 1ull);
       S.big2_list[2 * slot] = cr;

@@ -1201,6 +1201,7 @@ struct StagedState {
   double phase_ms[8] = {0};
   int64_t phase_n[8] = {0};
   Buf act0, act1, base0, base1, big_list, big2_list, two_list, one_list, big_ws, tmp, pend, act_l0;
+  Buf sp_ws;                        // k_big_sparse scratch (kSpSlot per wave)
   bool level0 = true;               // wave kernels (wf_fast.hip) before the staged kernels
   bool rollup = false;              // ... carrying the roll-up levels too
   bool lut_ready = false;
@@ -1901,6 +1902,8 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         st->sparse_res = b;
       }
       const int grid = std::min(n_big, st->cus * st->sparse_res);
+      ST_TRY(st->sp_ws.ensure(s, (size_t)grid * kSpSlot));
+      sa.sp_ws = st->sp_ws.as<char>();
       hipLaunchKernelGGL(k_big_sparse, dim3(grid), dim3(64), 0, s, sa, level, n_keys);
       ST_TRY(hipGetLastError());
       if (mailbox) {
