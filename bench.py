@@ -66,6 +66,10 @@ def parse_args():
     ap.add_argument("--k2-contigs", type=int, default=6250,
                     help="cfg5 contigs per rank for the k2 leg; 0 disables")
     ap.add_argument("--k2-steps", type=int, default=3)
+    ap.add_argument("--flags", default="",
+                    help="waafle_orgscorer flags for the main workload, e.g. '--weak-loci assign-unknown'")
+    ap.add_argument("--option", action="append", default=[],
+                    help="wf_set_option NAME=VALUE (sparse_big, att_limit); repeatable")
     ap.add_argument("--traffic-json", default=None)
     ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r03_k2_pmc.json"),
                     help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
@@ -384,8 +388,9 @@ def main():
     torch.cuda.set_device(dev)
 
     N, NH = batch.n_contigs, batch.n_hits
-    pdict = cli.param_dict(cli.parse_flags([]))
+    pdict = cli.param_dict(cli.parse_flags(args.flags.split()))
     params = engine.params_struct(pdict)
+    k2_params = engine.params_struct(cli.param_dict(cli.parse_flags([])))
     so = L.load()
     h = C.c_void_p()
     assert so.wf_init(local, C.byref(h)) == 0, "wf_init failed"
@@ -397,6 +402,10 @@ def main():
         chk(so.wf_set_lds_bytes(h, args.lds_bytes))
     if args.mode:
         chk(so.wf_set_mode(h, engine.MODES[args.mode]))
+    for o in args.option:
+        name, val = o.split("=")
+        chk(so.wf_set_option(h, {"sparse_big": L.OPT_SPARSE_BIG, "att_limit": L.OPT_ATT_LIMIT}[name],
+                             int(val)))
     tstruct = engine.taxonomy_struct(tax)
     chk(so.wf_set_taxonomy(h, C.byref(tstruct)))
     stream = torch.cuda.current_stream(dev)
@@ -440,9 +449,10 @@ def main():
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded generator, SURVEY §8(d) shapes)",
-        "config": {"workload": "{}: {} contigs x {} genes x {} clades, {} hits, default flags"
+        "config": {"workload": "{}: {} contigs x {} genes x {} clades, {} hits, {}"
                                .format(args.config, n_total, spec["genes"], spec["clades"],
-                                       NH * world if world == 1 else "~{}".format(NH * world)),
+                                       NH * world if world == 1 else "~{}".format(NH * world),
+                                       "flags " + args.flags if args.flags else "default flags"),
                    "contigs_total": n_total, "contigs_per_gpu": N, "hits_per_gpu": NH,
                    "parallelism": "dp{} (static contig split, no collective)".format(world)},
         "k2_pair_evals_per_sec": None,
@@ -463,6 +473,7 @@ def main():
                      "algorithmic_bytes_per_launch": b_alg,
                      "algorithmic_bytes_rule": "24 B/hit + 12 B/locus + 96 B/contig",
                      "traffic_detail": tsrc},
+        "options": args.option or None,
         "generate_s": t_gen,
         "cpu_baseline": None,
     }
@@ -470,7 +481,7 @@ def main():
         if ktax.names != tax.names:
             tk = engine.taxonomy_struct(ktax)
             chk(so.wf_set_taxonomy(h, C.byref(tk)))
-        result["k2"] = k2_leg(so, h, chk, kbatch, params, args.k2_steps, dist, dev, world,
+        result["k2"] = k2_leg(so, h, chk, kbatch, k2_params, args.k2_steps, dist, dev, world,
                               args.k2_pmc_json)
         result["k2_pair_evals_per_sec"] = result["k2"]["k2_pair_evals_per_sec"]
     if rank == 0 and world == 1 and args.pcie:

@@ -55,7 +55,8 @@ enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
  *   take the decision straight from the segment table, one wave per contig; 0: the dense
  *   matrix in an HBM slot (the only form for > 63 loci or --weak-loci assign-unknown);
  *   2: every decision the staged kernels make goes to the segment-table form (a test
- *   setting: it exercises that form on every input).
+ *   setting: it exercises that form on every input); 3: every contig the one-wave
+ *   explain_one (k_one) leaves open goes to the segment-table form.
  * WF_OPT_ATT_LIMIT: hit-locus attachments one wf_score call accepts (default and maximum
  *   2^31 - 1; more -> WF_E_TOOBIG, nothing scored). */
 enum wf_option { WF_OPT_SPARSE_BIG = 1, WF_OPT_ATT_LIMIT = 2 };

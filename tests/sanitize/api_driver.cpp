@@ -8,6 +8,7 @@
 // shrink (scratch reallocation), a second context on the same device, the genecaller and
 // the junction table.  Results are checked for internal consistency only (parity lives in
 // the pytest suite); the point is a clean sanitizer log.
+#include <sanitizer/lsan_interface.h>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -179,6 +180,29 @@ int main() {
   CHECK(wf_score(ctx, &v0, &p, &o0.r) == WF_OK);
   wf_timing tm{};
   CHECK(wf_timing_read(ctx, &tm) == WF_OK && tm.passes == 1 && tm.pass_ms > 0.0);
+  CHECK(tm.phase_spans[WF_PHASE_WAVES] == 1 && tm.phase_ms[WF_PHASE_WAVES] > 0.0);
+  CHECK(wf_timing_enable(ctx, 0) == WF_OK);
+  // options: validation, the attachment limit (WF_E_TOOBIG, nothing scored), the
+  // segment-table decision forced for every staged contig (same records)
+  CHECK(wf_set_option(ctx, WF_OPT_ATT_LIMIT, 0) == WF_E_BADINPUT);
+  CHECK(wf_set_option(ctx, WF_OPT_SPARSE_BIG, 4) == WF_E_BADINPUT);
+  CHECK(wf_set_option(ctx, 77, 1) == WF_E_BADINPUT);
+  {
+    Batch b = make_batch(1500, 7, 9, 11);
+    wf_batch v = view(b);
+    Out a(v), c(v);
+    CHECK(wf_set_mode(ctx, WF_MODE_STAGED) == WF_OK);
+    CHECK(wf_score(ctx, &v, &p, &a.r) == WF_OK);
+    CHECK(wf_set_option(ctx, WF_OPT_ATT_LIMIT, 5) == WF_OK);
+    CHECK(wf_score(ctx, &v, &p, &c.r) == WF_E_TOOBIG);
+    CHECK(wf_set_option(ctx, WF_OPT_ATT_LIMIT, (int64_t(1) << 31) - 1) == WF_OK);
+    CHECK(wf_set_option(ctx, WF_OPT_SPARSE_BIG, 2) == WF_OK);
+    CHECK(wf_score(ctx, &v, &p, &c.r) == WF_OK);
+    for (int i = 0; i < v.n_contigs; ++i)
+      CHECK(a.call[i] == c.call[i] && a.crit[i] == c.crit[i] && a.rank[i] == c.rank[i] && a.c1[i] == c.c1[i]);
+    CHECK(wf_set_option(ctx, WF_OPT_SPARSE_BIG, 1) == WF_OK);
+    CHECK(wf_set_mode(ctx, WF_MODE_LEVEL0) == WF_OK);
+  }
 
   // genecaller
   {
@@ -218,11 +242,20 @@ int main() {
   }
   wf_free(ctx);
   std::printf("api_driver ok check=%llu\n", check);
-  // Every check above has run and every context is freed.  Leave without the HIP/HSA
-  // runtimes' static destructors: under ASan they free runtime memory after the
-  // sanitizer's device-allocator hooks are gone, and ASan aborts in its own CHECK
-  // (sanitizer_allocator_device.h, dev_runtime_unloaded_) -- a teardown-order artefact,
-  // not a finding in this code.
+  // Every check above has run and every context is freed: leak-check now (the HIP/HSA
+  // runtimes' own allocations are still reachable from their globals, so only memory this
+  // code lost is reported; tests/sanitize/lsan.supp names the runtime libraries in case),
+  // then leave without the runtimes' static destructors: under ASan they free runtime
+  // memory after the sanitizer's device-allocator hooks are gone, and ASan aborts in its
+  // own CHECK (sanitizer_allocator_device.h, dev_runtime_unloaded_) -- a teardown-order
+  // artefact, not a finding in this code.
+  std::fflush(stdout);
+  if (__lsan_do_recoverable_leak_check() != 0) {
+    std::printf("api_driver: leaks reported\n");
+    std::fflush(stdout);
+    std::_Exit(23);
+  }
+  std::printf("api_driver leak check ok\n");
   std::fflush(stdout);
   std::_Exit(0);
 }

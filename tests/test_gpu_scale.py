@@ -138,7 +138,7 @@ def test_attachment_limit_splits_batch_like_unsplit():
 
 def test_option_validation():
     s = engine.GpuScorer(0)
-    for opt, val in ((lib.OPT_ATT_LIMIT, 0), (lib.OPT_ATT_LIMIT, 1 << 31), (lib.OPT_SPARSE_BIG, 3), (99, 1)):
+    for opt, val in ((lib.OPT_ATT_LIMIT, 0), (lib.OPT_ATT_LIMIT, 1 << 31), (lib.OPT_SPARSE_BIG, 4), (99, 1)):
         assert s.lib.wf_set_option(s.h, opt, val) == lib.WF_E_BADINPUT
     s.close()
 

@@ -540,6 +540,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     const int ci = xmap ? (it * kXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
     if (ci >= n_list) break;
     const int c = list ? list[ci] : ci;
+    // --weak-loci assign-unknown: the second form leaves every contig the first one handed
+    // over to the staged kernels (its pend / counts stand); they carry the virtual row
+    if (FULL && P.weak == 2) continue;
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
 #if WF_PREFETCH0
     // the first 64 hits' fields, issued together with the loci loads below (one global
@@ -975,7 +978,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
           for (int t = lane; t < ns; t += 64) {
             double rk = -1.0;
             const int clade = cg_of(F, t).x;
-            if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || (int)rc[t] == Gu)) {
+            // (assign-unknown: a real "Unknown" run is replaced by the virtual row, below)
+            if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || (int)rc[t] == Gu) &&
+                !(P.weak == 2 && clade == K.unknown)) {
               double crit, rnk;                            // (pruned: only runs on every unmasked locus)
               sparse_score(F, v, t, ns, clade, um, Gu, crit, rnk);
               if (crit >= P.k1) {
@@ -990,6 +995,22 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             const double r2 = __shfl_xor(br, off, 64), c2 = __shfl_xor(bcrit, off, 64);
             const long long k2 = __shfl_xor(bk, off, 64);
             if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
+          }
+          if (P.weak == 2) {
+            // assign-unknown (:416-418): the row "Unknown" = 1 - maxes is no option iff some
+            // locus has 1 - max < k1; a known clade's evaluated mean bounds that locus's max
+            // from below (1 - x is monotone), so one such locus settles it.  Otherwise -- or
+            // without a known option -- the staged kernels decide with the row.
+            bool settles = false;
+            for (int t = lane; t < ns; t += 64) {
+              const int2 cg = cg_of(F, t);
+              if (cg.x != K.unknown && v[t] >= 0.0 && (1.0 - v[t]) < P.k1) settles = true;
+            }
+            if (bk < 0 || __ballot(settles) == 0ull) {
+              staged = true;
+              outcome = 2;
+              break;
+            }
           }
           if (bk >= 0) {
             wave_sync();

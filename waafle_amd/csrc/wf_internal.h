@@ -96,7 +96,8 @@ struct SArgs {
   const int4* lut;               // (start, length, parent adds) per leaf
   int64_t dec_lds_bytes;         // LDS arena of the decision workgroup
   int sort_cap;                  // per-contig LDS sort capacity (power of 2; 0: device radix sort)
-  int force_big;                 // WF_OPT_SPARSE_BIG 2: every staged decision to k_big_sparse
+  int force_big;                 // WF_OPT_SPARSE_BIG 2: k_one hands every contig over
+  int route_sparse;              // WF_OPT_SPARSE_BIG 2, 3: every k_decide contig to k_big_sparse
   const unsigned long long* in_counts;   // this level's counts on the device (null: the
                                          // kernel arguments are exact)
 };

@@ -27,9 +27,11 @@
 //
 // The passes stage the contig's segments through LDS 256 at a time (plus 64 ahead: a run
 // has at most 63 segments), so a run is walked in LDS and each step of a pass waits on one
-// batch of coalesced loads.  A contig whose classes or class pairs outgrow the LDS tables,
-// whose members outgrow the scratch, with > 63 loci or with --weak-loci assign-unknown goes
-// on to the dense decision (k_decide_big) instead.
+// batch of coalesced loads.  --weak-loci assign-unknown (:416-418): the "Unknown" row is
+// 1 - maxes on every locus, kept in LDS and entered in clade order (a real "Unknown"
+// clade's run is replaced by it).  A contig whose classes or class pairs outgrow the LDS
+// tables, whose members outgrow the scratch, or with > 63 loci goes on to the dense
+// decision (k_decide_big) instead.
 constexpr int kSpCls = 128;      // mask-class hash slots (at most 3/4 used)
 constexpr int kSpPairs = 256;    // passing class pairs
 constexpr int kSpMemG = 2048;    // member clades per contig (HBM scratch)
@@ -58,6 +60,7 @@ struct SpShared {
   int pair[kSpPairs];                        // passing class pairs: a | b << 16 (a <= b)
   int pref[kSpPairs + 1];                    // candidate-pair prefix
   double row[64];                            // one dense row (explain_one's best)
+  double urow[64];                           // --weak-loci assign-unknown: 1 - maxes
   int len[64];                               // locus lengths (ambiguous fraction)
   uint8_t syn[64];                           // best option's synteny
   unsigned bm1[kSpMemG / 32], bm2[kSpMemG / 32];   // members melded as clade 1 / 2
@@ -68,11 +71,13 @@ __device__ __forceinline__ int sp_hash(uint64_t m, int cap) {
   return (int)((m * 0x9E3779B97F4A7C15ull) >> 40) & (cap - 1);
 }
 
-// Value of clade run `cl` at locus g (0 without a segment), from the segment table in HBM;
-// calls in ascending g.
+// Value of clade run `cl` at locus g (0 without a segment), from the segment table in HBM,
+// or of the virtual row `vrow` (run start < 0); calls in ascending g.
 struct SpCursor {
   int t, cl, se;
+  const double* vrow;
   __device__ __forceinline__ double at(const SArgs& S, int g) {
+    if (vrow) return vrow[g];
     while (t < se) {
       const int2 cg = S.seg_cg[t];
       if (cg.x != cl || cg.y >= g) break;
@@ -161,8 +166,8 @@ __device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, in
 // (rank, crit) of a clade pair over the kept loci: numpy-order mean and min of the
 // per-locus max (orgscorer.py:447-461), rows read from the segment table.
 __device__ __forceinline__ double sp_pair_rank(const SArgs& S, int ra, int ca, int rb, int cb, int se,
-                                               uint64_t keep, int Gu) {
-  SpCursor a{ra, ca, se}, b{rb, cb, se};
+                                               uint64_t keep, int Gu, const double* urow) {
+  SpCursor a{ra, ca, se, ra < 0 ? urow : nullptr}, b{rb, cb, se, rb < 0 ? urow : nullptr};
   uint64_t m = keep;
   auto next = [&]() -> double {
     const int g = __builtin_ctzll(m);
@@ -174,8 +179,8 @@ __device__ __forceinline__ double sp_pair_rank(const SArgs& S, int ra, int ca, i
 }
 
 __device__ __forceinline__ double sp_pair_crit(const SArgs& S, int ra, int ca, int rb, int cb, int se,
-                                               uint64_t keep) {
-  SpCursor a{ra, ca, se}, b{rb, cb, se};
+                                               uint64_t keep, const double* urow) {
+  SpCursor a{ra, ca, se, ra < 0 ? urow : nullptr}, b{rb, cb, se, rb < 0 ? urow : nullptr};
   double m = 0.0;
   bool first = true;
   for (uint64_t r = keep; r; r &= r - 1) {
@@ -216,7 +221,7 @@ __device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& s
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const bool unk = A.cl == K.unknown || B.cl == K.unknown;
-  SpCursor a{A.rs, A.cl, se}, b{B.rs, B.cl, se};
+  SpCursor a{A.rs, A.cl, se, A.rs < 0 ? sh.urow : nullptr}, b{B.rs, B.cl, se, B.rs < 0 ? sh.urow : nullptr};
   uint64_t mm = 0, ma = 0, mb = 0;
   for (int g = 0; g < G; ++g) {
     const uint64_t bit = 1ull << g;
@@ -352,7 +357,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   const int64_t l0 = K.loc_off[c];
   const int G = (int)(K.loc_off[c + 1] - l0);
   if (K.hit_off[c + 1] == h0 || G == 0) return true;   // never evaluated (orgscorer.py:959)
-  if (G > kSpMaxG || P.weak == 2) return false;
+  if (G > kSpMaxG) return false;
   const int so = n_keys > 0 ? S.crank_first[cr] : 0;
   const int se = n_keys > 0 ? S.crank_first[cr + 1] : 0;
   const uint64_t allg = (1ull << G) - 1ull;
@@ -394,7 +399,15 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   const uint64_t keep = __ballot(lane < G && (P.weak != 0 || mxv >= P.kmin));
   const uint64_t ign = allg & ~keep;
   const int Gu = __popcll(keep);
-  const bool no_rows = se == so;                    // Pn == 0
+  // --weak-loci assign-unknown: the virtual "Unknown" row 1 - maxes (:416-418) and its bits
+  const bool vu = P.weak == 2;
+  const double uval = 1.0 - mxv;
+  if (vu && lane < G) sh.urow[lane] = uval;
+  const uint64_t u_k1 = vu ? __ballot(lane < G && uval >= P.k1) : 0ull;
+  const uint64_t u_k2 = vu ? __ballot(lane < G && uval >= P.k2) : 0ull;
+  const uint64_t u_hs = vu ? __ballot(lane < G && uval >= P.sister_thr) : 0ull;
+  const bool u_pot = u_k2 != 0ull;                  // max over all loci >= k2 (:603-605)
+  const bool no_rows = se == so && !vu;             // Pn == 0
   if (level == 0 && keep == 0) return true;        // skipped contig (orgscorer.py:959)
   if (Gu == 0) {                                    // np.min of an empty array upstream
     if (lane == 0) {
@@ -409,11 +422,20 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   double br = -__builtin_inf();
   long long bk = -1;
   int brs = -1;
-  int Pp = 0;
+  int Pp = 0, upi = 0;                              // upi: potential clades before "Unknown"
+  auto ins_class = [&](uint64_t cmask) {
+    int h = sp_hash(cmask, kSpCls);
+    for (int probe = 0; probe < kSpCls; ++probe) {
+      const unsigned long long old = atomicCAS(&sh.ckey[h], ~0ull, (unsigned long long)cmask);
+      if (old == ~0ull) atomicAdd(&sh.n_used, 1);
+      if (old == ~0ull || old == cmask) { atomicAdd(&sh.ccnt[h], 1); break; }
+      h = (h + 1) & (kSpCls - 1);
+    }
+  };
   sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
     bool pot = false;
     uint64_t cmask = 0;
-    if (st) {
+    if (st && !(vu && cl == K.unknown)) {          // (a real "Unknown" run is replaced)
       const SpRow r = sp_row(sh, P, w, cl, allg);
       if ((r.mk1 & keep) == keep) {                 // crit >= k1 (:585-597)
         const double rank = sp_rank_w(sh, w, cl, keep, Gu);
@@ -423,15 +445,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       cmask = r.mk2 & keep;
     }
     Pp += __popcll(__ballot(pot));
-    if (pot) {
-      int h = sp_hash(cmask, kSpCls);
-      for (int probe = 0; probe < kSpCls; ++probe) {
-        const unsigned long long old = atomicCAS(&sh.ckey[h], ~0ull, (unsigned long long)cmask);
-        if (old == ~0ull) atomicAdd(&sh.n_used, 1);
-        if (old == ~0ull || old == cmask) { atomicAdd(&sh.ccnt[h], 1); break; }
-        h = (h + 1) & (kSpCls - 1);
-      }
-    }
+    upi += __popcll(__ballot(pot && cl < K.unknown));
+    if (pot) ins_class(cmask);
   });
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -440,6 +455,24 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     const int rs2 = __shfl_xor(brs, off, 64);
     if (better(r2, k2, br, bk)) { br = r2; bk = k2; brs = rs2; }
   }
+  // the virtual "Unknown" row: an option, a potential clade
+  double u_rank = 0.0;
+  const bool u_opt = vu && (u_k1 & keep) == keep;
+  if (u_opt) {
+    uint64_t m = keep;
+    auto next = [&]() -> double {
+      const int g = __builtin_ctzll(m);
+      m &= m - 1;
+      return sh.urow[g];
+    };
+    u_rank = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+    if (better(u_rank, K.unknown, br, bk)) { br = u_rank; bk = K.unknown; brs = -1; }
+  }
+  if (u_pot) {
+    Pp += 1;
+    if (lane == 0) ins_class(u_k2 & keep);
+  }
+  __syncthreads();
 
   if (bk >= 0) {
     // meld_one (:621-631): options within --range of the best
@@ -447,7 +480,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     int acc = -1;
     if (P.dis1 == 1) {
       sp_rows(S, sh, so, se, [&](bool st, int, int w, int cl) {
-        if (!st) return;
+        if (!st || (vu && cl == K.unknown)) return;
         const SpRow r = sp_row(sh, P, w, cl, allg);
         if ((r.mk1 & keep) != keep) return;
         const double rank = sp_rank_w(sh, w, cl, keep, Gu);
@@ -456,6 +489,11 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
           acc = lca2(K, acc, cl);
         }
       });
+      if (u_opt && lane == 0 && (br - u_rank) <= P.range) {
+        K.meld[mbase + atomicAdd(&sh.cnt, 1)] = K.unknown;
+        acc = lca2(K, acc, K.unknown);
+      }
+      __syncthreads();
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc = lca2(K, acc, __shfl_xor(acc, off, 64));
     }
@@ -465,9 +503,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       return true;
     }
     // the best clade's row: crit (min over kept loci) and set_synteny_one (:495-509)
-    sh.row[lane] = 0.0;
+    sh.row[lane] = brs < 0 && lane < G ? sh.urow[lane] : 0.0;
     __syncthreads();
-    {
+    if (brs >= 0) {
       const int t = brs + lane;
       if (t < se) {
         const int2 cg = S.seg_cg[t];
@@ -555,12 +593,12 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
       bool pot = false;
       SpRow r{0, 0, 0};
-      if (st) {
+      if (st && !(vu && cl == K.unknown)) {
         r = sp_row(sh, P, w, cl, allg);
         pot = r.mk2 != 0ull;
       }
       const uint64_t pb = __ballot(pot);
-      const int pi = pbase + __popcll(pb & below);
+      const int pi = pbase + __popcll(pb & below) + (u_pot && cl > K.unknown ? 1 : 0);
       pbase += __popcll(pb);
       if (pot) {
         const uint64_t cmask = r.mk2 & keep;
@@ -574,6 +612,19 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
         }
       }
     });
+    if (u_pot && lane == 0) {                        // the virtual "Unknown" row
+      const uint64_t cmask = u_k2 & keep;
+      int h = sp_hash(cmask, kSpCls);
+      while (sh.ckey[h] != cmask) h = (h + 1) & (kSpCls - 1);
+      if (sh.cint[h]) {
+        SpMember m;
+        m.rs = -1; m.cl = K.unknown; m.pi = upi; m.sp = K.sibp[K.unknown];
+        m.mask = cmask; m.hm = u_hs;
+        mem[sh.coff[h] + atomicAdd(&sh.cfill[h], 1)] = m;
+      }
+    }
+    __threadfence_block();
+    __syncthreads();
     // ---- pass 4: per parent of a member, clades listed under it scoring >= threshold ----
     int pcap = 64;
     while (pcap < 2 * M) pcap <<= 1;
@@ -591,13 +642,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       }
       __threadfence_block();
       __syncthreads();
-      sp_rows(S, sh, so, se, [&](bool st, int, int w, int cl) {
-        if (!st) return;
-        const int sp = K.sibp[cl];
-        const SpParent* e = sp >= 0 ? sp_par_find(par, pcap, sp) : nullptr;
+      auto count = [&](int sp, uint64_t hm) {
+        const SpParent* e = sp >= 0 && hm ? sp_par_find(par, pcap, sp) : nullptr;
         if (!e) return;
-        const uint64_t hm = sp_row(sh, P, w, cl, allg).mhs;
-        if (!hm) return;
         SpParent* x = const_cast<SpParent*>(e);
         const uint64_t o1 = atomicOr(&x->c1, (unsigned long long)hm);   // saturating count
         const uint64_t t2 = o1 & hm;
@@ -605,7 +652,14 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
           const uint64_t o2 = atomicOr(&x->c2, (unsigned long long)t2);
           if (o2 & t2) atomicOr(&x->c3, (unsigned long long)(o2 & t2));
         }
+      };
+      sp_rows(S, sh, so, se, [&](bool st, int, int w, int cl) {
+        if (!st || (vu && cl == K.unknown)) return;
+        const int sp = K.sibp[cl];
+        if (sp < 0) return;
+        count(sp, sp_row(sh, P, w, cl, allg).mhs);
       });
+      if (vu && lane == 0) count(K.sibp[K.unknown], u_hs);
       __threadfence_block();
     }
     __syncthreads();
@@ -615,7 +669,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     long long pk = -1;
     int pu = -1, pv = -1;
     sp_for_cands(sh, mem, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
-      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu);
+      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu, sh.urow);
       const long long key = (long long)mu.pi * Pp + mv.pi;
       if (better(r, key, pr, pk)) { pr = r; pk = key; pu = u; pv = v; }
     });
@@ -636,14 +690,14 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       best_ok = e.ok; best_dir = e.dir;
       best_c1 = e.c1p ? pv : pu;
       best_c2 = e.c2p ? pv : pu;
-      best_crit = sp_pair_crit(S, A.rs, A.cl, B.rs, B.cl, se, keep);
+      best_crit = sp_pair_crit(S, A.rs, A.cl, B.rs, B.cl, se, keep, sh.urow);
       sh.n_in = 0; sh.all_ok = 1; sh.all_same = 1;
     }
     for (int i = lane; i < kSpMemG / 32; i += 64) { sh.bm1[i] = 0; sh.bm2[i] = 0; }
     __syncthreads();
     // ---- pass 2 over the candidates: options within --range get the LGT filters --------
     sp_for_cands(sh, mem, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
-      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu);
+      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu, sh.urow);
       if (!((pr - r) <= P.range)) return;                       // (:636-639)
       const OptEval e = sp_eval_two(S, sh, mu, mv, par, pcap, se, G, ign, true, nullptr);
       atomicAdd(&sh.n_in, 1);

@@ -951,7 +951,7 @@ __device__ __forceinline__ bool decide_contig(const SArgs& S, int c, int cr, int
     C.xcap = cls_bytes(Pmax);
     C.xws = ar.take<char>(C.xcap);
   }
-  if (!ar.fits() || (in_lds && S.force_big)) {
+  if (!ar.fits() || (in_lds && S.route_sparse)) {
     if (tid == 0) K.need[c] = ar.used + 4096;
     __syncthreads();
     return false;
@@ -1190,7 +1190,7 @@ struct StagedState {
   Buf span_cnt, spans;                              // --write-details only
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
-  int sparse_big = 1;                // k_big_sparse before the HBM-slot decision (2: always)
+  int sparse_big = 1;                // WF_OPT_SPARSE_BIG (0 dense, 1 overflow, 2 all, 3 decisions)
   int sparse_res = -1;               // resident k_big_sparse waves per CU
   int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
   // per-phase timing (wf_phase): event pool, this call's spans (phase, begin, end)
@@ -1539,6 +1539,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   sa.lut = st->lut.as<int4>();
   sa.dec_lds_bytes = st->dec_lds;
   sa.force_big = st->sparse_big == 2 ? 1 : 0;
+  sa.route_sparse = st->sparse_big >= 2 ? 1 : 0;
   // kernels take SArgs by value (kernarg segment): no argument uploads, and the pointers
   // loaded from it are known to be global (global_* instead of flat_* memory operations)
   ST_TRY(st->counters.ensure(s, 8 * sizeof(unsigned long long)));
@@ -1554,11 +1555,10 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   ST_TRY(hipMemsetAsync(st->red.p, 0, 8 * sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt.as<int64_t>() + N, 0, sizeof(int64_t), s));
   ST_TRY(hipMemsetAsync(st->cnt_leaves.as<int64_t>() + N, 0, sizeof(int64_t), s));
-  // Fused level 0 (wf_fast.hip) unless --write-details (per-level records of every contig),
-  // --weak-loci assign-unknown (virtual "Unknown" row) or HBM annotation slots are needed.
+  // Fused level 0 (wf_fast.hip) unless --write-details (per-level records of every contig)
+  // or HBM annotation slots are needed.
   // (the wave kernels' 32-bit keys hold clade ids below 2^17)
-  const bool level0 = st->level0 && !det && k.p.weak != 2 && (int64_t)max_loci * k.n_sys <= kAnnSlots &&
-                      sa.key_tb <= 17;
+  const bool level0 = st->level0 && !det && (int64_t)max_loci * k.n_sys <= kAnnSlots && sa.key_tb <= 17;
   const int t_waves = level0 ? t_mark(st, s) : -1;
   hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, sa.k);
   if (level0) {
