@@ -19,7 +19,7 @@ def main():
     for r in csv.DictReader(open(files[0])):
         m = re.search(r"(k_\w+(<[^>]*>)?)", r["Kernel_Name"])
         acc[m.group(1) if m else r["Kernel_Name"][:30]][r["Counter_Name"]] += float(r["Counter_Value"])
-    print("rocprofv3 --pmc " + " ".join(COLS) + " over one cfg4 wf_score pass (" + d + ")")
+    print("rocprofv3 --pmc " + " ".join(COLS) + " summed over the 4 passes (1 warmup + 3 timed) of (" + d + ")")
     print("%-24s" % "kernel" + "".join("%20s" % c for c in COLS))
     for k, v in sorted(acc.items(), key=lambda x: -x[1]["SQ_WAVE_CYCLES"])[:14]:
         print("%-24s" % k[:24] + "".join("%20.4g" % v[c] for c in COLS))
