@@ -562,15 +562,25 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     const int Gs = min(G, kLoc0);
     // ---- loci (lane g), leaf-table bases ----
     int nl1 = 0;
+    int my_lo = 0, my_hi = -1;
     if (lane < Gs) {
       const int a = K.lstart[l0 + lane], b = K.lend[l0 + lane];
       const int len = max(a, b) - min(a, b) + 1;
-      F.lo[lane] = min(a, b);
+      my_lo = min(a, b);
+      my_hi = max(a, b);
+      F.lo[lane] = my_lo;
       F.len[lane] = len;
       F.st[lane] = K.lstrand[l0 + lane];
       if (len < kNpyBuf) nl1 = S.lut_off[len + 1] - S.lut_off[len];
       F.nl1[lane] = (int16_t)nl1;
     }
+    // loci ascending and disjoint (the usual GFF): with min_overlap > 0 a hit attaches only
+    // to the loci it overlaps (a disjoint pair scores 0 < min_overlap), which are a run found
+    // by binary search -- the attach loop then visits those, in GFF order, instead of every
+    // locus per hit
+    const int prev_hi = __shfl_up(my_hi, 1, 64);
+    const bool ordered = G <= kLoc0 && P.min_overlap > 0.0 &&
+                         __ballot(lane >= 1 && lane < Gs && my_lo <= prev_hi) == 0ull;
     int lut_total;
     const int lb = wave_excl_scan(nl1, &lut_total);
     F.lbase[lane] = (int16_t)min(lb, 32767);
@@ -612,7 +622,25 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       int n = 0;
       uint64_t am = 0;
-      if (h < h1 && scv >= P.min_scov) {
+      if (ordered) {
+        if (h < h1 && scv >= P.min_scov) {
+          int g = 0;                                 // first locus ending at or after qlo
+#pragma unroll
+          for (int b = 32; b > 0; b >>= 1) {
+            const int i = min(g + b, Gs) - 1;
+            if (g + b <= Gs && F.lo[i] + F.len[i] - 1 < qlo) g += b;
+          }
+          for (; g < Gs; ++g) {
+            const int lo = F.lo[g], len = F.len[g];
+            if (lo > qhi) break;
+            if (attaches(P, qlo, qhi, hs, lo, len, F.st[g])) {
+              ++n;
+              nl_sum += len < kNpyBuf ? F.nl1[g] : leaves_for(S, len);
+              am |= 1ull << g;
+            }
+          }
+        }
+      } else if (h < h1 && scv >= P.min_scov) {
         for (int g = 0; g < G; ++g) {
           int lo, len, st;
           if (g < kLoc0) {

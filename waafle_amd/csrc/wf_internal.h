@@ -98,6 +98,7 @@ struct SArgs {
   int sort_cap;                  // per-contig LDS sort capacity (power of 2; 0: device radix sort)
   int force_big;                 // WF_OPT_SPARSE_BIG 2: k_one hands every contig over
   int route_sparse;              // WF_OPT_SPARSE_BIG 2, 3: every k_decide contig to k_big_sparse
+  int sparse_on;                 // WF_OPT_SPARSE_BIG != 0: k_big_sparse runs
   const unsigned long long* in_counts;   // this level's counts on the device (null: the
                                          // kernel arguments are exact)
 };

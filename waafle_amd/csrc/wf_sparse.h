@@ -36,24 +36,33 @@ constexpr int kSpCls = 128;      // mask-class hash slots (at most 3/4 used)
 constexpr int kSpPairs = 256;    // passing class pairs
 constexpr int kSpMemG = 2048;    // member clades per contig (HBM scratch)
 constexpr int kSpParG = 4096;    // parent hash slots (HBM scratch), >= 2 * members
+constexpr int kSpDense = 16384;  // dense member rows (members x loci doubles, HBM scratch)
 constexpr int kSpWin = 256;      // segments staged per step
 constexpr int kSpMaxG = 63;      // loci per contig (mask bits; ~0 marks an empty class slot)
 
 struct SpMember {                // 32 B
-  int rs, cl, pi, sp;            // run start, clade, potential index, listed parent
-  unsigned long long mask, hm;   // >= k2 on kept loci; >= the sister threshold, all loci
+  int rs, cl, pi, sp;            // run start (-1: the virtual "Unknown" row), clade,
+                                 // potential index, listed parent
+  int h, pad;                    // class slot
+  unsigned long long hm;         // loci >= the sister threshold (all loci)
 };
 struct SpParent {                // 32 B: parent id (~0: empty), clades >= threshold at a
   unsigned long long key, c1, c2, c3;   // locus: >= 1, >= 2, >= 3 (bit per locus)
 };
-constexpr int64_t kSpSlot = (int64_t)kSpMemG * sizeof(SpMember) + (int64_t)kSpParG * sizeof(SpParent);
+// per-wave scratch: members (in the order found) | their positions grouped by class | parents
+// | the members' dense rows
+constexpr int64_t kSpOffGidx = (int64_t)kSpMemG * sizeof(SpMember);
+constexpr int64_t kSpOffPar = kSpOffGidx + (int64_t)kSpMemG * sizeof(int);
+constexpr int64_t kSpOffDense = kSpOffPar + (int64_t)kSpParG * sizeof(SpParent);
+constexpr int64_t kSpSlot = kSpOffDense + (int64_t)kSpDense * sizeof(double);
 
 struct SpShared {
   int2 wcg[kSpWin + 64];                     // staged segments: (clade, locus) ...
   double wv[kSpWin + 64];                    // ... and gene score
   unsigned long long mx[64];                 // per-locus max score bits (known clades)
   unsigned long long ckey[kSpCls];           // class mask (~0: empty)
-  int ccnt[kSpCls];                          // potential clades in the class
+  int cmany[kSpCls];                         // the class has at least 2 potential clades
+  int ccnt[kSpCls];                          // members of a passing class (pass 3)
   int cint[kSpCls];                          // class is in a passing pair
   int cls[kSpCls];                           // occupied slots, compacted
   int coff[kSpCls], cfill[kSpCls];           // members of the class: first, filled
@@ -89,6 +98,14 @@ struct SpCursor {
     }
     return 0.0;
   }
+};
+
+// A member's row for the pair evaluations: its dense copy in the scratch when the members'
+// rows fit it (independent loads), else read from the run (dependent loads).
+struct SpRowAcc {
+  const double* d;
+  SpCursor c;
+  __device__ __forceinline__ double at(const SArgs& S, int g) { return d ? d[g] : c.at(S, g); }
 };
 
 // Bit summary of the run staged at window index w: loci at or above k1 / k2 / the sister
@@ -165,9 +182,7 @@ __device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, in
 
 // (rank, crit) of a clade pair over the kept loci: numpy-order mean and min of the
 // per-locus max (orgscorer.py:447-461), rows read from the segment table.
-__device__ __forceinline__ double sp_pair_rank(const SArgs& S, int ra, int ca, int rb, int cb, int se,
-                                               uint64_t keep, int Gu, const double* urow) {
-  SpCursor a{ra, ca, se, ra < 0 ? urow : nullptr}, b{rb, cb, se, rb < 0 ? urow : nullptr};
+__device__ __forceinline__ double sp_pair_rank(const SArgs& S, SpRowAcc a, SpRowAcc b, uint64_t keep, int Gu) {
   uint64_t m = keep;
   auto next = [&]() -> double {
     const int g = __builtin_ctzll(m);
@@ -178,9 +193,7 @@ __device__ __forceinline__ double sp_pair_rank(const SArgs& S, int ra, int ca, i
   return (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
 }
 
-__device__ __forceinline__ double sp_pair_crit(const SArgs& S, int ra, int ca, int rb, int cb, int se,
-                                               uint64_t keep, const double* urow) {
-  SpCursor a{ra, ca, se, ra < 0 ? urow : nullptr}, b{rb, cb, se, rb < 0 ? urow : nullptr};
+__device__ __forceinline__ double sp_pair_crit(const SArgs& S, SpRowAcc a, SpRowAcc b, uint64_t keep) {
   double m = 0.0;
   bool first = true;
   for (uint64_t r = keep; r; r &= r - 1) {
@@ -216,12 +229,11 @@ __device__ __forceinline__ uint64_t sp_sisters(const SpParent* e, int p, const S
 // the synteny masks from the two runs, swap rule, direction, LGT filters, sister penalty.
 // c1p / c2p of the result are 0 (A) or 1 (B).
 __device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& sh, const SpMember& A,
-                                               const SpMember& B, const SpParent* par, int pcap, int se,
-                                               int G, uint64_t ign, bool cmp, uint8_t* out) {
+                                               const SpMember& B, SpRowAcc a, SpRowAcc b, const SpParent* par,
+                                               int pcap, int G, uint64_t ign, bool cmp, uint8_t* out) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const bool unk = A.cl == K.unknown || B.cl == K.unknown;
-  SpCursor a{A.rs, A.cl, se, A.rs < 0 ? sh.urow : nullptr}, b{B.rs, B.cl, se, B.rs < 0 ? sh.urow : nullptr};
   uint64_t mm = 0, ma = 0, mb = 0;
   for (int g = 0; g < G; ++g) {
     const uint64_t bit = 1ull << g;
@@ -281,7 +293,7 @@ __device__ __forceinline__ OptEval sp_eval_two(const SArgs& S, const SpShared& s
 // Every candidate pair (the members of each passing class pair): f(u, v, mu, mv) on the
 // lane that owns it, mu's potential index below mv's.
 template <class F>
-__device__ __forceinline__ void sp_for_cands(const SpShared& sh, const SpMember* mem, F f) {
+__device__ __forceinline__ void sp_for_cands(const SpShared& sh, const SpMember* mem, const int* gidx, F f) {
   const int lane = threadIdx.x & 63;
   const int np = sh.n_pairs;
   const int T = sh.pref[np];
@@ -310,9 +322,10 @@ __device__ __forceinline__ void sp_for_cands(const SpShared& sh, const SpMember*
       u = a0 + y / nb;
       v = sh.coff[b] + y % nb;
     }
-    const SpMember mu = mem[u], mv = mem[v];
-    if (mu.pi < mv.pi) f(u, v, mu, mv);
-    else f(v, u, mv, mu);
+    const int qu = gidx[u], qv = gidx[v];
+    const SpMember mu = mem[qu], mv = mem[qv];
+    if (mu.pi < mv.pi) f(qu, qv, mu, mv);
+    else f(qv, qu, mv, mu);
   }
 }
 
@@ -365,7 +378,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   const int iteration = level + 1;
   int64_t pair_evals = level == 0 ? 0 : K.pair_evals[c];
   SpMember* mem = reinterpret_cast<SpMember*>(ws);
-  SpParent* par = reinterpret_cast<SpParent*>(ws + (int64_t)kSpMemG * sizeof(SpMember));
+  int* gidx = reinterpret_cast<int*>(ws + kSpOffGidx);
+  SpParent* par = reinterpret_cast<SpParent*>(ws + kSpOffPar);
+  double* drows = reinterpret_cast<double*>(ws + kSpOffDense);
 
   // ---- pass 1: per-locus maxes over known clades, root present (:407-411) -------------
   sh.mx[lane] = 0;
@@ -373,7 +388,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     const int ls = K.lstart[l0 + lane], le = K.lend[l0 + lane];
     sh.len[lane] = max(ls, le) - min(ls, le) + 1;
   }
-  for (int i = lane; i < kSpCls; i += 64) { sh.ckey[i] = ~0ull; sh.ccnt[i] = 0; sh.cint[i] = 0; sh.cfill[i] = 0; }
+  for (int i = lane; i < kSpCls; i += 64) {
+    sh.ckey[i] = ~0ull; sh.cmany[i] = 0; sh.ccnt[i] = 0; sh.cint[i] = 0; sh.cfill[i] = 0;
+  }
   if (lane == 0) { sh.n_used = 0; sh.n_pairs = 0; sh.cnt = 0; sh.over = 0; }
   __syncthreads();
   bool root = false;
@@ -423,12 +440,17 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   long long bk = -1;
   int brs = -1;
   int Pp = 0, upi = 0;                              // upi: potential clades before "Unknown"
+  // class table: a plain read finds an existing class; only a new one takes a CAS (the
+  // loser of a race for the same new class is its second clade)
   auto ins_class = [&](uint64_t cmask) {
     int h = sp_hash(cmask, kSpCls);
     for (int probe = 0; probe < kSpCls; ++probe) {
-      const unsigned long long old = atomicCAS(&sh.ckey[h], ~0ull, (unsigned long long)cmask);
-      if (old == ~0ull) atomicAdd(&sh.n_used, 1);
-      if (old == ~0ull || old == cmask) { atomicAdd(&sh.ccnt[h], 1); break; }
+      unsigned long long k = sh.ckey[h];
+      if (k == ~0ull) {
+        k = atomicCAS(&sh.ckey[h], ~0ull, (unsigned long long)cmask);
+        if (k == ~0ull) { atomicAdd(&sh.n_used, 1); break; }
+      }
+      if (k == cmask) { sh.cmany[h] = 1; break; }
       h = (h + 1) & (kSpCls - 1);
     }
   };
@@ -555,7 +577,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     const unsigned long long ma = sh.ckey[a];
     for (int ib = ia + lane; ib < U; ib += 64) {
       const int b = sh.cls[ib];
-      if ((ma | sh.ckey[b]) != keep || (a == b && sh.ccnt[a] < 2)) continue;
+      if ((ma | sh.ckey[b]) != keep || (a == b && !sh.cmany[a])) continue;
       const int q = atomicAdd(&sh.n_pairs, 1);
       if (q < kSpPairs) sh.pair[q] = min(a, b) | (max(a, b) << 16);
       sh.cint[a] = 1;
@@ -566,29 +588,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   bool have_ok = false;
   if (sh.n_pairs > 0) {
     if (sh.n_pairs > kSpPairs) return false;
-    // members of the passing classes, grouped by class (first member of each class)
-    if (lane == 0) {
-      int acc = 0;
-      for (int ia = 0; ia < U; ++ia) {
-        const int a = sh.cls[ia];
-        sh.coff[a] = acc;
-        if (sh.cint[a]) acc += sh.ccnt[a];
-      }
-      sh.cnt = acc;
-      int tot = 0;                                   // candidates per pair, prefix
-      for (int q = 0; q < sh.n_pairs; ++q) {
-        sh.pref[q] = tot;
-        const int a = sh.pair[q] & 0xFFFF, b = sh.pair[q] >> 16;
-        const long long n = a == b ? (long long)sh.ccnt[a] * (sh.ccnt[a] - 1) / 2
-                                   : (long long)sh.ccnt[a] * sh.ccnt[b];
-        tot = (int)min<long long>((long long)tot + n, 0x7FFFFFFF);
-      }
-      sh.pref[sh.n_pairs] = tot;
-    }
-    __syncthreads();
-    const int M = sh.cnt;
-    if (M > kSpMemG || sh.pref[sh.n_pairs] == 0x7FFFFFFF) return false;
-    // ---- pass 3: members (potential clades of passing classes) -------------------------
+    // ---- pass 3: members (potential clades of passing classes), counted per class -------
     int pbase = 0;
     sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
       bool pot = false;
@@ -605,10 +605,14 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
         int h = sp_hash(cmask, kSpCls);
         while (sh.ckey[h] != cmask) h = (h + 1) & (kSpCls - 1);
         if (sh.cint[h]) {
-          SpMember m;
-          m.rs = t; m.cl = cl; m.pi = pi; m.sp = K.sibp[cl];
-          m.mask = cmask; m.hm = r.mhs;
-          mem[sh.coff[h] + atomicAdd(&sh.cfill[h], 1)] = m;
+          const int q = atomicAdd(&sh.cnt, 1);
+          atomicAdd(&sh.ccnt[h], 1);
+          if (q < kSpMemG) {
+            SpMember m;
+            m.rs = t; m.cl = cl; m.pi = pi; m.sp = K.sibp[cl];
+            m.h = h; m.pad = 0; m.hm = r.mhs;
+            mem[q] = m;
+          }
         }
       }
     });
@@ -617,12 +621,64 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       int h = sp_hash(cmask, kSpCls);
       while (sh.ckey[h] != cmask) h = (h + 1) & (kSpCls - 1);
       if (sh.cint[h]) {
-        SpMember m;
-        m.rs = -1; m.cl = K.unknown; m.pi = upi; m.sp = K.sibp[K.unknown];
-        m.mask = cmask; m.hm = u_hs;
-        mem[sh.coff[h] + atomicAdd(&sh.cfill[h], 1)] = m;
+        const int q = atomicAdd(&sh.cnt, 1);
+        atomicAdd(&sh.ccnt[h], 1);
+        if (q < kSpMemG) {
+          SpMember m;
+          m.rs = -1; m.cl = K.unknown; m.pi = upi; m.sp = K.sibp[K.unknown];
+          m.h = h; m.pad = 0; m.hm = u_hs;
+          mem[q] = m;
+        }
       }
     }
+    __threadfence_block();
+    __syncthreads();
+    const int M = sh.cnt;
+    if (M > kSpMemG) return false;
+    // members grouped by class (gidx), candidate counts per passing class pair
+    if (lane == 0) {
+      int acc = 0;
+      for (int ia = 0; ia < U; ++ia) {
+        const int a = sh.cls[ia];
+        sh.coff[a] = acc;
+        if (sh.cint[a]) acc += sh.ccnt[a];
+      }
+      int tot = 0;
+      for (int q = 0; q < sh.n_pairs; ++q) {
+        sh.pref[q] = tot;
+        const int a = sh.pair[q] & 0xFFFF, b = sh.pair[q] >> 16;
+        const long long n = a == b ? (long long)sh.ccnt[a] * (sh.ccnt[a] - 1) / 2
+                                   : (long long)sh.ccnt[a] * sh.ccnt[b];
+        tot = (int)min<long long>((long long)tot + n, 0x7FFFFFFF);
+      }
+      sh.pref[sh.n_pairs] = tot;
+    }
+    __syncthreads();
+    if (sh.pref[sh.n_pairs] == 0x7FFFFFFF) return false;
+    for (int q = lane; q < M; q += 64) {
+      const int h = mem[q].h;
+      gidx[sh.coff[h] + atomicAdd(&sh.cfill[h], 1)] = q;
+    }
+    // the members' dense rows (the pair evaluations then load a row's loci independently)
+    const bool dense = (int64_t)M * G <= kSpDense;
+    if (dense)
+      for (int q = lane; q < M; q += 64) {
+        const SpMember m = mem[q];
+        double* row = drows + (int64_t)q * G;
+        if (m.rs < 0) {
+          for (int g = 0; g < G; ++g) row[g] = sh.urow[g];
+        } else {
+          for (int g = 0; g < G; ++g) row[g] = 0.0;
+          for (int t = m.rs; t < se; ++t) {
+            const int2 cg = S.seg_cg[t];
+            if (cg.x != m.cl) break;
+            row[cg.y] = S.seg_mean[t];
+          }
+        }
+      }
+    auto acc = [&](int q, const SpMember& m) -> SpRowAcc {
+      return SpRowAcc{dense ? drows + (int64_t)q * G : nullptr, SpCursor{m.rs, m.cl, se, m.rs < 0 ? sh.urow : nullptr}};
+    };
     __threadfence_block();
     __syncthreads();
     // ---- pass 4: per parent of a member, clades listed under it scoring >= threshold ----
@@ -668,8 +724,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     double pr = -__builtin_inf();
     long long pk = -1;
     int pu = -1, pv = -1;
-    sp_for_cands(sh, mem, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
-      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu, sh.urow);
+    sp_for_cands(sh, mem, gidx, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
+      const double r = sp_pair_rank(S, acc(u, mu), acc(v, mv), keep, Gu);
       const long long key = (long long)mu.pi * Pp + mv.pi;
       if (better(r, key, pr, pk)) { pr = r; pk = key; pu = u; pv = v; }
     });
@@ -686,20 +742,21 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     double best_crit = 0.0;
     if (lane == 0) {
       const SpMember A = mem[pu], B = mem[pv];
-      const OptEval e = sp_eval_two(S, sh, A, B, par, pcap, se, G, ign, false, sh.syn);
+      const OptEval e = sp_eval_two(S, sh, A, B, acc(pu, A), acc(pv, B), par, pcap, G, ign, false, sh.syn);
       best_ok = e.ok; best_dir = e.dir;
       best_c1 = e.c1p ? pv : pu;
       best_c2 = e.c2p ? pv : pu;
-      best_crit = sp_pair_crit(S, A.rs, A.cl, B.rs, B.cl, se, keep, sh.urow);
+      best_crit = sp_pair_crit(S, acc(pu, A), acc(pv, B), keep);
       sh.n_in = 0; sh.all_ok = 1; sh.all_same = 1;
     }
     for (int i = lane; i < kSpMemG / 32; i += 64) { sh.bm1[i] = 0; sh.bm2[i] = 0; }
     __syncthreads();
     // ---- pass 2 over the candidates: options within --range get the LGT filters --------
-    sp_for_cands(sh, mem, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
-      const double r = sp_pair_rank(S, mu.rs, mu.cl, mv.rs, mv.cl, se, keep, Gu, sh.urow);
+    sp_for_cands(sh, mem, gidx, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
+      const SpRowAcc a = acc(u, mu), b = acc(v, mv);
+      const double r = sp_pair_rank(S, a, b, keep, Gu);
       if (!((pr - r) <= P.range)) return;                       // (:636-639)
-      const OptEval e = sp_eval_two(S, sh, mu, mv, par, pcap, se, G, ign, true, nullptr);
+      const OptEval e = sp_eval_two(S, sh, mu, mv, a, b, par, pcap, G, ign, true, nullptr);
       atomicAdd(&sh.n_in, 1);
       if (!e.ok) atomicAnd(&sh.all_ok, 0);
       if (!e.same) atomicAnd(&sh.all_same, 0);

@@ -763,6 +763,19 @@ __global__ void k_seg_combine(const SArgs S, int64_t n_keys) {
 // locus ('~' elsewhere), since its crit >= k1.  Contigs with more segments than the stage
 // holds, more than 64 loci or --weak-loci assign-unknown (virtual "Unknown" row) go to the
 // dense workgroup (k_decide<1>); contigs without a one-clade option go to explain_two.
+// Upper bound of decide_contig's arena for P clade rows (segments + 1) and G loci: every
+// take() of decide_contig with its 16-byte alignment, plus the mask-class workspace.
+__host__ __device__ int64_t arena_bound(int64_t P, int64_t G) {
+  int64_t cls = 0;
+  if (P >= kClsMin) {
+    int64_t n2 = 1;
+    while (n2 < P) n2 <<= 1;
+    cls = n2 * 8 + (P + 1) * 4 + (int64_t)kClsMaxPairs * 8 + ((int64_t)kClsMaxPairs + 1) * 8 + 64;
+  }
+  return 20 * 16 + P * (4 + 4 + 8 + 4 + 4 + 4 + 8 + 4) + 8 * P * G + G * (8 + 4 + 4 + 1 + 4) +
+         8 * (P / 32 + 2) + cls;
+}
+
 constexpr int kOneCap = 384;
 
 __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
@@ -785,6 +798,19 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
     if (K.hit_off[c + 1] == h0 || G == 0) continue;       // never evaluated (orgscorer.py:959)
     const int so = n_keys > 0 ? S.crank_first[cr] : 0;
     const int ns = (n_keys > 0 ? S.crank_first[cr + 1] : 0) - so;
+    if (S.sparse_on && G <= 63 && ns > kOneCap && arena_bound(ns + 1, G) + 4096 > S.dec_lds_bytes) {
+      // the dense matrix cannot fit the LDS arena: straight to the segment-table decision
+      // (k_big_sparse; need_bytes for the HBM-slot decision should it decline the contig)
+      if (lane == 0) {
+        const int64_t need = arena_bound(ns + 1, G) + 4096;
+        K.need[c] = need;
+        const int slot = (int)atomicAdd(&S.counters[2], 1ull);
+        S.big_list[2 * slot] = cr;
+        S.big_list[2 * slot + 1] = c;
+        atomicMax(&S.counters[3], (unsigned long long)need);
+      }
+      continue;
+    }
     if (ns > kOneCap || G > 64 || P.weak == 2 || S.force_big) {
       if (lane == 0) {
         const int slot = (int)atomicAdd(&S.counters[6], 1ull);
@@ -1131,19 +1157,6 @@ __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int lev
 }
 
 #include "wf_sparse.h"
-
-// Upper bound of decide_contig's arena for P clade rows (segments + 1) and G loci: every
-// take() of decide_contig with its 16-byte alignment, plus the mask-class workspace.
-int64_t arena_bound(int64_t P, int64_t G) {
-  int64_t cls = 0;
-  if (P >= kClsMin) {
-    int64_t n2 = 1;
-    while (n2 < P) n2 <<= 1;
-    cls = n2 * 8 + (P + 1) * 4 + kClsMaxPairs * 8 + (kClsMaxPairs + 1) * 8 + 64;
-  }
-  return 20 * 16 + P * (4 + 4 + 8 + 4 + 4 + 4 + 8 + 4) + 8 * P * G + G * (8 + 4 + 4 + 1 + 4) +
-         8 * (P / 32 + 2) + cls;
-}
 
 int bits_for(int64_t v) {   // bits to hold values 0..v
   int b = 1;
@@ -1540,6 +1553,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   sa.dec_lds_bytes = st->dec_lds;
   sa.force_big = st->sparse_big == 2 ? 1 : 0;
   sa.route_sparse = st->sparse_big >= 2 ? 1 : 0;
+  sa.sparse_on = st->sparse_big != 0 ? 1 : 0;
   // kernels take SArgs by value (kernarg segment): no argument uploads, and the pointers
   // loaded from it are known to be global (global_* instead of flat_* memory operations)
   ST_TRY(st->counters.ensure(s, 8 * sizeof(unsigned long long)));
@@ -1895,10 +1909,17 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       // the decision from the segment table, one wave per contig (wf_sparse.h): as many
       // waves as are resident at once (LDS-bound)
       if (st->sparse_res < 0) {
-        int b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_big_sparse), 64, 0) !=
-                hipSuccess || b < 1)
-          b = 8;
+        // resident one-wave workgroups per CU from the kernel's own VGPR and LDS use (the
+        // occupancy query returned 4 here: SQ_WAVES of the round-3 cfg5 profile): waves per
+        // SIMD = 512 / VGPRs (granule 8, at most 8), 4 SIMDs; LDS 160 KB per CU
+        hipFuncAttributes fa{};
+        int b = 8;
+        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_big_sparse)) == hipSuccess) {
+          const int vg = std::max(8, (fa.numRegs + 7) & ~7);
+          const int by_vgpr = 4 * std::min(8, 512 / vg);
+          const int by_lds = (int)((160 * 1024) / std::max<size_t>(1, fa.sharedSizeBytes));
+          b = std::max(1, std::min(by_vgpr, by_lds));
+        }
         st->sparse_res = b;
       }
       const int grid = std::min(n_big, st->cus * st->sparse_res);
