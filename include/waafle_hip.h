@@ -51,12 +51,14 @@ enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
 enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
 
 /* Context options (wf_set_option); every one leaves the results unchanged.
- * WF_OPT_SPARSE_BIG: 1 (default) contigs whose gene-score matrix outgrows the LDS arena
- *   take the decision straight from the segment table, one wave per contig; 0: the dense
- *   matrix in an HBM slot (the only form for > 63 loci or --weak-loci assign-unknown);
- *   2: every decision the staged kernels make goes to the segment-table form (a test
- *   setting: it exercises that form on every input); 3: every contig the one-wave
- *   explain_one (k_one) leaves open goes to the segment-table form.
+ * WF_OPT_SPARSE_BIG: the decision form of the staged kernels for contigs of <= 63 loci.
+ *   3 (default): explain_one by one wave per contig (k_one), and every contig it leaves
+ *   open (explain_two, more segments than its LDS holds, --weak-loci assign-unknown) takes
+ *   the decision straight from the segment table, one wave per contig (k_big_sparse);
+ *   1: only contigs whose gene-score matrix outgrows the LDS arena go there, the others
+ *   to the dense workgroup decision; 0: the dense matrix, in an HBM slot when it outgrows
+ *   the arena (the only form for > 63 loci); 2: every staged decision in the segment-table
+ *   form (a test setting: it exercises that form on every input).
  * WF_OPT_ATT_LIMIT: hit-locus attachments one wf_score call accepts (default and maximum
  *   2^31 - 1; more -> WF_E_TOOBIG, nothing scored). */
 enum wf_option { WF_OPT_SPARSE_BIG = 1, WF_OPT_ATT_LIMIT = 2 };

@@ -31,6 +31,8 @@ FORMS = {
     "staged": dict(mode="staged"),
     # every staged decision from the segment table (k_big_sparse, wf_sparse.h)
     "sparse": dict(mode="staged", options={lib.OPT_SPARSE_BIG: 2}),
+    # the dense workgroup decision, k_big_sparse only for contigs outgrowing its arena
+    "overflow": dict(mode="staged", options={lib.OPT_SPARSE_BIG: 1}),
     # every staged decision that outgrows a 4 KB arena in an HBM slot (k_decide_big)
     "dense_big": dict(mode="staged", lds_bytes=4096, options={lib.OPT_SPARSE_BIG: 0}),
 }

@@ -153,8 +153,9 @@ def cfg4_full():
 def test_cfg4_full_size(cfg4_full):
     """cfg4 at full size (1 M contigs, 210 M hits, one call): no contig errors, the same
     records on a second pass, from four cost-balanced shards, with a 16 KB decision arena
-    (round 2: WF_DEC_LDS=16384 produced WF_E_EMPTYMASK at this shape) and with the dense
-    HBM-slot decision only; and the oracle's records on a 200-contig sample."""
+    (round 2: WF_DEC_LDS=16384 produced WF_E_EMPTYMASK at this shape), with the dense
+    workgroup decision for the contigs k_one leaves open, and with the dense HBM-slot decision
+    only; and the oracle's records on a 200-contig sample."""
     batch, tax = cfg4_full
     s = engine.GpuScorer(0)
     s.set_taxonomy(tax)
@@ -166,7 +167,8 @@ def test_cfg4_full_size(cfg4_full):
     parts = [s.score(batch.slice(x, y), PARAMS) for x, y in bounds]
     s.close()
     assert_same(engine.Results.concat(parts, [int(batch.hit_off[x]) for x, _ in bounds]), a, batch)
-    for kw in (dict(lds_bytes=16384), dict(options={lib.OPT_SPARSE_BIG: 0})):
+    for kw in (dict(lds_bytes=16384), dict(options={lib.OPT_SPARSE_BIG: 1}),
+               dict(options={lib.OPT_SPARSE_BIG: 0})):
         c = score(batch, tax, **kw)
         assert not c.status.any(), kw
         assert_same(c, a, batch)

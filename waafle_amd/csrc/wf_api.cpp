@@ -46,7 +46,7 @@ struct wf_ctx {
   int64_t launches = 0;
   bool lds_set = false;            // wf_set_lds_bytes called: also the staged decision arena
   int mode = WF_MODE_LEVEL0;       // wf_set_mode
-  int sparse_big = 1;              // wf_set_option(WF_OPT_SPARSE_BIG)
+  int sparse_big = 3;              // wf_set_option(WF_OPT_SPARSE_BIG)
   int64_t att_limit = (int64_t(1) << 31) - 1;   // wf_set_option(WF_OPT_ATT_LIMIT)
   wf::StagedState* staged = nullptr;
   // --write-details

@@ -798,9 +798,9 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
     if (K.hit_off[c + 1] == h0 || G == 0) continue;       // never evaluated (orgscorer.py:959)
     const int so = n_keys > 0 ? S.crank_first[cr] : 0;
     const int ns = (n_keys > 0 ? S.crank_first[cr + 1] : 0) - so;
-    if (S.sparse_on && G <= 63 && ns > kOneCap && arena_bound(ns + 1, G) + 4096 > S.dec_lds_bytes) {
-      // the dense matrix cannot fit the LDS arena: straight to the segment-table decision
-      // (k_big_sparse; need_bytes for the HBM-slot decision should it decline the contig)
+    // straight to the segment-table decision (k_big_sparse), with need_bytes for the
+    // HBM-slot decision should it decline the contig
+    auto push_big = [&]() {
       if (lane == 0) {
         const int64_t need = arena_bound(ns + 1, G) + 4096;
         K.need[c] = need;
@@ -809,7 +809,15 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
         S.big_list[2 * slot + 1] = c;
         atomicMax(&S.counters[3], (unsigned long long)need);
       }
-      continue;
+    };
+    const bool to_sparse = S.sparse_on && G <= 63;
+    if (to_sparse && (S.route_sparse || (ns > kOneCap && arena_bound(ns + 1, G) + 4096 > S.dec_lds_bytes))) {
+      if (S.route_sparse && !S.force_big && ns <= kOneCap && P.weak != 2) {
+        // (routed decisions: explain_one here first, explain_two there)
+      } else {
+        push_big();                                     // the dense matrix cannot fit the arena
+        continue;
+      }
     }
     if (ns > kOneCap || G > 64 || P.weak == 2 || S.force_big) {
       if (lane == 0) {
@@ -878,6 +886,10 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
       if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
     }
     if (bk < 0) {                                          // explain_two (:570)
+      if (to_sparse && S.route_sparse) {
+        push_big();
+        continue;
+      }
       if (lane == 0) {
         const int slot = (int)atomicAdd(&S.counters[5], 1ull);
         S.two_list[2 * slot] = cr;
@@ -1203,7 +1215,7 @@ struct StagedState {
   Buf span_cnt, spans;                              // --write-details only
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
-  int sparse_big = 1;                // WF_OPT_SPARSE_BIG (0 dense, 1 overflow, 2 all, 3 decisions)
+  int sparse_big = 3;                // WF_OPT_SPARSE_BIG (0 dense, 1 overflow, 2 all, 3 decisions)
   int sparse_res = -1;               // resident k_big_sparse waves per CU
   int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
   // per-phase timing (wf_phase): event pool, this call's spans (phase, begin, end)
