@@ -703,6 +703,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     // ---- levels: sort, segments, means, explain_one [, explain_two, roll-up] ----
     int64_t pair_evals = 0;
     bool seed = false;                                 // raised at level 0: staged level 1 seed
+    bool dumped = false;                               // segment table handed to k_dump_sparse
     for (int level = 0; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
       const int iteration = level + 1;
       if (level > 0) {                               // roll up (:431-445): re-key to the parent clade
@@ -791,6 +792,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       const double bound_s = P.sister_thr * (1.0 - 1e-12);
       uint64_t open = 0;
       int outcome = 0;                                 // 2: decided (or stopped) by explain_one
+      // first form: the level's decision goes to k_dump_sparse with the whole segment table
+      // (pass 6 evaluates the rest) instead of the staged kernels
+      bool dump = false;
+      const bool can_dump = !FULL && S.dump_cap > 0;
       for (int pass = prune ? 0 : 3;;) {
         int n = ns;
         const uint16_t* list = nullptr;
@@ -1003,20 +1008,26 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
           double br = -__builtin_inf(), bcrit = 0.0;
           long long bk = -1;
           double* rank = F.rank();
-          for (int t = lane; t < ns; t += 64) {
-            double rk = -1.0;
+          // the rank of the option whose clade run starts at t, or -1 (crit: its crit)
+          auto option_rank = [&](int t, double& crit) -> double {
             const int clade = cg_of(F, t).x;
             // (assign-unknown: a real "Unknown" run is replaced by the virtual row, below)
             if ((t == 0 || cg_of(F, t - 1).x != clade) && (!prune || (int)rc[t] == Gu) &&
                 !(P.weak == 2 && clade == K.unknown)) {
-              double crit, rnk;                            // (pruned: only runs on every unmasked locus)
+              double rnk;                                  // (pruned: only runs on every unmasked locus)
               sparse_score(F, v, t, ns, clade, um, Gu, crit, rnk);
-              if (crit >= P.k1) {
-                rk = rnk;
-                if (better(rnk, clade, br, bk)) { br = rnk; bk = clade; bcrit = crit; }
-              }
+              if (crit >= P.k1) return rnk;
             }
-            rank[t] = rk;                                  // option rank by segment (-1: none)
+            return -1.0;
+          };
+          for (int t = lane; t < ns; t += 64) {
+            double crit = 0.0;
+            const double rk = option_rank(t, crit);
+            if (rk >= 0.0 && better(rk, cg_of(F, t).x, br, bk)) { br = rk; bk = cg_of(F, t).x; bcrit = crit; }
+            // option rank by segment (-1: none).  The first form's rank array is the
+            // attachment scores' (sc), which a hand-over to k_dump_sparse still needs
+            // (pass 6): meld_one recomputes the few options' ranks there instead
+            if (FULL) rank[t] = rk;
           }
     #pragma unroll
           for (int off = 32; off > 0; off >>= 1) {
@@ -1035,6 +1046,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
               if (cg.x != K.unknown && v[t] >= 0.0 && (1.0 - v[t]) < P.k1) settles = true;
             }
             if (bk < 0 || __ballot(settles) == 0ull) {
+              if (can_dump) {
+                dump = true;
+                if (pass == 3) break;
+                pass = 6;
+                continue;
+              }
               staged = true;
               outcome = 2;
               break;
@@ -1046,7 +1063,8 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             if (P.dis1 == 1)
               for (int t0 = 0; t0 < ns; t0 += 64) {
                 const int t = t0 + lane;
-                const double rk = t < ns ? rank[t] : -1.0;
+                double crit_unused;
+                const double rk = t < ns ? (FULL ? rank[t] : option_rank(t, crit_unused)) : -1.0;
                 const bool in = rk >= 0.0 && (br - rk) <= P.range;
                 const uint64_t im = __ballot(in);
                 if (in) F.mem()[nm + __popcll(im & lanes_below())] = cg_of(F, t).x;
@@ -1081,6 +1099,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             break;
           }
         if (!FULL) {                                   // explain_two (:570): the next kernel
+          if (can_dump) {
+            dump = true;
+            if (pass == 3) break;
+            pass = 6;
+            continue;
+          }
           staged = true;
           outcome = 2;
           break;
@@ -1090,6 +1114,29 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       staged = staged || __ballot(fail) != 0ull;
       wave_sync();
+      if (dump && !staged) {
+        // the table: one 64-bit atomic gives the slot (high bits) and its first entry (low
+        // 40), so slot k's entries start where slot k - 1's end
+        unsigned long long old = 0;
+        if (lane == 0) old = atomicAdd(S.dump_ctr, (1ull << 40) | (unsigned long long)ns);
+        old = __shfl(old, 0, 64);
+        const int slot = (int)(old >> 40);
+        const int64_t base = (int64_t)(old & ((1ull << 40) - 1));
+        dumped = base + ns <= S.dump_cap;            // else: the staged kernels (pend 1)
+        if (dumped)
+          for (int t = lane; t < ns; t += 64) {
+            S.dump_cg[base + t] = cg_of(F, t);
+            S.dump_mean[base + t] = v[t];
+          }
+        if (lane == 0) {
+          S.dump_first[slot] = (int)(base < INT32_MAX ? base : INT32_MAX);
+          S.dump_first[slot + 1] = (int)(base + ns < INT32_MAX ? base + ns : INT32_MAX);
+          S.dump_list[2 * slot] = slot;
+          S.dump_list[2 * slot + 1] = dumped ? c : -1;
+        }
+        staged = true;                                 // (its attachment counts stand)
+        break;
+      }
       if (staged || outcome == 2) break;
       const int Gu = __popcll(um);
       wave_sync();
@@ -1122,7 +1169,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     if (lane == 0) {
       ccnt[c] = staged ? n_att : 0;
       cleaves[c] = staged ? nl_sum : 0;
-      pend[c] = staged ? (seed ? 2 : 1) : 0;
+      pend[c] = staged ? (dumped ? 3 : (seed ? 2 : 1)) : 0;
     }
     wave_sync();                                       // the slice is reused by the next contig
   }

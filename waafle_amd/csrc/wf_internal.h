@@ -79,15 +79,6 @@ struct SArgs {
   int32_t* crank_first;          // [active + 1] first segment of each active contig
   int32_t* seg_cnt;              // [active + 1] segments per active contig (per-contig sort)
   int32_t* seg_len;              // [segments] locus length (k_seg_build; null on the radix path)
-  // flat explain_one (weak loci ignore/penalize, <= 64 loci)
-  uint64_t* lmax;                // [n_loci] per-locus max score bits over known clades
-  int32_t* c_gu;                 // [active] unmasked loci (-1: contig needs no decision)
-  uint64_t* c_umask;             // [active] unmasked-locus bit mask
-  unsigned long long* c_best;    // [active] best one-clade rank bits + 1 (0: none)
-  int32_t* c_bestcl;             // [active] best clade id (ties: larger id)
-  int32_t* c_nopt;               // [active] options within --range
-  double* run_crit;              // [segments] crit of the clade run starting here
-  double* run_rank;              // [segments] rank of the clade run starting here
   int2* satt_lohi;               // [attachments] site range, in sorted (segment) order
   double* satt_sc;               // [attachments] score, in sorted order
   double* leaf_val;              // [leaves] exact leaf sums
@@ -101,6 +92,16 @@ struct SArgs {
   int sparse_on;                 // WF_OPT_SPARSE_BIG != 0: k_big_sparse runs
   const unsigned long long* in_counts;   // this level's counts on the device (null: the
                                          // kernel arguments are exact)
+  // Level-0 segment tables the first wave form hands to k_dump_sparse: contigs it leaves at
+  // explain_two (or at an unproven --weak-loci assign-unknown row), every mean evaluated
+  int64_t dump_cap;              // entries dump_cg / dump_mean hold (0: no hand-over)
+  int2* dump_cg;                 // [dump_cap] (clade, locus), in (clade, locus) order per contig
+  double* dump_mean;             // [dump_cap] segment means
+  int32_t* dump_first;           // [n_contigs + 1] first entry of each slot
+  int32_t* dump_list;            // [2 n_contigs] (slot, contig); contig -1: did not fit
+  unsigned long long* dump_ctr;  // slots << 40 | entries
+  int32_t* seed_pend;            // k_dump_sparse: pend of the contigs it decides (0), raises
+                                 // (2: staged level-1 seed) or declines (1: staged level 0)
 };
 
 // waafle_genecaller (wf_genecall.hip): one contig group per wave

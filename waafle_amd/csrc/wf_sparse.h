@@ -836,6 +836,13 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   }
   const int dec = (no_rows || root_present) ? kDecStop : kDecRaise;
   if (dec == kDecRaise && iteration + 1 <= kMaxIter) {
+    if (S.seed_pend) {                               // level 0 of the wave kernels: a staged
+      if (lane == 0) {                               // level-1 seed (k_rekey_seeds rolls it up)
+        S.seed_pend[c] = 2;
+        K.pair_evals[c] = pair_evals;
+      }
+      return true;
+    }
     sp_raise(S, c, pair_evals);                      // roll up (orgscorer.py:431-445)
     return true;
   }
@@ -862,6 +869,32 @@ __global__ __launch_bounds__(64) void k_big_sparse(const SArgs S, int level, int
       const int slot = (int)atomicAdd(&S.counters[1], 1ull);
       S.big2_list[2 * slot] = cr;
       S.big2_list[2 * slot + 1] = c;
+    }
+    __syncthreads();
+  }
+}
+
+// Level 0 of the contigs the first wave form handed over with their segment tables
+// (S.dump_*: slot i holds entries [dump_first[i], dump_first[i + 1]) of contig
+// dump_list[2 i + 1]).  S.seed_pend / ccnt / cleaves: decided -> pend 0 and no staged
+// attachments; raised -> pend 2 (level-1 seed); declined (> 63 loci, class or pair tables
+// outgrown) -> pend 1, the staged kernels take level 0.
+__global__ __launch_bounds__(64) void k_dump_sparse(const SArgs S, int64_t* ccnt, int64_t* cleaves) {
+  __shared__ SpShared sh;
+  char* ws = S.sp_ws + (int64_t)blockIdx.x * kSpSlot;
+  const int count = (int)(*S.dump_ctr >> 40);
+  for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const int c = S.dump_list[2 * i + 1];
+    if (c < 0) continue;                             // (its table did not fit: pend 1 stands)
+    const bool ok = sp_level(S, sh, ws, c, i, 0, 1);
+    if (threadIdx.x == 0) {
+      if (!ok) {
+        S.seed_pend[c] = 1;
+      } else if (S.seed_pend[c] == 3) {
+        S.seed_pend[c] = 0;
+        ccnt[c] = 0;
+        cleaves[c] = 0;
+      }
     }
     __syncthreads();
   }

@@ -1227,6 +1227,7 @@ struct StagedState {
   int64_t phase_n[8] = {0};
   Buf act0, act1, base0, base1, big_list, big2_list, two_list, one_list, big_ws, tmp, pend, act_l0;
   Buf sp_ws;                        // k_big_sparse scratch (kSpSlot per wave)
+  Buf dump_cg, dump_mean, dump_first, dump_list, dump_ctr;   // level-0 hand-over (k_dump_sparse)
   bool level0 = true;               // wave kernels (wf_fast.hip) before the staged kernels
   bool rollup = false;              // ... carrying the roll-up levels too
   bool lut_ready = false;
@@ -1518,6 +1519,25 @@ __global__ void k_rekey_seeds(const int32_t* list, int n, const int64_t* catt_of
   }
 }
 
+// resident one-wave workgroups per CU of the segment-table kernels (k_big_sparse,
+// k_dump_sparse: the same sp_level body) from the kernel's own VGPR and LDS use (the
+// occupancy query returned 4 here: SQ_WAVES of the round-3 cfg5 profile): waves per SIMD =
+// 512 / VGPRs (granule 8, at most 8), 4 SIMDs; LDS 160 KB per CU
+static int sparse_waves(StagedState* st) {
+  if (st->sparse_res < 0) {
+    hipFuncAttributes fa{};
+    int b = 8;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_big_sparse)) == hipSuccess) {
+      const int vg = std::max(8, (fa.numRegs + 7) & ~7);
+      const int by_vgpr = 4 * std::min(8, 512 / vg);
+      const int by_lds = (int)((160 * 1024) / std::max<size_t>(1, fa.sharedSizeBytes));
+      b = std::max(1, std::min(by_vgpr, by_lds));
+    }
+    st->sparse_res = b;
+  }
+  return st->sparse_res;
+}
+
 template <class It>
 static hipError_t scan_list(StagedState* st, hipStream_t s, It in, int64_t* out, int n) {
   size_t ts = 0;
@@ -1590,13 +1610,43 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   if (level0) {
     ST_TRY(st->pend.ensure(s, (size_t)N * 4));
     ST_TRY(st->act0.ensure(s, (size_t)N * 4));
-    ST_TRY(launch_fast(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
+    // The first form hands the contigs it leaves at explain_two (or at an unproven
+    // assign-unknown row) over with their level-0 segment tables, every mean evaluated:
+    // k_dump_sparse decides them from the table (pend 3 -> 0, 2 or 1)
+    const bool dump = st->sparse_big != 0 && !st->rollup;
+    SArgs da = sa;
+    if (dump) {
+      const int64_t cap = std::min<int64_t>(std::max<int64_t>((int64_t)N * 32, 1 << 16), (1ll << 31) - 4096);
+      ST_TRY(st->dump_cg.ensure(s, (size_t)cap * 8)); ST_TRY(st->dump_mean.ensure(s, (size_t)cap * 8));
+      ST_TRY(st->dump_first.ensure(s, ((size_t)N + 1) * 4)); ST_TRY(st->dump_list.ensure(s, (size_t)N * 8));
+      ST_TRY(st->dump_ctr.ensure(s, 8));
+      ST_TRY(hipMemsetAsync(st->dump_ctr.p, 0, 8, s));
+      da.dump_cap = cap;
+      da.dump_cg = st->dump_cg.as<int2>(); da.dump_mean = st->dump_mean.as<double>();
+      da.dump_first = st->dump_first.as<int32_t>(); da.dump_list = st->dump_list.as<int32_t>();
+      da.dump_ctr = st->dump_ctr.as<unsigned long long>();
+    }
+    ST_TRY(launch_fast(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
                        st->cus, s));
-    // the contigs it handed over (explain_two, roll-up) through the second wave form, its
-    // list and count built on the device
-    ST_TRY(select_list(st, s, st->pend.as<int32_t>(), st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, N));
+    if (dump) {
+      const int grid = st->cus * sparse_waves(st);
+      ST_TRY(st->sp_ws.ensure(s, (size_t)grid * kSpSlot));
+      da.sp_ws = st->sp_ws.as<char>();
+      da.seg_cg = da.dump_cg; da.seg_mean = da.dump_mean; da.crank_first = da.dump_first;
+      da.seed_pend = st->pend.as<int32_t>();
+      hipLaunchKernelGGL(k_dump_sparse, dim3(grid), dim3(64), 0, s, da, st->cnt.as<int64_t>(),
+                         st->cnt_leaves.as<int64_t>());
+      ST_TRY(hipGetLastError());
+    }
+    // the other contigs it handed over (pend 1) through the second wave form, its list and
+    // count built on the device
+    using PendIt1 = hipcub::TransformInputIterator<bool, PendIs, const int32_t*>;
+    ST_TRY(select_list(st, s, PendIt1(st->pend.as<int32_t>(), PendIs{1}), st->act0.as<int32_t>(),
+                       st->red.as<int64_t>() + 3, N));
+#ifndef WF_NO_FULL
     ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                        st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
+#endif
   } else {
     hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
                        st->cnt_leaves.as<int64_t>(),
@@ -1920,21 +1970,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     if (n_big > 0 && st->sparse_big) {
       // the decision from the segment table, one wave per contig (wf_sparse.h): as many
       // waves as are resident at once (LDS-bound)
-      if (st->sparse_res < 0) {
-        // resident one-wave workgroups per CU from the kernel's own VGPR and LDS use (the
-        // occupancy query returned 4 here: SQ_WAVES of the round-3 cfg5 profile): waves per
-        // SIMD = 512 / VGPRs (granule 8, at most 8), 4 SIMDs; LDS 160 KB per CU
-        hipFuncAttributes fa{};
-        int b = 8;
-        if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_big_sparse)) == hipSuccess) {
-          const int vg = std::max(8, (fa.numRegs + 7) & ~7);
-          const int by_vgpr = 4 * std::min(8, 512 / vg);
-          const int by_lds = (int)((160 * 1024) / std::max<size_t>(1, fa.sharedSizeBytes));
-          b = std::max(1, std::min(by_vgpr, by_lds));
-        }
-        st->sparse_res = b;
-      }
-      const int grid = std::min(n_big, st->cus * st->sparse_res);
+      const int grid = std::min(n_big, st->cus * sparse_waves(st));
       ST_TRY(st->sp_ws.ensure(s, (size_t)grid * kSpSlot));
       sa.sp_ws = st->sp_ws.as<char>();
       hipLaunchKernelGGL(k_big_sparse, dim3(grid), dim3(64), 0, s, sa, level, n_keys);
