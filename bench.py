@@ -302,7 +302,7 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json):
     torch.cuda.empty_cache()
     ph = tm.phases()
     per = lambda k: ph[k][0] / max(1, tm.passes)
-    k2_ms = per("decide") + per("big")
+    k2_ms = per("decide") + per("big") + per("handover")
     # whole-job: pairs and B_k2 summed over ranks, times max over ranks
     v = np.array([counts["pairs"], counts["b_k2_bytes"], kbatch.n_contigs,
                   float((calls == 2).sum())], dtype=np.float64)
@@ -325,7 +325,8 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json):
         "contigs_per_sec": v[2] / pass_s,
         "pass_ms": pass_s * 1e3,
         "explain_two_ms_per_pass": k2_max * 1e3,
-        "explain_two_phases_ms": {"decide": per("decide"), "big": per("big")},
+        "explain_two_phases_ms": {"decide": per("decide"), "big": per("big"),
+                                  "handover": per("handover")},
         "other_phases_ms": {k: per(k) for k in ("waves", "attach", "segments")},
         "b_k2_bytes": v[1], "b_k2_rule": "sum over explain_two contigs of P_pot * G * 8 "
                                         "(SURVEY 8(d): the potential clades' score rows)",

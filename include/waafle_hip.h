@@ -157,6 +157,8 @@ enum wf_phase {
   WF_PHASE_SEGMENTS = 2,      /* staged, per level: sort, segments, exact segment means */
   WF_PHASE_DECIDE = 3,        /* staged, per level: k_one + k_decide (LDS arena) */
   WF_PHASE_BIG = 4,           /* staged, per level: k_big_sparse + k_decide_big */
+  WF_PHASE_HANDOVER = 5,      /* level 0 of the contigs the wave kernels hand over with
+                                 their segment tables (k_dump_sparse) */
   WF_N_PHASES = 8
 };
 typedef struct wf_timing {

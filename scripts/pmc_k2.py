@@ -1,4 +1,4 @@
-"""VALU instructions of the explain_two kernels (k_decide<3...>, k_big_sparse, k_decide_big)
+"""VALU instructions of the explain_two kernels (k_decide<3...>, k_big_sparse, k_dump_sparse, k_decide_big)
 per cfg5 pass, from a rocprofv3 --pmc SQ_INSTS_VALU ... run of bench.py on the cfg5
 6,250-contig share: the `valu` block of bench.py's k2 leg (--k2-pmc-json).
 
@@ -20,7 +20,7 @@ def main():
     f = glob.glob(d + "/**/*counter_collection.csv", recursive=True)[0]
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
-        m = re.search(r"(k_decide_big|k_big_sparse|k_decide<3[^>]*>)", r["Kernel_Name"])
+        m = re.search(r"(k_decide_big|k_big_sparse|k_dump_sparse|k_decide<3[^>]*>)", r["Kernel_Name"])
         if m:
             acc[m.group(1)][r["Counter_Name"]] += float(r["Counter_Value"])
     insts = sum(v["SQ_INSTS_VALU"] for v in acc.values()) / passes

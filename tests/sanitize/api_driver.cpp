@@ -180,7 +180,7 @@ int main() {
   CHECK(wf_score(ctx, &v0, &p, &o0.r) == WF_OK);
   wf_timing tm{};
   CHECK(wf_timing_read(ctx, &tm) == WF_OK && tm.passes == 1 && tm.pass_ms > 0.0);
-  CHECK(tm.phase_spans[WF_PHASE_WAVES] == 1 && tm.phase_ms[WF_PHASE_WAVES] > 0.0);
+  CHECK(tm.phase_spans[WF_PHASE_WAVES] >= 1 && tm.phase_ms[WF_PHASE_WAVES] > 0.0);
   CHECK(wf_timing_enable(ctx, 0) == WF_OK);
   // options: validation, the attachment limit (WF_E_TOOBIG, nothing scored), the
   // segment-table decision forced for every staged contig (same records)

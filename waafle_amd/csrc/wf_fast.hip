@@ -34,6 +34,9 @@
 #ifndef WF_SKIP
 #define WF_SKIP 0
 #endif
+#ifndef WF_LANE_MEANS6
+#define WF_LANE_MEANS6 0
+#endif
 
 namespace wf {
 
@@ -898,7 +901,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
               fail = true;                               // the staged leaf kernels take it
           }
           uint64_t mlist = __ballot(multi);
-          if (FULL && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
+          if ((FULL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
             // several multi-attachment segments (roll-up levels): one lane each
             if (multi) {
               const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
@@ -1020,14 +1023,28 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             }
             return -1.0;
           };
-          for (int t = lane; t < ns; t += 64) {
+          // Option ranks for meld_one.  FULL: by segment (-1: none).  The first form's rank
+          // array would be the attachment scores' (sc), which a hand-over to k_dump_sparse
+          // still needs (pass 6): its options are compacted instead, ranks into the mx
+          // region and clades into the mem region (meld_one compacts them in place), or --
+          // past 64 options -- recomputed there
+          double* opt_r = reinterpret_cast<double*>(F.mx());
+          int* opt_c = F.mem();
+          int nopt = 0;
+          for (int t0 = 0; t0 < ns; t0 += 64) {
+            const int t = t0 + lane;
             double crit = 0.0;
-            const double rk = option_rank(t, crit);
-            if (rk >= 0.0 && better(rk, cg_of(F, t).x, br, bk)) { br = rk; bk = cg_of(F, t).x; bcrit = crit; }
-            // option rank by segment (-1: none).  The first form's rank array is the
-            // attachment scores' (sc), which a hand-over to k_dump_sparse still needs
-            // (pass 6): meld_one recomputes the few options' ranks there instead
-            if (FULL) rank[t] = rk;
+            const double rk = t < ns ? option_rank(t, crit) : -1.0;
+            const int clade = t < ns ? cg_of(F, t).x : 0;
+            if (rk >= 0.0 && better(rk, clade, br, bk)) { br = rk; bk = clade; bcrit = crit; }
+            if (FULL) {
+              if (t < ns) rank[t] = rk;
+            } else {
+              const uint64_t im = __ballot(rk >= 0.0);
+              const int pos = nopt + __popcll(im & lanes_below());
+              if (rk >= 0.0 && pos < 64) { opt_r[pos] = rk; opt_c[pos] = clade; }
+              nopt += __popcll(im);
+            }
           }
     #pragma unroll
           for (int off = 32; off > 0; off >>= 1) {
@@ -1060,7 +1077,13 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
           if (bk >= 0) {
             wave_sync();
             int nm = 0;                                    // meld_one (:621-631): options within --range
-            if (P.dis1 == 1)
+            if (!FULL && P.dis1 == 1 && nopt <= 64) {      // (options in segment order)
+              const bool in = lane < nopt && (br - opt_r[lane]) <= P.range;
+              const int clade = in ? opt_c[lane] : 0;      // read by every lane before the writes
+              const uint64_t im = __ballot(in);
+              if (in) F.mem()[__popcll(im & lanes_below())] = clade;
+              nm = __popcll(im);
+            } else if (P.dis1 == 1)
               for (int t0 = 0; t0 < ns; t0 += 64) {
                 const int t = t0 + lane;
                 double crit_unused;

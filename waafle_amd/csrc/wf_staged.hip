@@ -1605,7 +1605,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   // or HBM annotation slots are needed.
   // (the wave kernels' 32-bit keys hold clade ids below 2^17)
   const bool level0 = st->level0 && !det && (int64_t)max_loci * k.n_sys <= kAnnSlots && sa.key_tb <= 17;
-  const int t_waves = level0 ? t_mark(st, s) : -1;
+  int t_waves = level0 ? t_mark(st, s) : -1;
   hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, sa.k);
   if (level0) {
     ST_TRY(st->pend.ensure(s, (size_t)N * 4));
@@ -1613,7 +1613,11 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     // The first form hands the contigs it leaves at explain_two (or at an unproven
     // assign-unknown row) over with their level-0 segment tables, every mean evaluated:
     // k_dump_sparse decides them from the table (pend 3 -> 0, 2 or 1)
+#ifdef WF_NO_DUMP
+    const bool dump = false;
+#else
     const bool dump = st->sparse_big != 0 && !st->rollup;
+#endif
     SArgs da = sa;
     if (dump) {
       const int64_t cap = std::min<int64_t>(std::max<int64_t>((int64_t)N * 32, 1 << 16), (1ll << 31) - 4096);
@@ -1629,6 +1633,8 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     ST_TRY(launch_fast(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
                        st->cus, s));
     if (dump) {
+      const int t_h0 = t_mark(st, s);
+      t_span(st, WF_PHASE_WAVES, t_waves, t_h0);
       const int grid = st->cus * sparse_waves(st);
       ST_TRY(st->sp_ws.ensure(s, (size_t)grid * kSpSlot));
       da.sp_ws = st->sp_ws.as<char>();
@@ -1637,6 +1643,9 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       hipLaunchKernelGGL(k_dump_sparse, dim3(grid), dim3(64), 0, s, da, st->cnt.as<int64_t>(),
                          st->cnt_leaves.as<int64_t>());
       ST_TRY(hipGetLastError());
+      const int t_h1 = t_mark(st, s);
+      t_span(st, WF_PHASE_HANDOVER, t_h0, t_h1);
+      t_waves = t_h1;                                  // the waves span resumes here
     }
     // the other contigs it handed over (pend 1) through the second wave form, its list and
     // count built on the device

@@ -16,7 +16,7 @@ MODE_STAGED = 0
 MODE_LEVEL0 = 2
 MODE_WAVES = 3
 OPT_SPARSE_BIG, OPT_ATT_LIMIT = 1, 2           # wf_set_option
-PHASES = ("waves", "attach", "segments", "decide", "big")   # wf_phase 0..4
+PHASES = ("waves", "attach", "segments", "decide", "big", "handover")   # wf_phase 0..5
 N_PHASES = 8
 ABI_VERSION = 3
 
