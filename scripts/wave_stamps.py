@@ -1,0 +1,78 @@
+"""Per-phase shader-clock laps of the first wave form (diagnostic build only).
+
+Build:  python -m waafle_amd.build --stamps   (waafle_amd/libwaafle_hip_stamps.so)
+Run:    WAAFLE_HIP_LIB=waafle_amd/libwaafle_hip_stamps.so python scripts/wave_stamps.py [--contigs N]
+
+k_wave<CAP, false> laps every 16th contig (wf_fast.hip WLAP): the sum of the laps is that
+contig's wall time in the wave, so each phase's share is its share of the kernel's time.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PHASES = ["loci+lut", "hits/attach", "annotations", "sort", "segments", "prune setup",
+          "pass select", "means", "post-pass/explain_one", "dump/level end", "record/end",
+          "means lane p6", "means multi p0", "means multi p1/7/6", "means lane p1/7/2",
+          "means prep (all passes)"]
+STATS = {16: "contigs", 17: "attachments", 18: "segments", 19: "pass iterations",
+         20: "segments listed", 21: "dumps", 22: "handed on", 23: "hits"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg4")
+    ap.add_argument("--contigs", type=int, default=None)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--flags", default="")
+    args = ap.parse_args()
+    import numpy as np
+    from waafle_amd import synth
+    n = args.contigs or synth.CONFIGS[args.config]["n"]
+    batch, tax = synth.generate_batch(args.config, 0, n, workers=16, n_total=n)
+    import torch
+    from bench import DeviceBatch
+    from waafle_amd import cli, engine, lib as L
+    so = L.load()
+    so.wf_stamps_read_fast.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    h = C.c_void_p()
+    assert so.wf_init(0, C.byref(h)) == 0
+    ts = engine.taxonomy_struct(tax)
+    assert so.wf_set_taxonomy(h, C.byref(ts)) == 0
+    stream = torch.cuda.current_stream()
+    so.wf_set_stream(h, C.c_void_p(stream.cuda_stream))
+    params = engine.params_struct(cli.param_dict(cli.parse_flags(args.flags.split())))
+    db = DeviceBatch(batch, torch.device("cuda", 0))
+    for i in range(args.steps):
+        if i == args.steps - 1:
+            torch.cuda.synchronize()
+            so.wf_stamps_reset_fast()
+        assert so.wf_score(h, C.byref(db.bs), C.byref(params), C.byref(db.rs)) == 0
+    torch.cuda.synchronize()
+    st = (C.c_ulonglong * 48)()
+    so.wf_stamps_read_fast(st, 48)
+    v = [int(x) for x in st]
+    tot = sum(v[:16])
+    nc = max(1, v[16])
+    out = {"config": args.config, "contigs": n, "flags": args.flags, "sampled": v[16],
+           "cycles_per_contig": tot / nc,
+           "phases": {p: {"cycles_per_contig": v[i] / nc, "frac": v[i] / max(1, tot)}
+                      for i, p in enumerate(PHASES)},
+           "stats_per_contig": {name: v[i] / nc for i, name in STATS.items()},
+           "pass_entries_per_contig": {str(p): v[24 + p] / nc for p in range(8)},
+           "one_run_mean_p0": {k: v[32 + i] / nc for i, k in enumerate(
+               ["classify", "boundary leaves", "inside leaves", "fold+div"])}}
+    print(json.dumps(out))
+    for p, d in out["phases"].items():
+        print("{:24s} {:10.0f} cyc  {:5.1f}%".format(p, d["cycles_per_contig"], 100 * d["frac"]),
+              file=sys.stderr)
+    print(out["stats_per_contig"], out["pass_entries_per_contig"], out["one_run_mean_p0"],
+          file=sys.stderr)
+    so.wf_free(h)
+
+
+if __name__ == "__main__":
+    main()

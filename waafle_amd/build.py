@@ -68,25 +68,39 @@ def build(force=False, verbose=True, stamps=False, defines=(), out=None):
     if not force and up_to_date(lib):
         return lib
     extra = (["-DWF_STAMPS"] if stamps else []) + ["-D" + d for d in defines]
-    # one compile per source, in parallel, then a link step
+    # one compile per source, in parallel, then a link step.  Objects are kept per library
+    # (waafle_amd/.objs/<lib>/, git- and gpurun-ignored) and recompiled only when their
+    # source or a header is newer, so an edit to one kernel file rebuilds that file alone.
     cflags = [f for f in FLAGS if f != "-shared"]
+    odir = os.path.join(HERE, ".objs", os.path.basename(lib))
+    os.makedirs(odir, exist_ok=True)
+    stamp = os.path.join(odir, "flags")
+    flags_txt = " ".join(cflags + extra)
+    same_flags = os.path.exists(stamp) and open(stamp).read() == flags_txt
+    headers = [d for d in DEPS if d not in SOURCES]
     objs, procs = [], []
     for src in SOURCES:
-        obj = "{}.{}.o".format(lib, os.path.splitext(os.path.basename(src))[0])
+        obj = os.path.join(odir, os.path.splitext(os.path.basename(src))[0] + ".o")
+        objs.append(obj)
+        if (same_flags and os.path.exists(obj) and
+                all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in [src] + headers)):
+            continue
         cmd = [hipcc()] + cflags + extra + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append(subprocess.Popen(cmd))
-        objs.append(obj)
     rcs = [p.wait() for p in procs]
     if any(rcs):
+        for o in objs:                       # a failed compile leaves no stale object
+            if os.path.exists(o) and not same_flags:
+                os.remove(o)
         raise subprocess.CalledProcessError(max(rcs), "hipcc -c")
+    with open(stamp, "w") as fh:
+        fh.write(flags_txt)
     cmd = [hipcc()] + FLAGS + objs + ["-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    for o in objs:
-        os.remove(o)
     os.replace(lib + ".tmp", lib)
     return lib
 

@@ -59,6 +59,80 @@ constexpr int kXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its 
 #ifndef WF_PREFETCH0
 #define WF_PREFETCH0 0
 #endif
+// Diagnostic build only (-DWF_STAMPS): per-phase shader-clock laps of the first form on
+// every 16th contig, plus counters (scripts/wave_stamps.py reads them).  Never in the
+// product build.
+#ifdef WF_STAMPS
+__device__ unsigned long long g_wstamps[48];
+#define WLAP_MARK() unsigned long long wlap_ = __builtin_amdgcn_s_memtime(); const bool wsamp_ = !FULL && (c & 15) == 0
+#define WLAP(i)                                                                     \
+  do {                                                                              \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
+    if (wsamp_ && lane == 0) atomicAdd(&g_wstamps[i], n_ - wlap_);                  \
+    wlap_ = n_;                                                                     \
+  } while (0)
+#define WSTAT(i, v) do { if (wsamp_ && lane == 0) atomicAdd(&g_wstamps[i], (unsigned long long)(v)); } while (0)
+#define OLAP(i)                                                                     \
+  do {                                                                              \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
+    if (samp && lane_id() == 0) atomicAdd(&g_wstamps[i], n_ - lap);                 \
+    lap = n_;                                                                       \
+  } while (0)
+// one_run_mean (wf_device.h) with laps: classify, boundary leaves, inside leaves, fold
+template <class LT>
+__device__ __forceinline__ double one_run_mean_st(LT lt, int nl, int len, int lo, int hi, double v, bool samp) {
+  unsigned long long lap = __builtin_amdgcn_s_memtime();
+  hi = max(hi, lo);
+  int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
+  int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
+#pragma unroll 4
+  for (int q = 0; q < nl; ++q) {
+    const int4 e = lt(q);
+    const int le = e.x + e.y;
+    const bool in = lo <= e.x && le <= hi && lo < hi;
+    const bool out = le <= lo || e.x >= hi || lo >= hi;
+    if (!in && !out) {
+      if (pst0 < 0) { pst0 = e.x; pln0 = e.y; } else { pst1 = e.x; pln1 = e.y; }
+    } else if (in && e.y != L0 && e.y != L1 && e.y != L2 && e.y != L3) {
+      if (L0 < 0) L0 = e.y; else if (L1 < 0) L1 = e.y; else if (L2 < 0) L2 = e.y; else L3 = e.y;
+    }
+  }
+  OLAP(32);
+  const double vp0 = pst0 >= 0 ? run_leaf(lo, hi, v, pst0, pln0) : 0.0;
+  const double vp1 = pst1 >= 0 ? run_leaf(lo, hi, v, pst1, pln1) : 0.0;
+  OLAP(33);
+  auto inside = [&](int ln) -> double {
+    if (ln < 0) return 0.0;
+    double b = 0.0;
+    for (int i = 0; i < (ln >> 3); ++i) b += v;
+    double res = 8.0 * b;
+    for (int x = ln & ~7; x < ln; ++x) res += v;
+    return res;
+  };
+  const double V0 = inside(L0), V1 = inside(L1), V2 = inside(L2), V3 = inside(L3);
+  OLAP(34);
+  SumStack stk;
+#pragma unroll 4
+  for (int q = 0; q < nl; ++q) {
+    const int4 e = lt(q);
+    const int le = e.x + e.y;
+    const bool in = lo <= e.x && le <= hi && lo < hi;
+    const bool out = le <= lo || e.x >= hi || lo >= hi;
+    double x = 0.0;
+    if (in) x = e.y == L0 ? V0 : e.y == L1 ? V1 : e.y == L2 ? V2 : V3;
+    else if (!out) x = e.x == pst0 ? vp0 : vp1;
+    stk.push(x);
+    for (int a = 0; a < e.z; ++a) stk.add_top();
+  }
+  const double r = (0.0 + stk.s0) / (double)len;
+  OLAP(35);
+  return r;
+}
+#else
+#define WLAP_MARK() do {} while (0)
+#define WLAP(i) do {} while (0)
+#define WSTAT(i, v) do {} while (0)
+#endif
 constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two ...
 #ifndef WF_KS0
 #define WF_KS0 640
@@ -123,6 +197,19 @@ static_assert(sizeof(WaveSmem<256, true>) <= 160 * 1024 / 8, "FULL slice: 8 wave
 __device__ __forceinline__ int leaves_for(const SArgs& S, int len) {
   return (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
          (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+}
+
+// The kernel's first argument (at kernarg offset 0), through a pointer the compiler cannot
+// see through: loads of its fields are not hoisted out of the loop that calls this.
+template <class T>
+__device__ __forceinline__ const T& kernarg_fresh(const T& arg) {
+#ifdef __HIP_DEVICE_COMPILE__
+  uint64_t a = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(a));
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(a);
+#else
+  return arg;                                        // (host pass: never executed)
+#endif
 }
 
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
@@ -523,15 +610,12 @@ template <int CAP, bool FULL>
 // rollup (FULL): carry a contig through its roll-up levels in the slice; else hand it to
 // the staged kernels at its first raise (they run every contig of a level together,
 // which measured 3x faster per contig-level on cfg4 than one wave per contig here).
-__global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
+__global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
                                              const int32_t* list, int n_list, const int64_t* n_dev, int rollup) {
   if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
-  const KArgs& K = S.k;
-  const DevParams& P = K.p;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WaveSmem<CAP, FULL>& F = *reinterpret_cast<WaveSmem<CAP, FULL>*>(smem);
   const int lane = threadIdx.x;
-  const int nsys = K.n_sys;
   // XCD-aware contig order.  Workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8),
   // so a plain grid stride puts neighbouring contigs on different XCDs, and the record
   // fields of 8 neighbours (1-8 B each, one array per field) share cache lines that 8 L2s
@@ -543,6 +627,15 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
     const int ci = xmap ? (it * kXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
     if (ci >= n_list) break;
     const int c = list ? list[ci] : ci;
+    WLAP_MARK();
+    // The argument block (~1 KB: some 40 array pointers and the parameters) is re-read per
+    // contig through an opaque copy of the kernarg pointer (scalar loads, constant cache):
+    // held across the whole persistent loop its fields overflowed the SGPR file (204 SGPRs
+    // spilled to VGPR lanes, a v_readlane + wait states per use).
+    const SArgs& S = kernarg_fresh<SArgs>(S_arg);
+    const KArgs& K = S.k;
+    const DevParams& P = K.p;
+    const int nsys = K.n_sys;
     // --weak-loci assign-unknown: the second form leaves every contig the first one handed
     // over to the staged kernels (its pend / counts stand); they carry the virtual row
     if (FULL && P.weak == 2) continue;
@@ -601,28 +694,51 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
         F.lut[i] = pack_leaf(S.lut[S.lut_off[F.len[g]] + (i - F.lbase[g])]);
       }
 
+    WLAP(0);
     // ---- hits -> attachments, in (hit, locus) order (orgscorer.py:359-382) ----
     int n_att = 0;
     long long nl_sum = 0;
-    for (int64_t hb = h0; hb < h1; hb += 64) {
-      const int64_t h = hb + lane;
-      int qlo = 0, qhi = 0, hs = 0, clade = 0;
-      double scv = 0.0, sc = 0.0;
-      uint32_t m = 0u;
+    // kHB batches of 64 hits per round: every field of all of them is loaded up front (one
+    // global round trip per round instead of one per batch), then the batches are attached
+    // in order, each picking its fields from the round's registers by a uniform select
+    constexpr int kHB = 4;
+    for (int64_t hq = h0; hq < h1; hq += 64 * kHB) {
+      int r_qlo[kHB], r_qhi[kHB], r_hs[kHB], r_cl[kHB];
+      double r_scv[kHB], r_sc[kHB];
+      uint32_t r_m[kHB];
+#pragma unroll
+      for (int b = 0; b < kHB; ++b) {
+        const int64_t h = hq + 64 * b + lane;
+        r_qlo[b] = 0; r_qhi[b] = 0; r_hs[b] = 0; r_cl[b] = 0;
+        r_scv[b] = 0.0; r_sc[b] = 0.0; r_m[b] = 0u;
 #if WF_PREFETCH0
-      if (h < h1 && hb == h0) {
-        scv = p_scv; qlo = p_qlo; qhi = p_qhi; hs = p_hs; clade = p_clade; sc = p_sc; m = p_m;
-      } else
+        if (h < h1 && hq == h0 && b == 0) {
+          r_scv[b] = p_scv; r_qlo[b] = p_qlo; r_qhi[b] = p_qhi; r_hs[b] = p_hs; r_cl[b] = p_clade;
+          r_sc[b] = p_sc; r_m[b] = p_m;
+        } else
 #endif
-      if (h < h1) {                                  // every field in one round of loads
-        scv = K.scov[h];
-        qlo = K.qlo[h];
-        qhi = K.qhi[h];
-        hs = K.hstrand[h];
-        clade = K.taxon[h];
-        sc = K.score[h];
-        if (nsys > 0) m = K.sysmask[h];
+        if (h < h1) {
+          r_scv[b] = K.scov[h];
+          r_qlo[b] = K.qlo[h];
+          r_qhi[b] = K.qhi[h];
+          r_hs[b] = K.hstrand[h];
+          r_cl[b] = K.taxon[h];
+          r_sc[b] = K.score[h];
+          if (nsys > 0) r_m[b] = K.sysmask[h];
+        }
       }
+    for (int bq = 0; bq < kHB && hq + 64 * bq < h1; ++bq) {
+      const int64_t hb = hq + 64 * bq;
+      const int64_t h = hb + lane;
+      int qlo = r_qlo[0], qhi = r_qhi[0], hs = r_hs[0], clade = r_cl[0];
+      double scv = r_scv[0], sc = r_sc[0];
+      uint32_t m = r_m[0];
+#pragma unroll
+      for (int b = 1; b < kHB; ++b)
+        if (bq == b) {
+          qlo = r_qlo[b]; qhi = r_qhi[b]; hs = r_hs[b]; clade = r_cl[b];
+          scv = r_scv[b]; sc = r_sc[b]; m = r_m[b];
+        }
       int n = 0;
       uint64_t am = 0;
       if (ordered) {
@@ -685,10 +801,15 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       n_att += total;
     }
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nl_sum += __shfl_xor(nl_sum, off, 64);
     staged = staged || n_att > CAP;
     wave_sync();
+    WLAP(1);
+    WSTAT(16, 1);
+    WSTAT(17, n_att);
+    WSTAT(23, h1 - h0);
     if (!staged && G > 0 && nsys > 0) {
       // annotation pass 2: the last hit (largest index) at the best score per (locus, system)
       for (int t = lane; t < n_att; t += 64) {
@@ -703,6 +824,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       wave_sync();
       if (lane < nann) K.annot[l0 * nsys + lane] = F.ahit()[lane];
     }
+    WLAP(2);
     // ---- levels: sort, segments, means, explain_one [, explain_two, roll-up] ----
     int64_t pair_evals = 0;
     bool seed = false;                                 // raised at level 0: staged level 1 seed
@@ -718,6 +840,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
         wave_sync();
       }
       if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64>(F, n_att);   // one network: code size
+      WLAP(3);
       // ---- segments = runs of equal (clade, locus) ----
       int ns = 0;
       for (int t0 = 0; t0 < n_att; t0 += 64) {
@@ -729,6 +852,8 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       if (lane == 0) F.seg[ns] = (uint32_t)n_att;    // end of the last segment (n_att <= CAP)
       wave_sync();
+      WLAP(4);
+      WSTAT(18, ns);
       // ---- segment means (numpy pairwise order, exact), evaluated pass by pass ----
       // Only what the decision can use is evaluated (exact for k1 > 0):
       //  - explain_one: an option has crit >= k1 > 0, so a segment on every unmasked locus;
@@ -782,11 +907,34 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
         return ub;
       };
       if (prune) {
-        for (int t = lane; t < ns; t += 64) {
-          v[t] = -1.0;                                 // not evaluated
-          if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
-            const int cnt = run_count(t, ~0ull);
-            for (int q = t; q < t + cnt; ++q) rc[q] = (uint8_t)cnt;
+        // every segment's clade-run size, from the run heads' ballot masks: a lane's run
+        // starts at the last head at or before it and ends at the next head after it
+        constexpr int kCh = (CAP + 63) / 64;
+        uint64_t hd[kCh];
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+          const int t = 64 * i + lane;
+          hd[i] = __ballot(t < ns && (t == 0 || (F.seg[t - 1] >> kCladeShift) != (F.seg[t] >> kCladeShift)));
+        }
+        const uint64_t le = lane == 63 ? ~0ull : (2ull << lane) - 1ull;   // lanes <= this one
+        int rs[kCh];
+        int carry = 0;
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {                // run starts, chunk by chunk
+          const uint64_t m = hd[i] & le;
+          rs[i] = m ? 64 * i + 63 - __clzll(m) : carry;
+          carry = hd[i] ? 64 * i + 63 - __clzll(hd[i]) : carry;
+        }
+        carry = ns;
+#pragma unroll
+        for (int i = kCh - 1; i >= 0; --i) {           // run ends, backwards
+          const int t = 64 * i + lane;
+          const uint64_t m = hd[i] & ~le;
+          const int re = m ? 64 * i + __ffsll((unsigned long long)m) - 1 : carry;
+          carry = hd[i] ? 64 * i + __ffsll((unsigned long long)hd[i]) - 1 : carry;
+          if (t < ns) {
+            v[t] = -1.0;                               // not evaluated
+            rc[t] = (uint8_t)(re - rs[i]);
           }
         }
         wave_sync();
@@ -799,7 +947,11 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       // (pass 6 evaluates the rest) instead of the staged kernels
       bool dump = false;
       const bool can_dump = !FULL && S.dump_cap > 0;
+      WLAP(5);
       for (int pass = prune ? 0 : 3;;) {
+        WLAP(8);
+        WSTAT(19, 1);
+        WSTAT(24 + pass, 1);
         int n = ns;
         const uint16_t* list = nullptr;
         if (pass == 1) {                               // per open locus: its best attachment score
@@ -854,10 +1006,15 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
           wave_sync();
           list = lst;
         }
+        WLAP(6);
+        WSTAT(20, n);
         for (int s0 = 0; s0 < n; s0 += 64) {
           const int s = s0 + lane < n ? (list ? (int)list[s0 + lane] : s0 + lane) : ns;
           bool multi = false, big = false;               // big: too many attachments for the wave path
           int g = 0, len = 0, nl = 0;
+          bool one_run = false;                          // one envelope run [lo, hi) of value vv
+          int lo = 0, hi = 0;
+          double vv = 0.0;
           if (WF_SKIP & 1) {
             if (s < ns) v[s] = 0.75;
           } else if (s < ns) {
@@ -866,9 +1023,6 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             len = F.len[g];
             nl = F.nl1[g];
             const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
-            bool one_run = false;
-            int lo = 0, hi = 0;
-            double vv = 0.0;
             if (na == 1) {
               if (thread_ok) {
                 const int slot = (int)(F.key[kb] & kSlotMask);
@@ -891,15 +1045,21 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
               }
               if (kept == 0 && thread_ok) { lo = 0; hi = len; vv = Fw; one_run = true; }
             }
-            if (one_run)
-              v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
-            else if ((FULL || na <= kMultiAttL0) && nl <= 64 && len < kNpyBuf) {
+            if (one_run) {
+            } else if ((FULL || na <= kMultiAttL0) && nl <= 64 && len < kNpyBuf) {
               multi = true;
               big = na > kMultiAtt0;
             }
             else
               fail = true;                               // the staged leaf kernels take it
           }
+          WLAP(15);
+#ifdef WF_STAMPS
+          if (one_run) v[s] = one_run_mean_st(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv, wsamp_ && pass == 0);
+#else
+          if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
+#endif
+          WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));
           uint64_t mlist = __ballot(multi);
           if ((FULL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
             // several multi-attachment segments (roll-up levels): one lane each
@@ -924,8 +1084,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
             const double mean = wave_seg_mean(PackedLut{F.lut + F.lbase[g2]}, nl2, len2, lo, hi, sc, F.runs());
             if (lane == 0) v[s2] = mean;
           }
+          WLAP(pass == 0 ? 12 : 13);
         }
         wave_sync();
+        WLAP(7);
         // after the pass: the weak-locus mask, explain_one, the next pass
         bool e1_now = false;
         if (pass == 0) {
@@ -1137,6 +1299,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       }
       staged = staged || __ballot(fail) != 0ull;
       wave_sync();
+      WLAP(8);
       if (dump && !staged) {
         // the table: one 64-bit atomic gives the slot (high bits) and its first entry (low
         // 40), so slot k's entries start where slot k - 1's end
@@ -1158,8 +1321,11 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
           S.dump_list[2 * slot + 1] = dumped ? c : -1;
         }
         staged = true;                                 // (its attachment counts stand)
+        WSTAT(21, 1);
+        WLAP(9);
         break;
       }
+      WLAP(9);
       if (staged || outcome == 2) break;
       const int Gu = __popcll(um);
       wave_sync();
@@ -1194,7 +1360,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S, int64_
       cleaves[c] = staged ? nl_sum : 0;
       pend[c] = staged ? (dumped ? 3 : (seed ? 2 : 1)) : 0;
     }
+    WSTAT(22, staged ? 1 : 0);
     wave_sync();                                       // the slice is reused by the next contig
+    WLAP(10);
   }
 }
 
@@ -1227,6 +1395,17 @@ hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t*
 }
 
 }  // namespace
+
+#ifdef WF_STAMPS
+extern "C" int wf_stamps_read_fast(unsigned long long* out, int n) {
+  if (n > 48) n = 48;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
+}
+extern "C" int wf_stamps_reset_fast(void) {
+  unsigned long long z[48] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_wstamps), z, sizeof z) == hipSuccess ? 0 : -2;
+}
+#endif
 
 hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                        hipStream_t s) {
