@@ -63,13 +63,13 @@ def main():
                       for i, p in enumerate(PHASES)},
            "stats_per_contig": {name: v[i] / nc for i, name in STATS.items()},
            "pass_entries_per_contig": {str(p): v[24 + p] / nc for p in range(8)},
-           "one_run_mean_p0": {k: v[32 + i] / nc for i, k in enumerate(
-               ["classify", "boundary leaves", "inside leaves", "fold+div"])}}
+           "explain_one": {k: v[32 + i] / nc for i, k in enumerate(
+               ["sure bits/pass choice", "option scan", "reduction", "meld_one+LCA"])}}
     print(json.dumps(out))
     for p, d in out["phases"].items():
         print("{:24s} {:10.0f} cyc  {:5.1f}%".format(p, d["cycles_per_contig"], 100 * d["frac"]),
               file=sys.stderr)
-    print(out["stats_per_contig"], out["pass_entries_per_contig"], out["one_run_mean_p0"],
+    print(out["stats_per_contig"], out["pass_entries_per_contig"], out["explain_one"],
           file=sys.stderr)
     so.wf_free(h)
 

@@ -15,7 +15,7 @@ SOURCES = [os.path.join(CSRC, "wf_staged.hip"), os.path.join(CSRC, "wf_fast.hip"
            os.path.join(CSRC, "wf_genecall.hip"), os.path.join(CSRC, "wf_junctions.hip"),
            os.path.join(CSRC, "wf_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "wf_internal.h"), os.path.join(CSRC, "wf_device.h"),
-                  os.path.join(CSRC, "wf_sparse.h"),
+                  os.path.join(CSRC, "wf_sparse.h"), os.path.join(CSRC, "wf_lanes.h"),
                   os.path.join(REPO, "include", "waafle_hip.h")]
 
 # -ffp-contract=off: no a*b+c fusion anywhere, so float64 results match numpy bit-for-bit.
@@ -105,6 +105,26 @@ def build(force=False, verbose=True, stamps=False, defines=(), out=None):
     return lib
 
 
+LANES_SRC = os.path.join(REPO, "tests", "lanes", "lanes_check.hip")
+LANES_BIN = os.path.join(REPO, "tests", "lanes", "lanes_check")
+
+
+def build_lanes_check(force=False, verbose=True):
+    """The GPU check program of the cross-lane primitives (csrc/wf_lanes.h), run by
+    tests/test_gpu_lanes.py."""
+    deps = [LANES_SRC, os.path.join(CSRC, "wf_lanes.h")]
+    if not force and os.path.exists(LANES_BIN) and all(
+            os.path.getmtime(d) <= os.path.getmtime(LANES_BIN) for d in deps):
+        return LANES_BIN
+    cmd = [hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-result",
+           "-I" + CSRC, LANES_SRC, "-o", LANES_BIN + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LANES_BIN + ".tmp", LANES_BIN)
+    return LANES_BIN
+
+
 if __name__ == "__main__":
     for arg in sys.argv[1:]:
         if arg.startswith("--variant="):      # --variant=NAME:DEF1,DEF2 -> libwaafle_hip_NAME.so
@@ -114,5 +134,6 @@ if __name__ == "__main__":
             sys.exit(0)
     build(force="--force" in sys.argv)
     build_ingest(force="--force" in sys.argv)
+    build_lanes_check(force="--force" in sys.argv)
     if "--stamps" in sys.argv:
         build(force="--force" in sys.argv, stamps=True)

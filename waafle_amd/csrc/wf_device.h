@@ -545,9 +545,74 @@ struct PackedLut {
   }
 };
 
+// numpy's pairwise sum of n copies of v (n < kNpyBuf: one buffer) from registers alone,
+// without the leaf table.  A node of size n > 128 splits into 8*floor(n/16) (left) and the
+// rest, so the right-most nodes (the spine) have sizes = n mod 8 and every other node is a
+// multiple of 8.  Those are 8*B_d or 8*(B_d + 1) at depth d, B_d = a0 >> d with a0 the top
+// split's left size / 8, and the spine's left sibling at depth d is one of the two.  So
+// with Q(x) = the sum over 8x sites (8 * seqsum(v, x) for x <= 16, else Q(floor(x/2)) +
+// Q(ceil(x/2))) one pair (Q(B_d), Q(B_d + 1)) per depth carries the whole tree: bottom pair
+// from seqsum captures (seqsum(v, x + 1) = seqsum(v, x) + v exactly), each pair above from
+// the one below, and the spine sum adds its left sibling's Q level by level.  Equal to the
+// leaf-table walk bit for bit for every n < 8192 (tests/test_pw_const.py checks the model).
+__device__ __forceinline__ double pw_const_sum(int n, double v) {
+  const int a0 = n >> 4;
+  int K = 0, m = n;
+  unsigned sel = 0;                                  // bit d: the spine's sibling is 8*(B_d + 1)
+  while (m > 128) {
+    const int a = m >> 4;
+    sel |= (a != (a0 >> K) ? 1u : 0u) << K;
+    m -= 8 * a;
+    ++K;
+  }
+  int Db = 0, Dmax = -1, xB = 0, xC = 0;
+  bool need16 = false;
+  if (K > 0) {
+    Db = max(0, 28 - __clz(a0));                     // first depth with B_d <= 15
+    Dmax = max(K - 1, Db);
+    xB = a0 >> Db;
+    xC = Dmax == Db + 1 ? a0 >> (Db + 1) : 0;
+    need16 = Db >= 1 && (a0 >> (Db - 1)) == 16;      // Q(16) is a leaf, not Q(8) + Q(8)
+  }
+  const int mL = m < 8 ? m : m >> 3;                 // the spine leaf's accumulator length
+  const int imax = max(max(xB, mL), need16 ? 16 : 0);
+  double t = 0.0, sB = 0.0, sC = 0.0, sL = 0.0;
+  for (int i = 1; i <= imax; ++i) {                  // seqsum(v, i), captured where needed
+    t += v;
+    sB = i == xB ? t : sB;
+    sC = i == xC ? t : sC;
+    sL = i == mL ? t : sL;
+  }
+  double R;
+  if (m < 8) {
+    R = sL;
+  } else {
+    R = 8.0 * sL;
+    for (int x = 0; x < (m & 7); ++x) R += v;
+  }
+  double q0 = 0.0, q1 = 0.0;
+  for (int d = Dmax; d >= 0; --d) {
+    const int B = a0 >> d;
+    if (d >= Db) {
+      const double sd = d == Db ? sB : sC;
+      q0 = 8.0 * sd;
+      q1 = 8.0 * (sd + v);
+    } else {
+      const double c0 = q0, c1 = q1;
+      q0 = (B & 1) ? c0 + c1 : c0 + c0;
+      q1 = (B & 1) ? c1 + c1 : c0 + c1;
+      if (B == 16) q0 = 8.0 * t;                     // t = seqsum(v, 16) (imax = 16)
+    }
+    if (d < K) R = (((sel >> d) & 1u) ? q1 : q0) + R;
+  }
+  return R;
+}
+
 template <class LT>
 __device__ __forceinline__ double one_run_mean(LT lt, int nl, int len, int lo, int hi, double v) {
   hi = max(hi, lo);
+  if (lo <= 0 && hi >= len && len < kNpyBuf)         // one run over the whole locus
+    return (0.0 + pw_const_sum(len, v)) / (double)len;
   int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
   int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
 #pragma unroll 4

@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "wf_device.h"
+#include "wf_lanes.h"
 
 // WF_SKIP (diagnostic variants only, never the product build): 1 skips the segment means,
 // 2 the sort, 4 explain_one, 8 everything after the attachments, 16 explain_two (FULL),
@@ -72,62 +73,6 @@ __device__ unsigned long long g_wstamps[48];
     wlap_ = n_;                                                                     \
   } while (0)
 #define WSTAT(i, v) do { if (wsamp_ && lane == 0) atomicAdd(&g_wstamps[i], (unsigned long long)(v)); } while (0)
-#define OLAP(i)                                                                     \
-  do {                                                                              \
-    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
-    if (samp && lane_id() == 0) atomicAdd(&g_wstamps[i], n_ - lap);                 \
-    lap = n_;                                                                       \
-  } while (0)
-// one_run_mean (wf_device.h) with laps: classify, boundary leaves, inside leaves, fold
-template <class LT>
-__device__ __forceinline__ double one_run_mean_st(LT lt, int nl, int len, int lo, int hi, double v, bool samp) {
-  unsigned long long lap = __builtin_amdgcn_s_memtime();
-  hi = max(hi, lo);
-  int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
-  int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
-#pragma unroll 4
-  for (int q = 0; q < nl; ++q) {
-    const int4 e = lt(q);
-    const int le = e.x + e.y;
-    const bool in = lo <= e.x && le <= hi && lo < hi;
-    const bool out = le <= lo || e.x >= hi || lo >= hi;
-    if (!in && !out) {
-      if (pst0 < 0) { pst0 = e.x; pln0 = e.y; } else { pst1 = e.x; pln1 = e.y; }
-    } else if (in && e.y != L0 && e.y != L1 && e.y != L2 && e.y != L3) {
-      if (L0 < 0) L0 = e.y; else if (L1 < 0) L1 = e.y; else if (L2 < 0) L2 = e.y; else L3 = e.y;
-    }
-  }
-  OLAP(32);
-  const double vp0 = pst0 >= 0 ? run_leaf(lo, hi, v, pst0, pln0) : 0.0;
-  const double vp1 = pst1 >= 0 ? run_leaf(lo, hi, v, pst1, pln1) : 0.0;
-  OLAP(33);
-  auto inside = [&](int ln) -> double {
-    if (ln < 0) return 0.0;
-    double b = 0.0;
-    for (int i = 0; i < (ln >> 3); ++i) b += v;
-    double res = 8.0 * b;
-    for (int x = ln & ~7; x < ln; ++x) res += v;
-    return res;
-  };
-  const double V0 = inside(L0), V1 = inside(L1), V2 = inside(L2), V3 = inside(L3);
-  OLAP(34);
-  SumStack stk;
-#pragma unroll 4
-  for (int q = 0; q < nl; ++q) {
-    const int4 e = lt(q);
-    const int le = e.x + e.y;
-    const bool in = lo <= e.x && le <= hi && lo < hi;
-    const bool out = le <= lo || e.x >= hi || lo >= hi;
-    double x = 0.0;
-    if (in) x = e.y == L0 ? V0 : e.y == L1 ? V1 : e.y == L2 ? V2 : V3;
-    else if (!out) x = e.x == pst0 ? vp0 : vp1;
-    stk.push(x);
-    for (int a = 0; a < e.z; ++a) stk.add_top();
-  }
-  const double r = (0.0 + stk.s0) / (double)len;
-  OLAP(35);
-  return r;
-}
 #else
 #define WLAP_MARK() do {} while (0)
 #define WLAP(i) do {} while (0)
@@ -214,21 +159,11 @@ __device__ __forceinline__ const T& kernarg_fresh(const T& arg) {
 
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
-__device__ __forceinline__ int wave_excl_scan(int v, int* total) {
-  const int lane = lane_id();
-  int x = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  *total = __shfl(x, 63, 64);
-  return x - v;
-}
+// (every lane active: wf_lanes.h)
+__device__ __forceinline__ int wave_excl_scan(int v, int* total) { return wave_excl_scan_dpp(v, total); }
 
 __device__ __forceinline__ int wave_lca(const KArgs& K, int acc) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) acc = lca2(K, acc, __shfl_xor(acc, off, 64));
+  each_stride([&](auto J) { acc = lca2(K, acc, xor_lanes<decltype(J)::value>(acc)); });
   return acc;
 }
 
@@ -262,7 +197,7 @@ __device__ __forceinline__ void wave_sort(T (&x)[R]) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int i = lane + 64 * r;
-        const T y = __shfl_xor(x[r], j, 64);
+        const T y = xor_lanes_rt(x[r], j);
         const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
         x[r] = keep_min ? (y < x[r] ? y : x[r]) : (y > x[r] ? y : x[r]);
       }
@@ -509,12 +444,11 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
       if (better(r, key, br, bk)) { br = r; bk = key; }
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double r2 = __shfl_xor(br, off, 64);
-    const long long k2 = __shfl_xor(bk, off, 64);
+  each_stride([&](auto J) {
+    const double r2 = xor_lanes<decltype(J)::value>(br);
+    const long long k2 = xor_lanes<decltype(J)::value>(bk);
     if (better(r2, k2, br, bk)) { br = r2; bk = k2; }
-  }
+  });
   if (bk >= 0) {
     const int bi = (int)(bk / Pp), bj = (int)(bk % Pp);
     int b_ok = 0, b_dir = 0, b_c1p = 0, b_c2p = 0;
@@ -524,9 +458,9 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
       b_ok = e.ok; b_dir = e.dir; b_c1p = e.c1p; b_c2p = e.c2p;
       bcrit = pair_crit(C, bi, bj, Gu);
     }
-    b_ok = __shfl(b_ok, 0, 64); b_dir = __shfl(b_dir, 0, 64);
-    b_c1p = __shfl(b_c1p, 0, 64); b_c2p = __shfl(b_c2p, 0, 64);
-    bcrit = __shfl(bcrit, 0, 64);
+    b_ok = lane_bcast(b_ok, 0); b_dir = lane_bcast(b_dir, 0);
+    b_c1p = lane_bcast(b_c1p, 0); b_c2p = lane_bcast(b_c2p, 0);
+    bcrit = lane_bcast(bcrit, 0);
     wave_sync();
     // pass 2: options within --range of the best get the LGT filters (:636-639)
     int n_in = 0;
@@ -546,12 +480,9 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
         b2 |= 1ull << e.c2p;
       }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      n_in += __shfl_xor(n_in, off, 64);
-      b1 |= __shfl_xor(b1, off, 64);
-      b2 |= __shfl_xor(b2, off, 64);
-    }
+    n_in = wave_sum_dpp(n_in);
+    b1 = wave_or_dpp(b1);
+    b2 = wave_or_dpp(b2);
     all_ok = __ballot(!all_ok) == 0ull;
     all_same = __ballot(!all_same) == 0ull;
     // meld_two (:640-669): 0 none, 1 best as is, 2 meld, 3 unchecked best, 4 upstream crash
@@ -802,8 +733,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
       n_att += total;
     }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) nl_sum += __shfl_xor(nl_sum, off, 64);
+    nl_sum = wave_sum_dpp(nl_sum);
     staged = staged || n_att > CAP;
     wave_sync();
     WLAP(1);
@@ -896,8 +826,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           const int2 cg = cg_of(F, t);
           if (cg.x != K.unknown && v[t] >= 0.0 && v[t] >= P.kmin) b |= 1ull << cg.y;
         }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) b |= __shfl_xor(b, off, 64);
+        b = wave_or_dpp(b);
         return b;
       };
       auto best_score = [&](int t) -> double {       // upper bound of segment t's mean
@@ -1054,11 +983,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
               fail = true;                               // the staged leaf kernels take it
           }
           WLAP(15);
-#ifdef WF_STAMPS
-          if (one_run) v[s] = one_run_mean_st(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv, wsamp_ && pass == 0);
-#else
           if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
-#endif
           WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));
           uint64_t mlist = __ballot(multi);
           if ((FULL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
@@ -1071,9 +996,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           }
           for (uint64_t mm = mlist; mm; mm &= mm - 1) {  // the wave, one segment each
             const int src = __builtin_ctzll(mm);
-            const int s2 = __shfl(s, src, 64);
+            const int s2 = lane_bcast(s, src);
             const int kb = seg_first(F, s2), na = (s2 + 1 < ns ? seg_first(F, s2 + 1) : n_att) - kb;
-            const int g2 = __shfl(g, src, 64), len2 = __shfl(len, src, 64), nl2 = __shfl(nl, src, 64);
+            const int g2 = lane_bcast(g, src), len2 = lane_bcast(len, src), nl2 = lane_bcast(nl, src);
             int lo = 0, hi = 0;
             double sc = 0.0;
             if (lane < na) {
@@ -1158,6 +1083,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           break;                                       // passes 5 / 6: explain_two's inputs
         }
         if (!e1_now) break;
+        WLAP(32);                                      // (stamps: sure bits, pass choice)
         if (__ballot(fail) != 0ull || (WF_SKIP & 4)) { staged = __ballot(fail) != 0ull; outcome = 2; break; }
         // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
         const int Gu = __popcll(um);
@@ -1208,12 +1134,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
               nopt += __popcll(im);
             }
           }
-    #pragma unroll
-          for (int off = 32; off > 0; off >>= 1) {
-            const double r2 = __shfl_xor(br, off, 64), c2 = __shfl_xor(bcrit, off, 64);
-            const long long k2 = __shfl_xor(bk, off, 64);
+          WLAP(33);                                      // (stamps: option scan)
+          each_stride([&](auto J) {
+            const double r2 = xor_lanes<decltype(J)::value>(br), c2 = xor_lanes<decltype(J)::value>(bcrit);
+            const long long k2 = xor_lanes<decltype(J)::value>(bk);
             if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
-          }
+          });
           if (P.weak == 2) {
             // assign-unknown (:416-418): the row "Unknown" = 1 - maxes is no option iff some
             // locus has 1 - max < k1; a known clade's evaluated mean bounds that locus's max
@@ -1236,6 +1162,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
               break;
             }
           }
+          WLAP(34);                                      // (stamps: reduction)
           if (bk >= 0) {
             wave_sync();
             int nm = 0;                                    // meld_one (:621-631): options within --range
@@ -1267,6 +1194,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
               for (int i = lane; i < nm; i += 64) acc = lca2(K, acc, F.mem()[i]);
               lca = wave_lca(K, acc);
             }
+            WLAP(35);                                      // (stamps: meld_one + LCA)
             const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
             for (int i = lane; i < nm; i += 64) K.meld[mbase + i] = F.mem()[i];
             if (lane < G) K.syn[l0 + lane] = ((um >> lane) & 1ull) ? 'A' : '~';   // set_synteny_one
@@ -1305,7 +1233,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
         // 40), so slot k's entries start where slot k - 1's end
         unsigned long long old = 0;
         if (lane == 0) old = atomicAdd(S.dump_ctr, (1ull << 40) | (unsigned long long)ns);
-        old = __shfl(old, 0, 64);
+        old = lane_bcast((uint64_t)old, 0);
         const int slot = (int)(old >> 40);
         const int64_t base = (int64_t)(old & ((1ull << 40) - 1));
         dumped = base + ns <= S.dump_cap;            // else: the staged kernels (pend 1)
