@@ -57,9 +57,6 @@ constexpr int kXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its 
 #ifndef WF_XCD_MAP
 #define WF_XCD_MAP 1
 #endif
-#ifndef WF_PREFETCH0
-#define WF_PREFETCH0 0
-#endif
 // Diagnostic build only (-DWF_STAMPS): per-phase shader-clock laps of the first form on
 // every 16th contig, plus counters (scripts/wave_stamps.py reads them).  Never in the
 // product build.
@@ -171,6 +168,11 @@ __device__ __forceinline__ int wave_lca(const KArgs& K, int acc) {
 // size k is a runtime loop (the unrolled network of every R and key width would not fit
 // the instruction cache); the strides j inside it are static, so in-lane partners are
 // static register indices and lane partners static shuffles.
+// Ascending bitonic sort of N = 64 * R keys, element R * lane + r in x[r] (lane-major: the
+// strides below R stay inside a lane, element stride j >= R is lane stride j / R, so the
+// most frequent strides -- every merge runs 1, 2, 4, ... -- are register swaps and one-DPP
+// exchanges).  The merge size k is a runtime loop (the unrolled network would not fit the
+// instruction cache); the strides inside it are static.
 template <int R, class T>
 __device__ __forceinline__ void wave_sort(T (&x)[R]) {
   const int lane = lane_id();
@@ -178,48 +180,48 @@ __device__ __forceinline__ void wave_sort(T (&x)[R]) {
 #pragma unroll 1
   for (int k = 2; k <= N; k <<= 1) {
 #pragma unroll
-    for (int jr = R / 2; jr >= 1; jr >>= 1) {        // strides 64 * jr: same lane, element r ^ jr
-      if (64 * jr >= k) continue;
+    for (int jl = 32; jl >= 1; jl >>= 1) {           // element strides jl * R: partner lane ^ jl
+      if (jl * R >= k) continue;
+      // i & (jl * R) and i & k (k > jl * R >= R) depend on the lane alone
+      const bool keep_min = ((lane & jl) == 0) == (((lane * R) & k) == 0);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        if (r & jr) continue;
-        const int i = lane + 64 * r;
-        const bool asc = (i & k) == 0;
-        const T a = x[r], b = x[r | jr];
-        const bool sw = (a > b) == asc;
-        x[r] = sw ? b : a;
-        x[r | jr] = sw ? a : b;
+        const T y = xor_lanes_rt(x[r], jl);
+        const T lo = y < x[r] ? y : x[r], hi = y < x[r] ? x[r] : y;
+        x[r] = keep_min ? lo : hi;
       }
     }
 #pragma unroll
-    for (int j = 32; j >= 1; j >>= 1) {              // strides < 64: partner lane ^ j
+    for (int j = R / 2; j >= 1; j >>= 1) {           // strides below R: element r ^ j, same lane
       if (j >= k) continue;
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const int i = lane + 64 * r;
-        const T y = xor_lanes_rt(x[r], j);
-        const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
-        x[r] = keep_min ? (y < x[r] ? y : x[r]) : (y > x[r] ? y : x[r]);
+        if (r & j) continue;
+        const bool asc = (((lane * R) | r) & k) == 0;
+        const T a = x[r], b = x[r | j];
+        const T lo = a < b ? a : b, hi = a < b ? b : a;
+        x[r] = asc ? lo : hi;
+        x[r | j] = asc ? hi : lo;
       }
     }
   }
 }
 
-// The slice's keys in sorted order (one network of 64 * R 32-bit keys).
+// The slice's keys in sorted order (one network of 64 * R 32-bit keys, lane-major).
 template <int R, class SM>
 __device__ __forceinline__ void sort_slice(SM& F, int n_att) {
   const int lane = lane_id();
   uint32_t y[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int t = lane + 64 * r;
+    const int t = R * lane + r;
     y[r] = t < n_att ? F.key[t] : ~0u;
   }
   wave_sort<R>(y);
   wave_sync();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const int t = lane + 64 * r;
+    const int t = R * lane + r;
     if (t < n_att) F.key[t] = y[r];
   }
   wave_sync();
@@ -302,6 +304,60 @@ __device__ __forceinline__ void sparse_score(SM& F, const double* v, int t, int 
   }
   crit = cnt < Gu ? 0.0 : mn;
   rank = (0.0 + res) / (double)Gu;
+}
+
+// Contig.score of the clade run starting at segment t (t uniform; orgscorer.py:447-461) by
+// the whole wave: lane i holds segment t + i (a run has at most 64 segments, one per locus).
+// crit = the min over the run's unmasked segments (0.0 when fewer than Gu); the rank only
+// when crit >= k1 (an option then has a segment on every unmasked locus, so the u-th
+// unmasked locus is the u-th used lane), summed in sparse_score's numpy order by a uniform
+// walk over the used lanes.  Returns the run's clade.
+template <class SM>
+__device__ __forceinline__ int wave_run_score(SM& F, const double* v, int t, int ns, uint64_t um, int Gu,
+                                              double k1, double& crit, double& rank) {
+  const int lane = lane_id();
+  const int clade = (int)(F.seg[t] >> kCladeShift);
+  const int q = t + lane;
+  bool in = false;
+  int g = 0;
+  double x = 0.0;
+  if (q < ns) {
+    const uint32_t w = F.seg[q];
+    in = (int)(w >> kCladeShift) == clade;
+    g = (int)((w >> kSlotBits) & (kLoc0 - 1));
+    x = v[q];
+  }
+  const uint64_t out = __ballot(!in);                // the run: lanes below the first other clade
+  const int len = out ? __builtin_ctzll(out) : 64;
+  const bool use = lane < len && ((um >> g) & 1ull);
+  const uint64_t used = __ballot(use);
+  const int cnt = __popcll(used);
+  double mn = use ? x : __builtin_inf();
+  mn = wave_butterfly(mn, [](double a, double b) { return b < a ? b : a; });
+  crit = (cnt < Gu || cnt == 0) ? 0.0 : mn;
+  rank = 0.0;
+  if (crit >= k1) {
+    const int m8 = Gu < 8 ? 0 : Gu - (Gu & 7);
+    double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
+    uint64_t rest = used;
+    for (int u = 0; u < m8; ++u, rest &= rest - 1) {  // value u -> accumulator u % 8, in order
+      const double xu = lane_bcast(x, __builtin_ctzll(rest));
+      switch (u & 7) {
+        case 0: r0 += xu; break;
+        case 1: r1 += xu; break;
+        case 2: r2 += xu; break;
+        case 3: r3 += xu; break;
+        case 4: r4 += xu; break;
+        case 5: r5 += xu; break;
+        case 6: r6 += xu; break;
+        default: r7 += xu; break;
+      }
+    }
+    double res = m8 > 0 ? leaf_tree(r0, r1, r2, r3, r4, r5, r6, r7) : 0.0;
+    for (; rest; rest &= rest - 1) res += lane_bcast(x, __builtin_ctzll(rest));   // the rest, in order
+    rank = (0.0 + res) / (double)Gu;
+  }
+  return clade;
 }
 
 // explain_two + LGT filters + meld_two for one level in the slice (decide_two's arithmetic,
@@ -571,19 +627,30 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     // over to the staged kernels (its pend / counts stand); they carry the virtual row
     if (FULL && P.weak == 2) continue;
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
-#if WF_PREFETCH0
-    // the first 64 hits' fields, issued together with the loci loads below (one global
-    // round trip fewer per contig on the serial path)
-    double p_scv = 0.0, p_sc = 0.0;
-    int p_qlo = 0, p_qhi = 0, p_hs = 0, p_clade = 0;
-    uint32_t p_m = 0u;
-    if (h0 + lane < h1) {
-      const int64_t h = h0 + lane;
-      p_scv = K.scov[h]; p_qlo = K.qlo[h]; p_qhi = K.qhi[h]; p_hs = K.hstrand[h];
-      p_clade = K.taxon[h]; p_sc = K.score[h];
-      if (nsys > 0) p_m = K.sysmask[h];
-    }
-#endif
+    // the first round of hits: every field of up to kHB batches of 64, issued before the loci
+    // (their chain -- offsets, loci, leaf counts -- then overlaps these loads)
+    constexpr int kHB = 4;
+    int r_qlo[kHB], r_qhi[kHB], r_hs[kHB], r_cl[kHB];
+    double r_scv[kHB], r_sc[kHB];
+    uint32_t r_m[kHB];
+    auto load_round = [&](int64_t hq) {
+#pragma unroll
+      for (int b = 0; b < kHB; ++b) {
+        const int64_t h = hq + 64 * b + lane;
+        r_qlo[b] = 0; r_qhi[b] = 0; r_hs[b] = 0; r_cl[b] = 0;
+        r_scv[b] = 0.0; r_sc[b] = 0.0; r_m[b] = 0u;
+        if (h < h1) {
+          r_scv[b] = K.scov[h];
+          r_qlo[b] = K.qlo[h];
+          r_qhi[b] = K.qhi[h];
+          r_hs[b] = K.hstrand[h];
+          r_cl[b] = K.taxon[h];
+          r_sc[b] = K.score[h];
+          if (nsys > 0) r_m[b] = K.sysmask[h];
+        }
+      }
+    };
+    load_round(h0);
     const int64_t l0 = K.loc_off[c];
     const int G = (int)(K.loc_off[c + 1] - l0);
     const int Gs = min(G, kLoc0);
@@ -617,13 +684,19 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     const bool long_locus = __ballot(lane < Gs && F.len[lane] > 65535) != 0ull;   // lohi is 16-bit
     bool staged = G > kLoc0 || lut_total > kLut0 || nann > kAnn0 || long_locus;
     wave_sync();
-    if (!staged)                                     // packed leaf tables: one flat batch of loads
+    // packed leaf tables, one flat batch of loads -- only once a segment needs them (a run
+    // that does not cover its locus, or several runs): whole-locus runs have a closed form
+    bool lut_ready = false;
+    auto load_lut = [&]() {
       for (int i = lane; i < lut_total; i += 64) {
         int g = 0;                                   // last locus whose table starts at or before i
         for (int b = 32; b > 0; b >>= 1)
           if (g + b < Gs && F.lbase[g + b] <= i) g += b;
         F.lut[i] = pack_leaf(S.lut[S.lut_off[F.len[g]] + (i - F.lbase[g])]);
       }
+      wave_sync();
+      lut_ready = true;
+    };
 
     WLAP(0);
     // ---- hits -> attachments, in (hit, locus) order (orgscorer.py:359-382) ----
@@ -632,32 +705,8 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     // kHB batches of 64 hits per round: every field of all of them is loaded up front (one
     // global round trip per round instead of one per batch), then the batches are attached
     // in order, each picking its fields from the round's registers by a uniform select
-    constexpr int kHB = 4;
     for (int64_t hq = h0; hq < h1; hq += 64 * kHB) {
-      int r_qlo[kHB], r_qhi[kHB], r_hs[kHB], r_cl[kHB];
-      double r_scv[kHB], r_sc[kHB];
-      uint32_t r_m[kHB];
-#pragma unroll
-      for (int b = 0; b < kHB; ++b) {
-        const int64_t h = hq + 64 * b + lane;
-        r_qlo[b] = 0; r_qhi[b] = 0; r_hs[b] = 0; r_cl[b] = 0;
-        r_scv[b] = 0.0; r_sc[b] = 0.0; r_m[b] = 0u;
-#if WF_PREFETCH0
-        if (h < h1 && hq == h0 && b == 0) {
-          r_scv[b] = p_scv; r_qlo[b] = p_qlo; r_qhi[b] = p_qhi; r_hs[b] = p_hs; r_cl[b] = p_clade;
-          r_sc[b] = p_sc; r_m[b] = p_m;
-        } else
-#endif
-        if (h < h1) {
-          r_scv[b] = K.scov[h];
-          r_qlo[b] = K.qlo[h];
-          r_qhi[b] = K.qhi[h];
-          r_hs[b] = K.hstrand[h];
-          r_cl[b] = K.taxon[h];
-          r_sc[b] = K.score[h];
-          if (nsys > 0) r_m[b] = K.sysmask[h];
-        }
-      }
+      if (hq != h0) load_round(hq);
     for (int bq = 0; bq < kHB && hq + 64 * bq < h1; ++bq) {
       const int64_t hb = hq + 64 * bq;
       const int64_t h = hb + lane;
@@ -803,6 +852,16 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
       bool fail = false;
       const bool prune = P.k1 > 0.0 && !(WF_SKIP & 1);
       const bool prune2 = FULL && prune && P.k2 > 0.0 && (!P.sister_on || P.sister_thr > 0.0);
+      // first form, hand-over to k_dump_sparse after explain_one found no option: only what
+      // its explain_two can read is evaluated (passes 4 and 5 as in the FULL form); the rest
+      // goes over as 0.0.  Exact because (a) the unmasked-locus set it rebuilds is this one
+      // (every locus in it holds an evaluated known-clade mean >= kmin, every other locus has
+      // none), (b) with no option here, zeros create none there, (c) a clade none of whose
+      // segments can reach k2 is no potential clade either way, and potential clades' rows
+      // are evaluated whole, (d) the sister counts read only clades listed under a potential
+      // clade's parent, at scores >= the threshold (bound as in pass 5).  More than 64
+      // potential clades (the parent list's size) evaluate everything (pass 6).
+      const bool prune2d = !FULL && prune && P.k2 > 0.0 && (!P.sister_on || P.sister_thr > 0.0) && P.weak != 2;
       const uint64_t allG = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
       uint64_t um = 0;
       uint8_t* rc = F.rc();                            // per segment: its clade run's size / flag
@@ -835,6 +894,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
         for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[F.key[q] & kSlotMask]);
         return ub;
       };
+      int n_pass0 = -1;                                // pass 0's list, built with the run sizes
       if (prune) {
         // every segment's clade-run size, from the run heads' ballot masks: a lane's run
         // starts at the last head at or before it and ends at the next head after it
@@ -855,16 +915,29 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           carry = hd[i] ? 64 * i + 63 - __clzll(hd[i]) : carry;
         }
         carry = ns;
+        int rsz[kCh];
 #pragma unroll
         for (int i = kCh - 1; i >= 0; --i) {           // run ends, backwards
           const int t = 64 * i + lane;
           const uint64_t m = hd[i] & ~le;
           const int re = m ? 64 * i + __ffsll((unsigned long long)m) - 1 : carry;
           carry = hd[i] ? 64 * i + __ffsll((unsigned long long)hd[i]) - 1 : carry;
+          rsz[i] = re - rs[i];
           if (t < ns) {
             v[t] = -1.0;                               // not evaluated
-            rc[t] = (uint8_t)(re - rs[i]);
+            rc[t] = (uint8_t)rsz[i];
           }
+        }
+        // pass 0's list (segments of clades on every locus), in segment order
+        uint16_t* lst = F.list();
+        n_pass0 = 0;
+#pragma unroll
+        for (int i = 0; i < kCh; ++i) {
+          const int t = 64 * i + lane;
+          const bool in = t < ns && rsz[i] == G;
+          const uint64_t im = __ballot(in);
+          if (in) lst[n_pass0 + __popcll(im & lanes_below())] = (uint16_t)t;
+          n_pass0 += __popcll(im);
         }
         wave_sync();
       }
@@ -893,7 +966,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           }
           wave_sync();
         }
-        if (pass != 3) {                               // compact this pass's segments
+        if (pass == 0 && n_pass0 >= 0) {
+          n = n_pass0;
+          list = F.list();
+        } else if (pass != 3) {                        // compact this pass's segments
           uint16_t* lst = F.list();
           const int gu = __popcll(um);
           n = 0;
@@ -982,6 +1058,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
             else
               fail = true;                               // the staged leaf kernels take it
           }
+          if (!lut_ready && __ballot((one_run && !(lo <= 0 && hi >= len)) || multi) != 0ull) load_lut();
           WLAP(15);
           if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
           WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));
@@ -1068,16 +1145,19 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
             }
           wave_sync();
           npp = 0;                                     // their parents (sister checks, :717-744)
+          int npot = 0;
           for (int t0 = 0; t0 < ns; t0 += 64) {
             const int t = t0 + lane;
             const bool in = t < ns && rc[t] && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
             const uint64_t im = __ballot(in);
             if (in && npp + __popcll(im & lanes_below()) < 64)
-              pp[npp + __popcll(im & lanes_below())] = K.parent[cg_of(F, t).x];
+              pp[npp + __popcll(im & lanes_below())] = FULL ? K.parent[cg_of(F, t).x]
+                                                            : K.sibp[cg_of(F, t).x];   // (k_dump_sparse's key)
             npp = min(npp + __popcll(im), 64);
+            npot += __popcll(im);
           }
           wave_sync();
-          pass = 5;
+          pass = (!FULL && npot > 64) ? 6 : 5;         // (hand-over: the parent list overflowed)
           continue;
         } else {
           break;                                       // passes 5 / 6: explain_two's inputs
@@ -1119,6 +1199,30 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           double* opt_r = reinterpret_cast<double*>(F.mx());
           int* opt_c = F.mem();
           int nopt = 0;
+          if (!FULL && prune) {
+            // the candidates (run heads whose run counts Gu segments on the unmasked loci, in
+            // segment order), each scored by the whole wave: the best option stays uniform
+            for (int t0 = 0; t0 < ns; t0 += 64) {
+              const int t = t0 + lane;
+              bool cand = false;
+              if (t < ns) {
+                const int clade = (int)(F.seg[t] >> kCladeShift);
+                cand = (t == 0 || (int)(F.seg[t - 1] >> kCladeShift) != clade) && (int)rc[t] == Gu &&
+                       !(P.weak == 2 && clade == K.unknown);
+              }
+              for (uint64_t cm = __ballot(cand); cm; cm &= cm - 1) {
+                const int tt = t0 + __builtin_ctzll(cm);
+                double crit, rk;
+                const int clade = wave_run_score(F, v, tt, ns, um, Gu, P.k1, crit, rk);
+                if (crit >= P.k1) {
+                  if (better(rk, clade, br, bk)) { br = rk; bk = clade; bcrit = crit; }
+                  if (nopt < 64 && lane == 0) { opt_r[nopt] = rk; opt_c[nopt] = clade; }
+                  ++nopt;
+                }
+              }
+            }
+            WLAP(33);                                    // (stamps: option scan)
+          } else {
           for (int t0 = 0; t0 < ns; t0 += 64) {
             const int t = t0 + lane;
             double crit = 0.0;
@@ -1140,6 +1244,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
             const long long k2 = xor_lanes<decltype(J)::value>(bk);
             if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
           });
+          }
           if (P.weak == 2) {
             // assign-unknown (:416-418): the row "Unknown" = 1 - maxes is no option iff some
             // locus has 1 - max < k1; a known clade's evaluated mean bounds that locus's max
@@ -1215,7 +1320,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           if (can_dump) {
             dump = true;
             if (pass == 3) break;
-            pass = 6;
+            pass = prune2d ? 4 : 6;
             continue;
           }
           staged = true;
@@ -1240,7 +1345,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
         if (dumped)
           for (int t = lane; t < ns; t += 64) {
             S.dump_cg[base + t] = cg_of(F, t);
-            S.dump_mean[base + t] = v[t];
+            S.dump_mean[base + t] = v[t] < 0.0 ? 0.0 : v[t];   // (not evaluated: see prune2d)
           }
         if (lane == 0) {
           S.dump_first[slot] = (int)(base < INT32_MAX ? base : INT32_MAX);
