@@ -1,7 +1,9 @@
-"""The register-only pairwise sum of a constant run (wf_device.h pw_const_sum: spine + one
-(Q(B_d), Q(B_d + 1)) pair per depth, no leaf table) restated line by line in Python and
-checked against numpy's pairwise tree (the leaf-table walk the oracle follows,
-numpy/_core/src/umath/loops_utils.h.src pairwise_sum) for every buffer length."""
+"""The register-only pairwise sums of one-run segments (wf_device.h): pw_const_sum (a run
+over the whole locus: spine + one (Q(B_d), Q(B_d + 1)) pair per depth, no leaf table) and
+pw_run_sum (any run [lo, hi): the split node, a suffix and a prefix path, whole siblings
+from the same pair chain, run_leaf at the path ends), restated line by line in Python and
+checked against numpy's pairwise tree (numpy/_core/src/umath/loops_utils.h.src
+pairwise_sum) -- for every buffer length, and on explicit arrays for partial runs."""
 import random
 
 import numpy as np
@@ -71,6 +73,167 @@ def pw_const_sum(n, v):
         if d < K:
             R = (q1 if (sel >> d) & 1 else q0) + R
     return R
+
+
+def pairwise_arr(a):
+    n = len(a)
+    if n < 8:
+        r = 0.0
+        for x in a: r += x
+        return r
+    if n <= 128:
+        r = list(a[:8])
+        i = 8
+        m = n - (n % 8)
+        while i < m:
+            for j in range(8): r[j] += a[i + j]
+            i += 8
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        while i < n:
+            res += a[i]; i += 1
+        return res
+    n2 = n // 2; n2 -= n2 % 8
+    return pairwise_arr(a[:n2]) + pairwise_arr(a[n2:])
+
+
+def run_leaf(lo, hi, v, st, ln):
+    # device run_leaf restated: leaf [st, st+ln) over sites v on [lo, hi)
+    m = ln >> 3; be = st + (m << 3)
+    hi = max(hi, lo)
+    res = 0.0
+    def below(base, bound, m):
+        d = bound - base
+        return 0 if d <= 0 else min(m, (d + 7) >> 3)
+    if m > 0:
+        k = [below(st + c, hi, m) - below(st + c, lo, m) for c in range(8)]
+        kmin = min(k)
+        s0 = seqsum(v, kmin); s1 = s0 + v; s2 = s1 + v
+        r = [s0 if kc == kmin else (s1 if kc == kmin + 1 else s2) for kc in k]
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+    for x in range(be, st + ln):
+        res += v if (lo <= x < hi) else 0.0
+    return res
+
+
+def pw_run_sum(n, lo, hi, v):
+    """Line-by-line restatement of wf_device.h pw_run_sum (bitmask bookkeeping, one ascent)."""
+    lo = max(lo, 0); hi = min(hi, n)
+    if hi <= lo: return 0.0
+    a0 = n >> 4; K = 0; m = n; sel = 0
+    while m > 128:
+        a = m >> 4
+        sel |= (1 if a != (a0 >> K) else 0) << K
+        m -= 8 * a; K += 1
+    Db, Dmax, xB, xC, need16 = 0, -1, 0, 0, False
+    if K > 0:
+        Db = max(0, a0.bit_length() - 4); Dmax = max(K - 1, Db)
+        xB = a0 >> Db; xC = (a0 >> (Db + 1)) if Dmax == Db + 1 else 0
+        need16 = Db >= 1 and (a0 >> (Db - 1)) == 16
+    # node = (s, size, kind(1 pair), cls, t)
+    def child(s, size, kind, cls, t, right):
+        if kind == 0:
+            nl = 8 * (size >> 4)
+            return (s + nl, size - nl, 0, 0, t + 1) if right else (s, nl, 1, (sel >> t) & 1, t + 1)
+        x = size >> 3; xl = x >> 1; Bt = a0 >> t
+        return (s + 8 * xl, 8 * (x - xl), 1, (x - xl) - Bt, t + 1) if right else (s, 8 * xl, 1, xl - Bt, t + 1)
+    s, size, kind, cls, t = 0, n, 0, 0, 0
+    mode = 0   # 0 split, 1 whole
+    while True:
+        if lo <= s and hi >= s + size: mode = 1; break
+        if size <= 128: return run_leaf(lo, hi, v, s, size)
+        nl = 8 * (size >> 4) if kind == 0 else 8 * ((size >> 3) >> 1)
+        if hi <= s + nl: s, size, kind, cls, t = child(s, size, kind, cls, t, False)
+        elif lo >= s + nl: s, size, kind, cls, t = child(s, size, kind, cls, t, True)
+        else: break
+    ts = t
+    W_t = t; W_kind = kind; W_cls = cls
+    # walks: per path (term depth, term type: 0 full spine, 1 full pair, 2 leaf), cls, value; ev bits
+    P = []
+    if mode == 0:
+        for suffix in (True, False):
+            s2, sz2, k2, c2, t2 = child(s, size, kind, cls, t, not suffix)
+            ev = evk = evc = 0
+            while True:
+                if (suffix and lo <= s2) or ((not suffix) and hi >= s2 + sz2):
+                    P.append([t2, 0 if k2 == 0 else 1, c2, 0.0, ev, evk, evc]); break
+                if sz2 <= 128:
+                    lv = run_leaf(lo, s2 + sz2, v, s2, sz2) if suffix else run_leaf(s2, hi, v, s2, sz2)
+                    P.append([t2, 2, 0, lv, ev, evk, evc]); break
+                L = child(s2, sz2, k2, c2, t2, False); R = child(s2, sz2, k2, c2, t2, True)
+                if suffix:
+                    if lo < R[0]:
+                        ev |= 1 << (t2 + 1); evk |= (1 if R[2] == 0 else 0) << (t2 + 1); evc |= R[3] << (t2 + 1)
+                        s2, sz2, k2, c2, t2 = L
+                    else: s2, sz2, k2, c2, t2 = R
+                else:
+                    if hi > R[0]:
+                        ev |= 1 << (t2 + 1); evc |= L[3] << (t2 + 1)
+                        s2, sz2, k2, c2, t2 = R
+                    else: s2, sz2, k2, c2, t2 = L
+    mL = m if m < 8 else m >> 3
+    imax = max(xB, mL, 16 if need16 else 0)
+    tt = 0.0; sB = sC = sL = 0.0
+    for i in range(1, imax + 1):
+        tt += v
+        if i == xB: sB = tt
+        if i == xC: sC = tt
+        if i == mL: sL = tt
+    if m < 8: Rv = sL
+    else:
+        Rv = 8.0 * sL
+        for _ in range(m & 7): Rv += v
+    q0 = q1 = 0.0
+    acc = [0.0, 0.0]
+    for d in range(Dmax, -2, -1):
+        u = d + 1
+        if d >= 0:
+            B = a0 >> d
+            if d >= Db:
+                sd = sB if d == Db else sC
+                q0, q1 = 8.0 * sd, 8.0 * (sd + v)
+            else:
+                c0, c1 = q0, q1
+                q0, q1 = (c0 + c1, c1 + c1) if B & 1 else (c0 + c0, c0 + c1)
+                if B == 16: q0 = 8.0 * tt
+        # (Rv is R_u here)
+        if mode == 1 and u == W_t:
+            return Rv if W_kind == 0 else (q1 if W_cls else q0)
+        if mode == 0:
+            for i in (0, 1):
+                tu, ty, tc, lv, ev, evk, evc = P[i]
+                if u == tu:
+                    acc[i] = lv if ty == 2 else (Rv if ty == 0 else (q1 if tc else q0))
+                if u <= tu and (ev >> u) & 1:
+                    sib = Rv if (evk >> u) & 1 else (q1 if (evc >> u) & 1 else q0)
+                    acc[i] = acc[i] + sib if i == 0 else sib + acc[i]
+            if u == ts + 1:
+                return acc[0] + acc[1]
+        if 0 <= d < K:
+            Rv = (q1 if (sel >> d) & 1 else q0) + Rv
+    raise Exception("unreachable")
+
+
+def test_pw_run_sum_matches_pairwise_on_arrays():
+    rng = random.Random(11)
+    lengths = list(range(1, 260)) + rng.sample(range(260, 8192), 250) + [1000, 1031, 2048, 4096,
+                                                                          4103, 8190, 8191]
+    for n in lengths:
+        for trial in range(6):
+            v = rng.uniform(0.05, 1.0)
+            if trial == 0:
+                lo, hi = 0, n
+            elif trial == 1:
+                lo, hi = rng.randrange(n), n
+            elif trial == 2:
+                lo, hi = 0, rng.randrange(1, n + 1)
+            elif trial == 3:
+                lo = rng.randrange(n)
+                hi = min(n, lo + rng.randrange(1, 10))
+            else:
+                lo = rng.randrange(n)
+                hi = rng.randrange(lo + 1, n + 1)
+            a = [v if lo <= i < hi else 0.0 for i in range(n)]
+            assert pw_run_sum(n, lo, hi, v) == pairwise_arr(a), (n, lo, hi, v)
 
 
 def test_pw_const_sum_matches_pairwise_every_length():

@@ -608,11 +608,144 @@ __device__ __forceinline__ double pw_const_sum(int n, double v) {
   return R;
 }
 
+// numpy's pairwise sum of n sites (n < kNpyBuf) holding v on [lo, hi) and 0.0 elsewhere,
+// from registers alone.  A node disjoint from the run sums to 0.0 and x + 0.0 = x, so above
+// the split node (the deepest one holding the whole run) every node passes its child's sum
+// up; below it the run is a suffix of the left child and a prefix of the right one.  A
+// suffix (prefix) node whose boundary falls in its left (right) child adds the whole other
+// child, else it passes the child holding the boundary up; each path ends at a node inside
+// the run or at a leaf (run_leaf).  Whole nodes are the spine or pair nodes of
+// pw_const_sum, so one ascent of its pair chain supplies every whole node's sum at its
+// depth, and the two paths' additions (recorded as bits per depth on the way down) are
+// applied in the same ascent.  tests/test_pw_const.py restates this line by line and checks
+// it against numpy's tree on explicit arrays.
+__device__ __forceinline__ double pw_run_sum(int n, int lo, int hi, double v) {
+  lo = max(lo, 0);
+  hi = min(hi, n);
+  if (hi <= lo) return 0.0;
+  const int a0 = n >> 4;
+  int K = 0, m = n;
+  unsigned sel = 0;
+  while (m > 128) {
+    const int a = m >> 4;
+    sel |= (a != (a0 >> K) ? 1u : 0u) << K;
+    m -= 8 * a;
+    ++K;
+  }
+  int Db = 0, Dmax = -1, xB = 0, xC = 0;
+  bool need16 = false;
+  if (K > 0) {
+    Db = max(0, 28 - __clz(a0));
+    Dmax = max(K - 1, Db);
+    xB = a0 >> Db;
+    xC = Dmax == Db + 1 ? a0 >> (Db + 1) : 0;
+    need16 = Db >= 1 && (a0 >> (Db - 1)) == 16;
+  }
+  // a node: start s, size z, spine (kind 0) or pair node of size 8 * (B_{t-1} + cls), depth t
+  struct Nd { int s, z, kind, cls, t; };
+  auto child = [&](const Nd& x, bool right) -> Nd {
+    if (x.kind == 0) {
+      const int nl = 8 * (x.z >> 4);
+      return right ? Nd{x.s + nl, x.z - nl, 0, 0, x.t + 1} : Nd{x.s, nl, 1, (int)((sel >> x.t) & 1u), x.t + 1};
+    }
+    const int xx = x.z >> 3, xl = xx >> 1, Bt = a0 >> x.t;
+    return right ? Nd{x.s + 8 * xl, 8 * (xx - xl), 1, (xx - xl) - Bt, x.t + 1} : Nd{x.s, 8 * xl, 1, xl - Bt, x.t + 1};
+  };
+  Nd nd{0, n, 0, 0, 0};
+  bool whole = false;
+  for (;;) {                                         // down to the split node
+    if (lo <= nd.s && hi >= nd.s + nd.z) { whole = true; break; }
+    if (nd.z <= 128) return run_leaf(lo, hi, v, nd.s, nd.z);
+    const int nl = nd.kind == 0 ? 8 * (nd.z >> 4) : 8 * ((nd.z >> 3) >> 1);
+    if (hi <= nd.s + nl) nd = child(nd, false);
+    else if (lo >= nd.s + nl) nd = child(nd, true);
+    else break;
+  }
+  // the two paths: terminal depth / type (0 whole spine, 1 whole pair, 2 leaf) / class /
+  // leaf sum, and per depth: a whole sibling to add, is it the spine, its class
+  struct Path { int tu, ty, tc; unsigned ev, evk, evc; double lv; };
+  auto walk = [&](bool suffix) -> Path {
+    Path q{0, 0, 0, 0u, 0u, 0u, 0.0};
+    Nd x = child(nd, !suffix);
+    for (;;) {
+      if (suffix ? lo <= x.s : hi >= x.s + x.z) { q.tu = x.t; q.ty = x.kind; q.tc = x.cls; return q; }
+      if (x.z <= 128) {
+        q.tu = x.t; q.ty = 2;
+        q.lv = suffix ? run_leaf(lo, x.s + x.z, v, x.s, x.z) : run_leaf(x.s, hi, v, x.s, x.z);
+        return q;
+      }
+      const Nd L = child(x, false), R = child(x, true);
+      if (suffix ? lo < R.s : hi > R.s) {
+        const Nd& w = suffix ? R : L;                // the whole sibling
+        q.ev |= 1u << w.t;
+        q.evk |= (w.kind == 0 ? 1u : 0u) << w.t;
+        q.evc |= (unsigned)w.cls << w.t;
+        x = suffix ? L : R;
+      } else {
+        x = suffix ? R : L;
+      }
+    }
+  };
+  Path p0{0, 0, 0, 0u, 0u, 0u, 0.0}, p1{0, 0, 0, 0u, 0u, 0u, 0.0};
+  if (!whole) {
+    p0 = walk(true);
+    p1 = walk(false);
+  }
+  const int mL = m < 8 ? m : m >> 3;
+  const int imax = max(max(xB, mL), need16 ? 16 : 0);
+  double t = 0.0, sB = 0.0, sC = 0.0, sL = 0.0;
+  for (int i = 1; i <= imax; ++i) {
+    t += v;
+    sB = i == xB ? t : sB;
+    sC = i == xC ? t : sC;
+    sL = i == mL ? t : sL;
+  }
+  double R;                                          // the spine below the current depth
+  if (m < 8) {
+    R = sL;
+  } else {
+    R = 8.0 * sL;
+    for (int x = 0; x < (m & 7); ++x) R += v;
+  }
+  double q0 = 0.0, q1 = 0.0, acc0 = 0.0, acc1 = 0.0;
+  for (int d = Dmax; d >= -1; --d) {                 // tree depth u = d + 1, bottom up
+    const int u = d + 1;
+    if (d >= 0) {
+      const int B = a0 >> d;
+      if (d >= Db) {
+        const double sd = d == Db ? sB : sC;
+        q0 = 8.0 * sd;
+        q1 = 8.0 * (sd + v);
+      } else {
+        const double c0 = q0, c1 = q1;
+        q0 = (B & 1) ? c0 + c1 : c0 + c0;
+        q1 = (B & 1) ? c1 + c1 : c0 + c1;
+        if (B == 16) q0 = 8.0 * t;
+      }
+    }
+    if (whole) {
+      if (u == nd.t) return nd.kind == 0 ? R : (nd.cls ? q1 : q0);
+    } else {
+      if (u == p0.tu) acc0 = p0.ty == 2 ? p0.lv : (p0.ty == 0 ? R : (p0.tc ? q1 : q0));
+      if (u <= p0.tu && ((p0.ev >> u) & 1u))
+        acc0 = acc0 + (((p0.evk >> u) & 1u) ? R : (((p0.evc >> u) & 1u) ? q1 : q0));
+      if (u == p1.tu) acc1 = p1.ty == 2 ? p1.lv : (p1.ty == 0 ? R : (p1.tc ? q1 : q0));
+      if (u <= p1.tu && ((p1.ev >> u) & 1u))
+        acc1 = (((p1.evc >> u) & 1u) ? q1 : q0) + acc1;
+      if (u == nd.t + 1) return acc0 + acc1;
+    }
+    if (d >= 0 && d < K) R = (((sel >> d) & 1u) ? q1 : q0) + R;
+  }
+  return 0.0;                                        // (not reached)
+}
+
 template <class LT>
 __device__ __forceinline__ double one_run_mean(LT lt, int nl, int len, int lo, int hi, double v) {
   hi = max(hi, lo);
   if (lo <= 0 && hi >= len && len < kNpyBuf)         // one run over the whole locus
     return (0.0 + pw_const_sum(len, v)) / (double)len;
+  if (len < kNpyBuf)                                 // any other run: no leaf table either
+    return (0.0 + pw_run_sum(len, lo, hi, v)) / (double)len;
   int pst0 = -1, pln0 = 0, pst1 = -1, pln1 = 0;
   int L0 = -1, L1 = -1, L2 = -1, L3 = -1;
 #pragma unroll 4

@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
             else
               fail = true;                               // the staged leaf kernels take it
           }
-          if (!lut_ready && __ballot((one_run && !(lo <= 0 && hi >= len)) || multi) != 0ull) load_lut();
+          if (!lut_ready && __ballot(multi) != 0ull) load_lut();   // (one runs: closed forms)
           WLAP(15);
           if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
           WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));

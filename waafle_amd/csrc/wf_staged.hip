@@ -788,6 +788,7 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
   __shared__ double s_rank[kOneCap];     // rank of the option whose clade run starts here, or -1
   __shared__ int s_mem[kOneCap];
   __shared__ unsigned long long s_max[64];
+  __shared__ unsigned long long s_head[kOneCap / 64];   // clade-run heads, one ballot per 64
   __shared__ int s_cnt;
   const int lane = threadIdx.x;
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
@@ -833,11 +834,19 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
     }
     s_max[lane] = 0;
     __syncthreads();
-    // per-locus max over known clades (:407-411)
-    for (int t = lane; t < ns; t += 64) {
-      const int2 cg = s_cg[t];
-      const double v = s_v[t];
-      if (cg.x != K.unknown && v > 0.0) atomicMax(&s_max[cg.y], dbits(v));
+    // per-locus max over known clades (:407-411); clade-run heads
+    const int nch = (ns + 63) / 64;
+    for (int i = 0; i < nch; ++i) {
+      const int t = 64 * i + lane;
+      bool hd = false;
+      if (t < ns) {
+        const int2 cg = s_cg[t];
+        const double v = s_v[t];
+        if (cg.x != K.unknown && v > 0.0) atomicMax(&s_max[cg.y], dbits(v));
+        hd = t == 0 || s_cg[t - 1].x != cg.x;
+      }
+      const unsigned long long hm = __ballot(hd);
+      if (lane == 0) s_head[i] = hm;
     }
     __syncthreads();
     // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
@@ -857,7 +866,17 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
     for (int t = lane; t < ns; t += 64) {
       double rk = -1.0;
       const int clade = s_cg[t].x;
-      if (t == 0 || s_cg[t - 1].x != clade) {
+      // a run of fewer than Gu segments misses an unmasked locus: crit 0.0 < k1 (k1 > 0),
+      // no option, and its rank is never read
+      bool can = t == 0 || s_cg[t - 1].x != clade;
+      if (can && P.k1 > 0.0) {
+        int i = t >> 6;
+        unsigned long long m = s_head[i] & ((t & 63) == 63 ? 0ull : ~((2ull << (t & 63)) - 1ull));
+        while (m == 0ull && ++i < nch) m = s_head[i];
+        const int re = m ? 64 * i + __builtin_ctzll(m) : ns;
+        can = re - t >= Gu;
+      }
+      if (can) {
         uint64_t m = um;
         int q = t;
         double crit = 0.0;
