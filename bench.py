@@ -69,7 +69,7 @@ def parse_args():
     ap.add_argument("--flags", default="",
                     help="waafle_orgscorer flags for the main workload, e.g. '--weak-loci assign-unknown'")
     ap.add_argument("--option", action="append", default=[],
-                    help="wf_set_option NAME=VALUE (sparse_big, att_limit); repeatable")
+                    help="wf_set_option NAME=VALUE (sparse_big, att_limit, wave_two, dump_cap); repeatable")
     ap.add_argument("--traffic-json", default=None)
     ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r03_k2_pmc.json"),
                     help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
@@ -405,7 +405,8 @@ def main():
         chk(so.wf_set_mode(h, engine.MODES[args.mode]))
     for o in args.option:
         name, val = o.split("=")
-        chk(so.wf_set_option(h, {"sparse_big": L.OPT_SPARSE_BIG, "att_limit": L.OPT_ATT_LIMIT}[name],
+        chk(so.wf_set_option(h, {"sparse_big": L.OPT_SPARSE_BIG, "att_limit": L.OPT_ATT_LIMIT,
+                                       "wave_two": L.OPT_WAVE_TWO, "dump_cap": L.OPT_DUMP_CAP}[name],
                              int(val)))
     tstruct = engine.taxonomy_struct(tax)
     chk(so.wf_set_taxonomy(h, C.byref(tstruct)))

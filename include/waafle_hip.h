@@ -60,8 +60,14 @@ enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
  *   the arena (the only form for > 63 loci); 2: every staged decision in the segment-table
  *   form (a test setting: it exercises that form on every input).
  * WF_OPT_ATT_LIMIT: hit-locus attachments one wf_score call accepts (default and maximum
- *   2^31 - 1; more -> WF_E_TOOBIG, nothing scored). */
-enum wf_option { WF_OPT_SPARSE_BIG = 1, WF_OPT_ATT_LIMIT = 2 };
+ *   2^31 - 1; more -> WF_E_TOOBIG, nothing scored).
+ * WF_OPT_WAVE_TWO (WF_MODE_LEVEL0): 1 (default) the first wave form also decides explain_two
+ *   (up to 64 potential clades, <= 63 loci) and carries the roll-up levels, one pass per level
+ *   over the contigs still open; the rest goes to the segment-table decision (k_dump_sparse);
+ *   0: every explain_two contig goes there and the roll-up levels run in the staged kernels.
+ * WF_OPT_DUMP_CAP: segment-table entries of the wave form's hand-over buffer (default
+ *   max(32 * contigs, 65536)); contigs past it go to the staged kernels (a test setting). */
+enum wf_option { WF_OPT_SPARSE_BIG = 1, WF_OPT_ATT_LIMIT = 2, WF_OPT_WAVE_TWO = 3, WF_OPT_DUMP_CAP = 4 };
 
 typedef struct wf_ctx wf_ctx;
 
@@ -159,6 +165,8 @@ enum wf_phase {
   WF_PHASE_BIG = 4,           /* staged, per level: k_big_sparse + k_decide_big */
   WF_PHASE_HANDOVER = 5,      /* level 0 of the contigs the wave kernels hand over with
                                  their segment tables (k_dump_sparse) */
+  WF_PHASE_ROLLUP = 6,        /* roll-up levels 1, 2, ... in the first wave form (with their
+                                 hand-overs), WF_OPT_WAVE_TWO 1 */
   WF_N_PHASES = 8
 };
 typedef struct wf_timing {

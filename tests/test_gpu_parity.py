@@ -26,7 +26,12 @@ FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n
 
 
 FORMS = {
+    # (default) explain_two and the roll-up levels in the first wave form's hand-over
     "level0": dict(mode="level0"),
+    # round-3 flow: every explain_two contig handed over whole, roll-up in the staged kernels
+    "handover": dict(mode="level0", options={lib.OPT_WAVE_TWO: 0}),
+    # a hand-over buffer of 96 entries: the contigs past it take the staged kernels
+    "dumpcap": dict(mode="level0", options={lib.OPT_DUMP_CAP: 96}),
     "waves": dict(mode="waves"),
     "staged": dict(mode="staged"),
     # every staged decision from the segment table (k_big_sparse, wf_sparse.h)

@@ -70,7 +70,8 @@ def build(force=False, verbose=True, stamps=False, defines=(), out=None):
     extra = (["-DWF_STAMPS"] if stamps else []) + ["-D" + d for d in defines]
     # one compile per source, in parallel, then a link step.  Objects are kept per library
     # (waafle_amd/.objs/<lib>/, git- and gpurun-ignored) and recompiled only when their
-    # source or a header is newer, so an edit to one kernel file rebuilds that file alone.
+    # source or a header is newer, so an edit to one kernel file rebuilds that file alone;
+    # force=True recompiles every object (e.g. after a toolchain change).
     cflags = [f for f in FLAGS if f != "-shared"]
     odir = os.path.join(HERE, ".objs", os.path.basename(lib))
     os.makedirs(odir, exist_ok=True)
@@ -82,7 +83,7 @@ def build(force=False, verbose=True, stamps=False, defines=(), out=None):
     for src in SOURCES:
         obj = os.path.join(odir, os.path.splitext(os.path.basename(src))[0] + ".o")
         objs.append(obj)
-        if (same_flags and os.path.exists(obj) and
+        if (not force and same_flags and os.path.exists(obj) and
                 all(os.path.getmtime(d) <= os.path.getmtime(obj) for d in [src] + headers)):
             continue
         cmd = [hipcc()] + cflags + extra + ["-c", src, "-o", obj]

@@ -488,6 +488,9 @@ __device__ __forceinline__ int below(int base, int bound, int m) {
 // segment means shared by the staged kernels and the fused level-0 kernel (wf_fast.hip)
 // --------------------------------------------------------------------------
 constexpr int kThreadLeaves = 32;
+// explain_two from the wave form's compact hand-over (wf_fast.hip, sp_two in wf_sparse.h)
+constexpr int kE2Seg = 320;        // segments of one compact table (LDS of k_dump_sparse)
+constexpr int kE2MaxG = 63;        // loci (locus masks keep bit 63 for the root flag)
 constexpr int kPruneMax = 64;      // attachments scanned for whole-locus domination
 
 __device__ __forceinline__ bool attaches(const DevParams& P, int qlo, int qhi, int hs, int l1,

@@ -597,8 +597,12 @@ template <int CAP, bool FULL>
 // rollup (FULL): carry a contig through its roll-up levels in the slice; else hand it to
 // the staged kernels at its first raise (they run every contig of a level together,
 // which measured 3x faster per contig-level on cfg4 than one wave per contig here).
+// S_arg must stay the first parameter: kernarg_fresh reads the argument block at kernarg
+// offset 0.  start_level > 0 (first form only): roll-up level start_level of the contigs in
+// `list` (the wave levels, S.anc set).
 __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
-                                             const int32_t* list, int n_list, const int64_t* n_dev, int rollup) {
+                                             const int32_t* list, int n_list, const int64_t* n_dev, int rollup,
+                                             int start_level) {
   if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WaveSmem<CAP, FULL>& F = *reinterpret_cast<WaveSmem<CAP, FULL>*>(smem);
@@ -623,6 +627,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     const KArgs& K = S.k;
     const DevParams& P = K.p;
     const int nsys = K.n_sys;
+    const bool ann_on = start_level == 0 && nsys > 0;  // annotations: level 0 only (never raised, :383-392)
     // --weak-loci assign-unknown: the second form leaves every contig the first one handed
     // over to the staged kernels (its pend / counts stand); they carry the virtual row
     if (FULL && P.weak == 2) continue;
@@ -646,7 +651,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           r_hs[b] = K.hstrand[h];
           r_cl[b] = K.taxon[h];
           r_sc[b] = K.score[h];
-          if (nsys > 0) r_m[b] = K.sysmask[h];
+          if (ann_on) r_m[b] = K.sysmask[h];
         }
       }
     };
@@ -758,7 +763,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
       int total;
       const int o = wave_excl_scan(n, &total);
       if (!staged && n > 0 && n_att + o + n <= CAP) {
-        for (int j = 0; j < P.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
+        if (start_level > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
+        else
+          for (int j = 0; j < P.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
         const bool ann = m != 0 && sc >= P.annot_ref;
         int slot = n_att + o;
         for (uint64_t bits = am; bits; bits &= bits - 1, ++slot) {
@@ -789,7 +796,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     WSTAT(16, 1);
     WSTAT(17, n_att);
     WSTAT(23, h1 - h0);
-    if (!staged && G > 0 && nsys > 0) {
+    if (!staged && G > 0 && ann_on) {
       // annotation pass 2: the last hit (largest index) at the best score per (locus, system)
       for (int t = lane; t < n_att; t += 64) {
         const uint32_t m = (uint32_t)F.sm()[t];
@@ -805,12 +812,13 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     }
     WLAP(2);
     // ---- levels: sort, segments, means, explain_one [, explain_two, roll-up] ----
-    int64_t pair_evals = 0;
+    int64_t pair_evals = (start_level > 0 && lane == 0) ? K.pair_evals[c] : 0;
+    pair_evals = lane_bcast((uint64_t)pair_evals, 0);
     bool seed = false;                                 // raised at level 0: staged level 1 seed
     bool dumped = false;                               // segment table handed to k_dump_sparse
-    for (int level = 0; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
+    for (int level = start_level; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
       const int iteration = level + 1;
-      if (level > 0) {                               // roll up (:431-445): re-key to the parent clade
+      if (level > start_level) {                     // roll up (:431-445): re-key to the parent clade
         for (int t = lane; t < n_att; t += 64) {
           const uint32_t k0 = F.key[t];
           const int parent = K.parent[(int)(k0 >> kCladeShift)];
@@ -945,6 +953,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
       const double bound_s = P.sister_thr * (1.0 - 1e-12);
       uint64_t open = 0;
       int outcome = 0;                                 // 2: decided (or stopped) by explain_one
+      bool compact_ok = false;                         // passes 4, 5 ran: explain_two's inputs only
       // first form: the level's decision goes to k_dump_sparse with the whole segment table
       // (pass 6 evaluates the rest) instead of the staged kernels
       bool dump = false;
@@ -1150,14 +1159,17 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
             const int t = t0 + lane;
             const bool in = t < ns && rc[t] && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
             const uint64_t im = __ballot(in);
+            // the sisters of X are the clades listed under parent(X) (get_sisters, utils.py:428-434):
+            // pass 5 evaluates clades whose listed parent is one of these.  (Not sibp(X): an
+            // unlisted X has sibp -1 but parent r__Root, whose listed children are its sisters.)
             if (in && npp + __popcll(im & lanes_below()) < 64)
-              pp[npp + __popcll(im & lanes_below())] = FULL ? K.parent[cg_of(F, t).x]
-                                                            : K.sibp[cg_of(F, t).x];   // (k_dump_sparse's key)
+              pp[npp + __popcll(im & lanes_below())] = K.parent[cg_of(F, t).x];
             npp = min(npp + __popcll(im), 64);
             npot += __popcll(im);
           }
           wave_sync();
           pass = (!FULL && npot > 64) ? 6 : 5;         // (hand-over: the parent list overflowed)
+          compact_ok = pass == 5;
           continue;
         } else {
           break;                                       // passes 5 / 6: explain_two's inputs
@@ -1334,24 +1346,62 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
       wave_sync();
       WLAP(8);
       if (dump && !staged) {
+        // The compact form (WF_OPT_WAVE_TWO; passes 4 and 5 ran, <= 64 potential clades):
+        // only what explain_two reads -- the potential clades' rows (rc) and the segments at
+        // or above the sister threshold -- plus the unmasked loci and whether r__Root is
+        // present; k_dump_sparse decides from it (sp_two).  Else the whole table (sp_level).
+        bool compact = !FULL && compact_ok && S.wave_two && G <= kE2MaxG && P.weak != 2;
+        int n_out = ns;
+        bool rootp = false;
+        auto want = [&](int t) { return rc[t] != 0 || (P.sister_on && v[t] >= P.sister_thr); };
+        if (compact) {
+          int n2 = 0;
+          for (int t0 = 0; t0 < ns; t0 += 64) {
+            const int t = t0 + lane;
+            bool w = false;
+            if (t < ns) {
+              w = want(t);
+              rootp = rootp || cg_of(F, t).x == K.root;
+            }
+            n2 += __popcll(__ballot(w));
+          }
+          rootp = __ballot(rootp) != 0ull;
+          compact = n2 <= kE2Seg;
+          if (compact) n_out = n2;
+        }
         // the table: one 64-bit atomic gives the slot (high bits) and its first entry (low
         // 40), so slot k's entries start where slot k - 1's end
         unsigned long long old = 0;
-        if (lane == 0) old = atomicAdd(S.dump_ctr, (1ull << 40) | (unsigned long long)ns);
+        if (lane == 0) old = atomicAdd(S.dump_ctr, (1ull << 40) | (unsigned long long)n_out);
         old = lane_bcast((uint64_t)old, 0);
         const int slot = (int)(old >> 40);
         const int64_t base = (int64_t)(old & ((1ull << 40) - 1));
-        dumped = base + ns <= S.dump_cap;            // else: the staged kernels (pend 1)
-        if (dumped)
+        dumped = base + n_out <= S.dump_cap;         // else: the staged kernels (pend 1)
+        if (dumped && compact) {
+          int o = 0;
+          for (int t0 = 0; t0 < ns; t0 += 64) {
+            const int t = t0 + lane;
+            const bool w = t < ns && want(t);
+            const uint64_t wm = __ballot(w);
+            if (w) {
+              const int q = o + __popcll(wm & lanes_below());
+              S.dump_cg[base + q] = cg_of(F, t);
+              S.dump_mean[base + q] = v[t];          // (evaluated: potential rows are whole)
+            }
+            o += __popcll(wm);
+          }
+        } else if (dumped) {
           for (int t = lane; t < ns; t += 64) {
             S.dump_cg[base + t] = cg_of(F, t);
             S.dump_mean[base + t] = v[t] < 0.0 ? 0.0 : v[t];   // (not evaluated: see prune2d)
           }
+        }
         if (lane == 0) {
           S.dump_first[slot] = (int)(base < INT32_MAX ? base : INT32_MAX);
-          S.dump_first[slot + 1] = (int)(base + ns < INT32_MAX ? base + ns : INT32_MAX);
-          S.dump_list[2 * slot] = slot;
+          S.dump_first[slot + 1] = (int)(base + n_out < INT32_MAX ? base + n_out : INT32_MAX);
+          S.dump_list[2 * slot] = compact ? 1 : 0;   // the table's form
           S.dump_list[2 * slot + 1] = dumped ? c : -1;
+          if (compact) S.dump_um[slot] = um | (rootp ? (1ull << 63) : 0ull);
         }
         staged = true;                                 // (its attachment counts stand)
         WSTAT(21, 1);
@@ -1391,7 +1441,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     if (lane == 0) {
       ccnt[c] = staged ? n_att : 0;
       cleaves[c] = staged ? nl_sum : 0;
-      pend[c] = staged ? (dumped ? 3 : (seed ? 2 : 1)) : 0;
+      const int pd = staged ? (dumped ? 3 : (seed ? 2 : 1)) : 0;
+      pend[c] = pd;
+      if (pd == 1 && S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);   // (wave levels: staged from level 0)
     }
     WSTAT(22, staged ? 1 : 0);
     wave_sync();                                       // the slice is reused by the next contig
@@ -1420,10 +1472,10 @@ int blocks_per_cu() {
 // n_list: the list length, or (n_dev set) an upper bound for the grid
 template <int CAP, bool FULL>
 hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
-                      int n_list, const int64_t* n_dev, int cus, int rollup, hipStream_t s) {
+                      int n_list, const int64_t* n_dev, int cus, int rollup, hipStream_t s, int start_level = 0) {
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_list, (int64_t)cus * blocks_per_cu<CAP, FULL>()));
   hipLaunchKernelGGL((k_wave<CAP, FULL>), dim3(grid), dim3(64), sizeof(WaveSmem<CAP, FULL>), s, sa, ccnt, cleaves, pend,
-                     list, n_list, n_dev, rollup);
+                     list, n_list, n_dev, rollup, start_level);
   return hipGetLastError();
 }
 
@@ -1448,6 +1500,16 @@ hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t
 #endif
   return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s)
                          : launch_cap<512, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s);
+}
+
+hipError_t launch_level(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
+                        const int64_t* n_dev, int level, int max_hits, int cus, hipStream_t s) {
+  const int N = sa.k.n_contigs;
+#ifndef WF_NO_CAP224
+  if (max_hits <= 224) return launch_cap<224, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
+#endif
+  return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level)
+                         : launch_cap<512, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
 }
 
 hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,

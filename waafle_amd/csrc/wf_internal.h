@@ -98,10 +98,24 @@ struct SArgs {
   int2* dump_cg;                 // [dump_cap] (clade, locus), in (clade, locus) order per contig
   double* dump_mean;             // [dump_cap] segment means
   int32_t* dump_first;           // [n_contigs + 1] first entry of each slot
-  int32_t* dump_list;            // [2 n_contigs] (slot, contig); contig -1: did not fit
+  int32_t* dump_list;            // [2 n_contigs] (form, contig); contig -1: did not fit; form 1:
+                                 // compact (explain_two's inputs only, sp_two), 0: the whole table
+  uint64_t* dump_um;             // [n_contigs] compact slots: unmasked loci | r__Root present << 63
   unsigned long long* dump_ctr;  // slots << 40 | entries
   int32_t* seed_pend;            // k_dump_sparse: pend of the contigs it decides (0), raises
                                  // (2: staged level-1 seed) or declines (1: staged level 0)
+  // Roll-up levels by the first wave form (wave levels): level L re-attaches its contigs'
+  // hits with clade anc[taxon] = parent^(jump + L)(taxon), decides explain_one and
+  // explain_two in the wave, and appends the contigs it raises to roll_next (count in
+  // *roll_next_n); contigs that leave the wave forms count in *fail_ctr (pend 1)
+  int32_t* anc;                  // [n_tax] ancestor of each name at this level (null: level 0)
+  int n_tax;
+  int wave_two;                  // explain_two in the first form (else every such contig
+                                 // goes to k_dump_sparse with its segment table)
+  int32_t* roll_next;            // contigs raised at this level (null: no wave levels)
+  unsigned long long* roll_next_n;
+  unsigned long long* fail_ctr;
+  unsigned long long* dump_ctr_next;   // k_dump_sparse zeroes the next level's table counter
 };
 
 // waafle_genecaller (wf_genecall.hip): one contig group per wave
@@ -166,12 +180,16 @@ hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t
                        hipStream_t s);
 hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
                        const int64_t* n_dev, int max_hits, int cus, bool rollup, hipStream_t s);
+// roll-up level `level` (>= 1) of the first wave form over `list` (length *n_dev)
+hipError_t launch_level(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
+                        const int64_t* n_dev, int level, int max_hits, int cus, hipStream_t s);
 StagedState* staged_create(int device);
 void staged_destroy(StagedState* st);
 void staged_set_lds(StagedState* st, int64_t bytes);
 // context options (include/waafle_hip.h wf_option): the segment-table decision for contigs
-// that outgrow the LDS arena, and the attachments one call accepts (more: WF_E_TOOBIG)
-void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit);
+// that outgrow the LDS arena, the attachments one call accepts (more: WF_E_TOOBIG), explain_two
+// and the roll-up levels in the first wave form, the hand-over buffer's size (0: default)
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap);
 // per-phase timing (wf_phase): HIP events around each phase of each level, read back at the
 // end of every staged_score call into the accumulators (reset by staged_timing(st, on))
 void staged_timing(StagedState* st, bool on);

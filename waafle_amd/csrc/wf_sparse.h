@@ -855,6 +855,348 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   return true;
 }
 
+// ---- explain_two from the wave form's compact hand-over ---------------------------------
+// sp_level's explain_two, LGT checks and meld_two (orgscorer.py:599-744) on the compact table
+// the first wave form writes when passes 4 and 5 ran (<= 64 potential clades, <= 63 loci,
+// wf_fast.hip): the potential clades' rows whole, plus every other segment at or above the
+// sister threshold; the unmasked loci (the first form's weak-locus mask, :420-427) and
+// whether r__Root is present come with it.  A segment left out either belongs to no
+// potential clade and scores below the threshold (it enters no test), or was never
+// evaluated because its mean cannot reach one (the prune2d comment in k_wave).
+//
+// The table is staged in LDS once; potential clade i (clade order) gets a row of summaries
+// (loci present, ">= k2 on unmasked loci", ">= the sister threshold"), and its gene scores
+// are read from its run (locus g is segment t + popcount(present loci below g), 0.0 without
+// a segment).  The sister checks (:717-744) use, per potential clade X, the loci where at
+// least one / two clades listed under parent(X), X excluded, score at or above the
+// threshold: the pair's other clade is removed with one bit operation (sp_sisters'
+// saturating counts, restated for one parent per clade).
+struct E2Shared {
+  int2 cg[kE2Seg];                           // (clade, locus), clade then locus order
+  double v[kE2Seg];                          // gene score
+  int t[64], cl[64], par[64], sibp[64];      // potential clade i: run start, clade, parent,
+                                             // listed parent
+  unsigned long long pres[64], pm[64], hm[64], s1[64], s2[64];
+  int len[64];                               // locus lengths (ambiguous fraction)
+};
+
+// S[row][g] (0.0 without a segment)
+__device__ __forceinline__ double e2_at(const E2Shared& sh, int t, uint64_t pres, int g) {
+  return ((pres >> g) & 1ull) ? sh.v[t + __popcll(pres & ((1ull << g) - 1ull))] : 0.0;
+}
+
+// Contig.score(c1, c2) rank (orgscorer.py:447-461): numpy-order mean over the unmasked loci
+// of the per-locus max (sp_pair_rank's arithmetic)
+__device__ __forceinline__ double e2_rank(const E2Shared& sh, int a, int b, uint64_t um, int Gu) {
+  const int ta = sh.t[a], tb = sh.t[b];
+  const uint64_t pa = sh.pres[a], pb = sh.pres[b];
+  uint64_t m = um;
+  auto next = [&]() -> double {
+    const int g = __builtin_ctzll(m);
+    m &= m - 1;
+    const double x = e2_at(sh, ta, pa, g), y = e2_at(sh, tb, pb, g);
+    return x < y ? y : x;
+  };
+  return (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
+}
+
+struct E2Eval {
+  int ok, swapped, dir;
+  uint64_t mm, mA, mB;                       // synteny '*', 'A', 'B' after the swap
+};
+
+// set_synteny_two + apply_lgt_checks (orgscorer.py:511-545, 678-744) for potential clades
+// a < b: sp_eval_two's arithmetic
+__device__ __forceinline__ E2Eval e2_eval(const KArgs& K, const E2Shared& sh, int a, int b, uint64_t um) {
+  const DevParams& P = K.p;
+  const bool unk = sh.cl[a] == K.unknown || sh.cl[b] == K.unknown;
+  uint64_t mm = 0, ma = 0, mb = 0;
+  {
+    const int ta = sh.t[a], tb = sh.t[b];
+    const uint64_t pa = sh.pres[a], pb = sh.pres[b];
+    for (uint64_t r = um; r; r &= r - 1) {
+      const int g = __builtin_ctzll(r);
+      const uint64_t bit = 1ull << g;
+      const double s1 = e2_at(sh, ta, pa, g), s2 = e2_at(sh, tb, pb, g);
+      const double mn = s2 < s1 ? s2 : s1;
+      if (mn >= P.k_amb && !unk) mm |= bit;
+      else if (s1 >= P.k2) ma |= bit;
+      else if (s2 >= P.k2) mb |= bit;
+    }
+  }
+  E2Eval e;
+  const uint64_t ab = ma | mb;                       // "^[^A]*B" -> swap (:537-540)
+  e.swapped = (ab && ((mb >> __builtin_ctzll(ab)) & 1ull)) ? 1 : 0;
+  e.mm = mm;
+  e.mA = e.swapped ? mb : ma;
+  e.mB = e.swapped ? ma : mb;
+  int64_t tot = 0, amb = 0;
+  int state = 0;
+  bool dir_ok = true;
+  for (uint64_t r = um; r; r &= r - 1) {             // "^A+B+A+$" without '~' (:542)
+    const int g = __builtin_ctzll(r);
+    const uint64_t bit = 1ull << g;
+    const char c = (mm & bit) ? '*' : (e.mA & bit) ? 'A' : (e.mB & bit) ? 'B' : '!';
+    if (c != '!') {
+      tot += sh.len[g];
+      if (c == '*') amb += sh.len[g];
+    }
+    if (state == 0) { if (c == 'A') state = 1; else dir_ok = false; }
+    else if (state == 1) { if (c == 'B') state = 2; else if (c != 'A') dir_ok = false; }
+    else if (state == 2) { if (c == 'A') state = 3; else if (c != 'B') dir_ok = false; }
+    else { if (c != 'A') dir_ok = false; }
+  }
+  e.dir = (dir_ok && state == 3) ? 1 : 0;
+  e.ok = 1;
+  if ((double)amb / (double)tot > P.amb_frac) e.ok = 0;                       // :693-702
+  if (P.clade_genes >= 0 && min(__popcll(e.mA), __popcll(e.mB)) < P.clade_genes) e.ok = 0;   // :704-708
+  const int x = e.swapped ? b : a, y = e.swapped ? a : b;   // clade1 / clade2 after the swap
+  if (P.clade_leaves >= 0) {                         // :710-715 (recip = clade2 when B>A)
+    const int64_t ly = K.leaves[sh.cl[y]];
+    const int64_t lc = e.dir ? ly : min(K.leaves[sh.cl[x]], ly);
+    if (lc < P.clade_leaves) e.ok = 0;
+  }
+  if (P.sister_on && e.ok) {                         // :717-744
+    // sisters["B"] = get_sisters(clade1) - {clade2}; sisters["A"] = get_sisters(clade2) - {clade1}
+    const int px = sh.par[x], py = sh.par[y];
+    const uint64_t fb = sh.sibp[y] == px ? (sh.s2[x] | (sh.s1[x] & ~sh.hm[y])) : sh.s1[x];
+    uint64_t fa = 0;
+    if (!e.dir) fa = sh.sibp[x] == py ? (sh.s2[y] | (sh.s1[y] & ~sh.hm[x])) : sh.s1[y];
+    if ((fb & e.mB) || (fa & e.mA)) e.ok = 0;
+  }
+  return e;
+}
+
+__device__ __forceinline__ int e2_wave_lca(const KArgs& K, int acc) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc = lca2(K, acc, __shfl_xor(acc, off, 64));
+  return acc;
+}
+
+// One compact slot (table [so, se), contig c, the roll-up level): writes the contig's
+// result or its roll-up bookkeeping (as sp_level).  False: the table breaks the compact
+// form's limits (the dense decision takes the contig; never expected).
+__device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int so, int se, uint64_t hdr, int level) {
+  const KArgs& K = S.k;
+  const DevParams& P = K.p;
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int64_t h0 = K.hit_off[c];
+  const int64_t l0 = K.loc_off[c];
+  const int G = (int)(K.loc_off[c + 1] - l0);
+  const int ns = se - so;
+  if (G > kE2MaxG || ns > kE2Seg) return false;
+  const uint64_t um = hdr & ~(1ull << 63);
+  const bool root = (hdr >> 63) != 0ull;
+  const int Gu = __popcll(um);
+  const uint64_t allG = (1ull << G) - 1ull;
+  const int iteration = level + 1;
+  int64_t pair_evals = level == 0 ? 0 : K.pair_evals[c];
+  for (int q = lane; q < ns; q += 64) {
+    sh.cg[q] = S.dump_cg[so + q];
+    sh.v[q] = S.dump_mean[so + q];
+  }
+  if (lane < G) {
+    const int ls = K.lstart[l0 + lane], le = K.lend[l0 + lane];
+    sh.len[lane] = max(ls, le) - min(ls, le) + 1;
+  }
+  __syncthreads();
+  // potential clades (a locus >= k2, missing loci scoring 0.0; :603-605)
+  int Pp = 0;
+  for (int t0 = 0; t0 < ns; t0 += 64) {
+    const int t = t0 + lane;
+    bool pot = false;
+    uint64_t pres = 0, mk2 = 0, hm = 0;
+    int cl = -1;
+    if (t < ns) {
+      cl = sh.cg[t].x;
+      if (t == 0 || sh.cg[t - 1].x != cl) {
+        for (int q = t; q < ns && sh.cg[q].x == cl; ++q) {
+          const uint64_t bit = 1ull << sh.cg[q].y;
+          const double x = sh.v[q];
+          pres |= bit;
+          if (x >= P.k2) mk2 |= bit;
+          if (x >= P.sister_thr) hm |= bit;
+        }
+        const uint64_t miss = allG & ~pres;
+        if (0.0 >= P.k2) mk2 |= miss;
+        if (0.0 >= P.sister_thr) hm |= miss;
+        pot = mk2 != 0ull;
+      }
+    }
+    const uint64_t pb = __ballot(pot);
+    const int i = Pp + __popcll(pb & below);
+    if (pot && i < 64) {
+      sh.t[i] = t; sh.cl[i] = cl; sh.par[i] = K.parent[cl]; sh.sibp[i] = K.sibp[cl];
+      sh.pres[i] = pres; sh.pm[i] = mk2 & um; sh.hm[i] = hm; sh.s1[i] = 0; sh.s2[i] = 0;
+    }
+    Pp += __popcll(pb);
+  }
+  if (Pp > 64) return false;
+  __syncthreads();
+  pair_evals += (int64_t)Pp * (Pp - 1) / 2;
+  if (P.sister_on) {
+    // per potential clade, the present clades listed under its parent (itself excluded) at
+    // or above the threshold (a segment left out of the table scores below it)
+    const int my_par = lane < Pp ? sh.par[lane] : -2, my_cl = lane < Pp ? sh.cl[lane] : -1;
+    uint64_t s1 = 0, s2 = 0;
+    for (int t0 = 0; t0 < ns; t0 += 64) {
+      const int t = t0 + lane;
+      int sp = -1, cl = -1;
+      uint64_t h = 0;
+      if (t < ns) {
+        cl = sh.cg[t].x;
+        if (t == 0 || sh.cg[t - 1].x != cl) {
+          uint64_t pres = 0;
+          for (int q = t; q < ns && sh.cg[q].x == cl; ++q) {
+            pres |= 1ull << sh.cg[q].y;
+            if (sh.v[q] >= P.sister_thr) h |= 1ull << sh.cg[q].y;
+          }
+          if (0.0 >= P.sister_thr) h |= allG & ~pres;
+          if (h) sp = K.sibp[cl];
+        }
+      }
+      bool match = false;
+      for (int i = 0; i < Pp; ++i) match = match || (sp >= 0 && sp == sh.par[i]);
+      for (uint64_t mb = __ballot(match); mb; mb &= mb - 1) {
+        const int src = __builtin_ctzll(mb);
+        const int sp_r = __shfl(sp, src, 64), cl_r = __shfl(cl, src, 64);
+        const uint64_t h_r = (uint64_t)__shfl((long long)h, src, 64);
+        if (my_par == sp_r && my_cl != cl_r) {
+          s2 |= s1 & h_r;
+          s1 |= h_r;
+        }
+      }
+    }
+    if (lane < Pp) { sh.s1[lane] = s1; sh.s2[lane] = s2; }
+    __syncthreads();
+  }
+  // pass 1: the best candidate pair by (rank, pair index); crit >= k2 <=> (m_i | m_j) == um
+  const uint64_t my_pm = lane < Pp ? sh.pm[lane] : 0ull;
+  double pr = -__builtin_inf();
+  long long pk = -1;
+  for (int i = 0; i + 1 < Pp; ++i) {
+    const bool cand = lane > i && lane < Pp && (sh.pm[i] | my_pm) == um;
+    if (cand) {
+      const double r = e2_rank(sh, i, lane, um, Gu);
+      const long long key = (long long)i * Pp + lane;
+      if (better(r, key, pr, pk)) { pr = r; pk = key; }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double r2 = __shfl_xor(pr, off, 64);
+    const long long k2 = __shfl_xor(pk, off, 64);
+    if (better(r2, k2, pr, pk)) { pr = r2; pk = k2; }
+  }
+  if (pk >= 0) {
+    const int bi = (int)(pk / Pp), bj = (int)(pk % Pp);
+    const E2Eval be = e2_eval(K, sh, bi, bj, um);
+    // pass 2: options within --range of the best get the LGT checks (:636-639)
+    int n_in = 0;
+    bool all_ok = true, all_same = true;
+    uint64_t b1 = 0, b2 = 0;
+    for (int i = 0; i + 1 < Pp; ++i) {
+      const bool cand = lane > i && lane < Pp && (sh.pm[i] | my_pm) == um;
+      if (cand && (pr - e2_rank(sh, i, lane, um, Gu)) <= P.range) {
+        const E2Eval e = e2_eval(K, sh, i, lane, um);
+        ++n_in;
+        all_ok = all_ok && e.ok;
+        all_same = all_same && e.mm == be.mm && e.mA == be.mA && e.mB == be.mB;
+        b1 |= 1ull << (e.swapped ? lane : i);
+        b2 |= 1ull << (e.swapped ? i : lane);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      n_in += __shfl_xor(n_in, off, 64);
+      b1 |= (uint64_t)__shfl_xor((long long)b1, off, 64);
+      b2 |= (uint64_t)__shfl_xor((long long)b2, off, 64);
+    }
+    all_ok = __ballot(!all_ok) == 0ull;
+    all_same = __ballot(!all_same) == 0ull;
+    // meld_two (:640-669): 0 none, 1 best as is, 2 meld, 3 unchecked best, 4 upstream crash
+    int kind;
+    if (n_in == 0) kind = (P.dis2 == 0) ? 3 : (P.dis2 == 1 ? 0 : 4);   // --range < 0
+    else if (n_in == 1 || P.dis2 == 0) kind = 1;
+    else if (P.dis2 == 1) kind = 0;
+    else kind = (all_ok && all_same) ? 2 : 0;
+    if (kind == 4) {
+      if (lane == 0) K.status[c] = WF_E_BADINPUT;
+      return true;
+    }
+    bool have_ok = false;
+    int lca1 = -1, lca2v = -1;
+    const bool in1 = (b1 >> lane) & 1ull, in2 = (b2 >> lane) & 1ull;
+    const int my_cl = lane < Pp ? sh.cl[lane] : -1;
+    if (kind == 2) {
+      lca1 = e2_wave_lca(K, in1 ? my_cl : -1);
+      lca2v = e2_wave_lca(K, in2 ? my_cl : -1);
+      bool keep = true;
+      if (!P.allow_lca) {
+        const int nl = lca2(K, lca1, lca2v);
+        keep = !(nl == lca1 || nl == lca2v);
+      }
+      have_ok = keep;                                // melded options are all OK
+    } else if (kind == 1) {
+      have_ok = be.ok != 0;
+    } else if (kind == 3) {
+      have_ok = true;
+    }
+    if (have_ok) {
+      const int64_t mbase = 2 * h0 + 2 * (int64_t)c;
+      const int m1 = __popcll(b1), m2 = __popcll(b2);
+      if (kind == 2) {                               // melded clades, in potential order
+        if (in1) K.meld[mbase + __popcll(b1 & below)] = my_cl;
+        if (in2) K.meld[mbase + m1 + __popcll(b2 & below)] = my_cl;
+      }
+      if (lane < G) {
+        const uint64_t bit = 1ull << lane;
+        K.syn[l0 + lane] = !(um & bit) ? '~' : (be.mm & bit) ? '*' : (be.mA & bit) ? 'A' : (be.mB & bit) ? 'B' : '!';
+      }
+      if (lane == 0) {
+        double bcrit = 0.0;                          // sp_pair_crit: min over the unmasked loci
+        bool first = true;
+        const int ta = sh.t[bi], tb = sh.t[bj];
+        const uint64_t pa = sh.pres[bi], pb = sh.pres[bj];
+        for (uint64_t r = um; r; r &= r - 1) {
+          const int g = __builtin_ctzll(r);
+          const double x = e2_at(sh, ta, pa, g), y = e2_at(sh, tb, pb, g);
+          const double m = x < y ? y : x;
+          bcrit = (first || m < bcrit) ? m : bcrit;
+          first = false;
+        }
+        K.call[c] = WF_CALL_LGT;
+        K.crit[c] = bcrit;
+        K.rank[c] = pr;
+        K.dir[c] = (int8_t)be.dir;
+        K.c1[c] = kind == 2 ? lca1 : sh.cl[be.swapped ? bj : bi];
+        K.c2[c] = kind == 2 ? lca2v : sh.cl[be.swapped ? bi : bj];
+        K.nm1[c] = kind == 2 ? m1 : 0;
+        K.nm2[c] = kind == 2 ? m2 : 0;
+        K.iters[c] = (int16_t)iteration;
+        K.pair_evals[c] = pair_evals;
+      }
+      return true;
+    }
+  }
+  // no explanation at this level (:570-583): raise, or stop at r__Root (the table is never
+  // empty: explain_one ran on this contig's segments)
+  if (!root && iteration + 1 <= kMaxIter) {
+    if (lane == 0) {
+      S.seed_pend[c] = 2;
+      K.pair_evals[c] = pair_evals;
+    }
+    return true;
+  }
+  if (lane == 0) {                                   // unclassified after evaluation
+    K.iters[c] = (int16_t)min(root ? iteration : iteration + 1, 32767);
+    K.pair_evals[c] = pair_evals;
+    K.status[c] = root ? 0 : WF_E_RUNAWAY;
+  }
+  return true;
+}
+
 // The contigs whose dense decision state outgrew the LDS arena (big_list, counters[2]):
 // one wave each with kSpSlot bytes of HBM scratch (S.sp_ws); the ones sp_level declines go
 // to big2_list (counters[1]) for k_decide_big.
@@ -879,21 +1221,44 @@ __global__ __launch_bounds__(64) void k_big_sparse(const SArgs S, int level, int
 // dump_list[2 i + 1]).  S.seed_pend / ccnt / cleaves: decided -> pend 0 and no staged
 // attachments; raised -> pend 2 (level-1 seed); declined (> 63 loci, class or pair tables
 // outgrown) -> pend 1, the staged kernels take level 0.
-__global__ __launch_bounds__(64) void k_dump_sparse(const SArgs S, int64_t* ccnt, int64_t* cleaves) {
-  __shared__ SpShared sh;
+//
+// Wave levels (S.roll_next set): level `level` of the contigs the first form handed over at
+// that level; a raised contig is appended to the next level's list.  The kernel also sets up
+// the next level: its table counter (S.dump_ctr_next) and the ancestors one level up
+// (S.anc: parent^(jump + level + 1) of every name; k_wave of this level is done with them).
+__global__ __launch_bounds__(64) void k_dump_sparse(const SArgs S, int64_t* ccnt, int64_t* cleaves, int level) {
+  constexpr size_t kShBytes = sizeof(SpShared) > sizeof(E2Shared) ? sizeof(SpShared) : sizeof(E2Shared);
+  __shared__ __attribute__((aligned(16))) char sh_raw[kShBytes];
+  SpShared& sh = *reinterpret_cast<SpShared*>(sh_raw);
+  E2Shared& sh2 = *reinterpret_cast<E2Shared*>(sh_raw);
+  if (S.dump_ctr_next && blockIdx.x == 0 && threadIdx.x == 0) *S.dump_ctr_next = 0ull;
+  if (S.anc) {
+    const int up = level == 0 ? S.k.p.jump + 1 : 1;
+    for (int t = blockIdx.x * 64 + threadIdx.x; t < S.n_tax; t += gridDim.x * 64) {
+      int x = level == 0 ? t : S.anc[t];
+      for (int j = 0; j < up; ++j) x = S.k.parent[x];
+      S.anc[t] = x;
+    }
+  }
   char* ws = S.sp_ws + (int64_t)blockIdx.x * kSpSlot;
   const int count = (int)(*S.dump_ctr >> 40);
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
     const int c = S.dump_list[2 * i + 1];
     if (c < 0) continue;                             // (its table did not fit: pend 1 stands)
-    const bool ok = sp_level(S, sh, ws, c, i, 0, 1);
+    const bool ok = S.dump_list[2 * i] == 1
+                        ? sp_two(S, sh2, c, S.dump_first[i], S.dump_first[i + 1], S.dump_um[i], level)
+                        : sp_level(S, sh, ws, c, i, level, 1);
     if (threadIdx.x == 0) {
+      const int pd = S.seed_pend[c];
       if (!ok) {
         S.seed_pend[c] = 1;
-      } else if (S.seed_pend[c] == 3) {
+        if (S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);
+      } else if (pd == 3) {
         S.seed_pend[c] = 0;
         ccnt[c] = 0;
         cleaves[c] = 0;
+      } else if (pd == 2 && S.roll_next) {
+        S.roll_next[atomicAdd(S.roll_next_n, 1ull)] = c;
       }
     }
     __syncthreads();

@@ -1008,7 +1008,9 @@ __device__ __forceinline__ bool decide_contig(const SArgs& S, int c, int cr, int
     C.xcap = cls_bytes(Pmax);
     C.xws = ar.take<char>(C.xcap);
   }
-  if (!ar.fits() || (in_lds && S.route_sparse)) {
+  // routed decisions go to k_big_sparse -- unless it would decline them (> 63 loci: the
+  // segment-table form's locus masks), then the arena decides here
+  if (!ar.fits() || (in_lds && S.route_sparse && G <= 63)) {
     if (tid == 0) K.need[c] = ar.used + 4096;
     __syncthreads();
     return false;
@@ -1237,6 +1239,9 @@ struct StagedState {
   int sparse_big = 3;                // WF_OPT_SPARSE_BIG (0 dense, 1 overflow, 2 all, 3 decisions)
   int sparse_res = -1;               // resident k_big_sparse waves per CU
   int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
+  int wave_two = 1;                  // WF_OPT_WAVE_TWO: explain_two + roll-up levels in the wave form
+  int64_t dump_cap = 0;              // WF_OPT_DUMP_CAP (0: max(32 N, 65536))
+  Buf roll0, roll1, roll_cnt, anc;   // wave levels: contig lists, per-level counts, ancestors
   // per-phase timing (wf_phase): event pool, this call's spans (phase, begin, end)
   bool timing = false;
   std::vector<hipEvent_t> tev;
@@ -1246,7 +1251,7 @@ struct StagedState {
   int64_t phase_n[8] = {0};
   Buf act0, act1, base0, base1, big_list, big2_list, two_list, one_list, big_ws, tmp, pend, act_l0;
   Buf sp_ws;                        // k_big_sparse scratch (kSpSlot per wave)
-  Buf dump_cg, dump_mean, dump_first, dump_list, dump_ctr;   // level-0 hand-over (k_dump_sparse)
+  Buf dump_cg, dump_mean, dump_first, dump_list, dump_ctr, dump_um;   // hand-over (k_dump_sparse)
   bool level0 = true;               // wave kernels (wf_fast.hip) before the staged kernels
   bool rollup = false;              // ... carrying the roll-up levels too
   bool lut_ready = false;
@@ -1303,9 +1308,11 @@ void staged_set_lds(StagedState* st, int64_t bytes) {
   st->dec_lds_fixed = true;
 }
 
-void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit) {
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap) {
   st->sparse_big = sparse_big;
   st->att_limit = att_limit;
+  st->wave_two = wave_two;
+  st->dump_cap = dump_cap;
 }
 
 void staged_timing(StagedState* st, bool on) {
@@ -1637,17 +1644,36 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
 #else
     const bool dump = st->sparse_big != 0 && !st->rollup;
 #endif
+    // Wave levels (WF_OPT_WAVE_TWO): the first form also decides explain_two and carries the
+    // roll-up levels, one launch per level over the contigs the level before raised
+    const bool levels = dump && st->wave_two;
     SArgs da = sa;
+    unsigned long long* rcnt = nullptr;              // [kMaxIter + 2] per-level list counts, fail count
     if (dump) {
-      const int64_t cap = std::min<int64_t>(std::max<int64_t>((int64_t)N * 32, 1 << 16), (1ll << 31) - 4096);
+      int64_t cap = std::min<int64_t>(std::max<int64_t>((int64_t)N * 32, 1 << 16), (1ll << 31) - 4096);
+      if (st->dump_cap > 0) cap = st->dump_cap;      // WF_OPT_DUMP_CAP (tests: the overflow branch)
       ST_TRY(st->dump_cg.ensure(s, (size_t)cap * 8)); ST_TRY(st->dump_mean.ensure(s, (size_t)cap * 8));
       ST_TRY(st->dump_first.ensure(s, ((size_t)N + 1) * 4)); ST_TRY(st->dump_list.ensure(s, (size_t)N * 8));
-      ST_TRY(st->dump_ctr.ensure(s, 8));
-      ST_TRY(hipMemsetAsync(st->dump_ctr.p, 0, 8, s));
+      ST_TRY(st->dump_ctr.ensure(s, 16));
+      ST_TRY(hipMemsetAsync(st->dump_ctr.p, 0, 16, s));
       da.dump_cap = cap;
       da.dump_cg = st->dump_cg.as<int2>(); da.dump_mean = st->dump_mean.as<double>();
       da.dump_first = st->dump_first.as<int32_t>(); da.dump_list = st->dump_list.as<int32_t>();
       da.dump_ctr = st->dump_ctr.as<unsigned long long>();
+      if (levels) {
+        ST_TRY(st->dump_um.ensure(s, (size_t)N * 8));
+        da.dump_um = st->dump_um.as<uint64_t>();
+        ST_TRY(st->roll0.ensure(s, (size_t)N * 4)); ST_TRY(st->roll1.ensure(s, (size_t)N * 4));
+        ST_TRY(st->roll_cnt.ensure(s, (kMaxIter + 3) * sizeof(unsigned long long)));
+        ST_TRY(st->anc.ensure(s, (size_t)std::max(n_tax, 1) * 4));
+        ST_TRY(hipMemsetAsync(st->roll_cnt.p, 0, (kMaxIter + 3) * sizeof(unsigned long long), s));
+        rcnt = st->roll_cnt.as<unsigned long long>();
+        da.n_tax = n_tax;
+        da.wave_two = 1;
+        da.roll_next = st->roll1.as<int32_t>();     // level L appends to roll[(L + 1) & 1]
+        da.roll_next_n = rcnt + 1;
+        da.fail_ctr = rcnt + kMaxIter + 2;
+      }
     }
     ST_TRY(launch_fast(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
                        st->cus, s));
@@ -1659,12 +1685,52 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       da.sp_ws = st->sp_ws.as<char>();
       da.seg_cg = da.dump_cg; da.seg_mean = da.dump_mean; da.crank_first = da.dump_first;
       da.seed_pend = st->pend.as<int32_t>();
+      if (levels) {
+        da.anc = st->anc.as<int32_t>();               // (k_dump_sparse: ancestors of level 1)
+        da.dump_ctr_next = da.dump_ctr + 1;
+      }
       hipLaunchKernelGGL(k_dump_sparse, dim3(grid), dim3(64), 0, s, da, st->cnt.as<int64_t>(),
-                         st->cnt_leaves.as<int64_t>());
+                         st->cnt_leaves.as<int64_t>(), 0);
       ST_TRY(hipGetLastError());
       const int t_h1 = t_mark(st, s);
       t_span(st, WF_PHASE_HANDOVER, t_h0, t_h1);
       t_waves = t_h1;                                  // the waves span resumes here
+      if (levels) {
+        // levels 1, 2, ...: enqueued kLevelChunk at a time (a level with an empty list costs two
+        // near-empty launches), then the next level's count is read back
+        constexpr int kLevelChunk = 5;
+        unsigned long long* dctr = st->dump_ctr.as<unsigned long long>();
+        int32_t* roll[2] = {st->roll0.as<int32_t>(), st->roll1.as<int32_t>()};
+        int L = 1;
+        unsigned long long* hcnt = st->host_counters;
+        for (;;) {
+          const int L_end = std::min(L + kLevelChunk - 1, kMaxIter);
+          for (; L <= L_end; ++L) {
+            SArgs la = da;
+            la.dump_ctr = dctr + (L & 1);
+            la.dump_ctr_next = dctr + ((L + 1) & 1);
+            la.roll_next = roll[(L + 1) & 1];
+            la.roll_next_n = rcnt + L + 1;
+            ST_TRY(launch_level(la, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
+                                roll[L & 1], reinterpret_cast<const int64_t*>(rcnt + L), L, max_hits, st->cus, s));
+            hipLaunchKernelGGL(k_dump_sparse, dim3(grid), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
+                               st->cnt_leaves.as<int64_t>(), L);
+            ST_TRY(hipGetLastError());
+          }
+          if (st->mbox) {
+            ST_TRY(publish_sync(st, s, rcnt + L, 1, rcnt + kMaxIter + 2, 1, hcnt));
+          } else {
+            ST_TRY(hipMemcpyAsync(hcnt, rcnt + L, 8, hipMemcpyDeviceToHost, s));
+            ST_TRY(hipMemcpyAsync(hcnt + 1, rcnt + kMaxIter + 2, 8, hipMemcpyDeviceToHost, s));
+            ST_TRY(spin_sync(s, st->lvl_ev[0]));
+          }
+          if (hcnt[0] == 0 || L > kMaxIter) break;
+        }
+        const int t_r1 = t_mark(st, s);
+        t_span(st, WF_PHASE_ROLLUP, t_h1, t_r1);
+        t_waves = t_r1;
+        if (hcnt[1] == 0) return 0;                    // every contig finished in the wave forms
+      }
     }
     // the other contigs it handed over (pend 1) through the second wave form, its list and
     // count built on the device
