@@ -70,7 +70,15 @@ def parse_args():
                     help="waafle_orgscorer flags for the main workload, e.g. '--weak-loci assign-unknown'")
     ap.add_argument("--option", action="append", default=[],
                     help="wf_set_option NAME=VALUE (sparse_big, att_limit, wave_two, dump_cap); repeatable")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: "
+                         "control traffic on the CPU, e.g. with several ranks on one device)")
+    ap.add_argument("--device-map", default=None,
+                    help="device of each local rank, e.g. '0,0' (two ranks on device 0: a "
+                         "rehearsal of the N > 1 branch on one GPU, not a scaling number)")
     ap.add_argument("--traffic-json", default=None)
+    ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r04", "cfg4_valu.json"),
+                    help="PMC VALU counts of the main pass (scripts/pmc_main.py, optional)")
     ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r03_k2_pmc.json"),
                     help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
     return ap.parse_args()
@@ -260,7 +268,7 @@ class DeviceBatch:
         return self.out[f].cpu().numpy()
 
 
-def timed_passes(so, h, chk, db, params, steps, warmup, dist, dev):
+def timed_passes(so, h, chk, db, params, steps, warmup, dist, dev, cdev=None):
     """W untimed passes, then K passes bracketed by barrier + synchronize, with the
     library's HIP-event timing on: (elapsed seconds max over ranks, wf_timing)."""
     import torch
@@ -287,14 +295,14 @@ def timed_passes(so, h, chk, db, params, steps, warmup, dist, dev):
     tm = L.WfTiming()
     chk(so.wf_timing_read(h, C.byref(tm)))
     chk(so.wf_timing_enable(h, 0))
-    return wdist.max_over_ranks(t1 - t0, dist, dev), tm
+    return wdist.max_over_ranks(t1 - t0, dist, cdev), tm
 
 
-def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json):
+def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=None):
     """The explain_two stress leg (BASELINE configs[4]) on this rank's cfg5 share."""
     import torch
     db = DeviceBatch(kbatch, dev)
-    elapsed, tm = timed_passes(so, h, chk, db, params, steps, 1, dist, dev)
+    elapsed, tm = timed_passes(so, h, chk, db, params, steps, 1, dist, dev, cdev)
     pe = db.host("pair_evals")
     calls = db.host("call")
     counts = k2_algorithmic(pe, kbatch)
@@ -307,11 +315,11 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json):
     v = np.array([counts["pairs"], counts["b_k2_bytes"], kbatch.n_contigs,
                   float((calls == 2).sum())], dtype=np.float64)
     if dist:
-        t = torch.tensor(v, device=dev)
+        t = torch.tensor(v, device=cdev)
         dist.all_reduce(t)
         v = t.cpu().numpy()
     k2_s = np.array([k2_ms * 1e-3])
-    k2_max = float(wdist_max(k2_s[0], dist, dev))
+    k2_max = float(wdist_max(k2_s[0], dist, cdev))
     pass_s = elapsed / steps
     achieved = v[1] / k2_max / 1e9
     out = {
@@ -359,9 +367,13 @@ def main():
     cores, _ = host_cpus()
     workers = max(1, min(16, cores // world))
 
-    # ---- generate this rank's contig ranges BEFORE touching the GPU (fork-safe) ----
-    n_total = args.contigs or synth.CONFIGS[args.config]["n"]
-    a, b = wdist.rank_bounds(np.ones(n_total), world)[rank]    # uniform expected cost
+    # ---- generate this rank's contigs BEFORE touching the GPU (fork-safe) ----
+    # Weak scaling (contigs are independent, no data-path collective): every rank scores the
+    # configuration's full per-GPU workload, rank r the contigs [r n, (r + 1) n) of one
+    # seeded stream of world * n contigs
+    n_per = args.contigs or synth.CONFIGS[args.config]["n"]
+    n_total = n_per * world
+    a, b = rank * n_per, (rank + 1) * n_per
     t_gen = time.perf_counter()
     batch, tax = synth.generate_batch(args.config, a, b, workers=workers, n_total=n_total)
     kbatch = ktax = None
@@ -381,12 +393,19 @@ def main():
     import torch
     from waafle_amd import cli, engine, lib as L
     dist = None
+    dmap = [int(x) for x in args.device_map.split(",")] if args.device_map else None
+    ordinal = dmap[local] if dmap else local
+    dev = torch.device("cuda", ordinal)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(dev)
+    # collectives' tensors: on the device for RCCL, on the host for gloo
+    cdev = dev if args.backend == "nccl" else None
 
     N, NH = batch.n_contigs, batch.n_hits
     pdict = cli.param_dict(cli.parse_flags(args.flags.split()))
@@ -394,7 +413,7 @@ def main():
     k2_params = engine.params_struct(cli.param_dict(cli.parse_flags([])))
     so = L.load()
     h = C.c_void_p()
-    assert so.wf_init(local, C.byref(h)) == 0, "wf_init failed"
+    assert so.wf_init(ordinal, C.byref(h)) == 0, "wf_init failed"
 
     def chk(rc):
         if rc:
@@ -414,7 +433,7 @@ def main():
     chk(so.wf_set_stream(h, C.c_void_p(stream.cuda_stream)))
 
     db = DeviceBatch(batch, dev)
-    elapsed, tm = timed_passes(so, h, chk, db, params, args.steps, args.warmup, dist, dev)
+    elapsed, tm = timed_passes(so, h, chk, db, params, args.steps, args.warmup, dist, dev, cdev)
     calls, pe, iters = db.host("call"), db.host("pair_evals"), db.host("iterations")
     del db
     torch.cuda.empty_cache()
@@ -423,7 +442,7 @@ def main():
     if dist:          # whole-job counts
         v = torch.tensor([pairs, float((calls == 2).sum()), float((calls == 1).sum()),
                           float((calls == 0).sum()), float((iters > 1).sum())],
-                         dtype=torch.float64, device=dev)
+                         dtype=torch.float64, device=cdev)
         dist.all_reduce(v)
         pairs, n_lgt, n_no, n_un, n_up = v.tolist()
     else:
@@ -432,31 +451,54 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     value = n_total / (elapsed / args.steps)
     pass_ms = tm.pass_ms / max(1, tm.passes)
+    phases = tm.phases()
+    # the dominant kernel: the first wave form's level-0 launch (wf_phase "waves" spans that
+    # launch alone when the wave levels run), every contig's hits and loci read once and
+    # every record written -- the whole algorithmic byte count of the pass
+    dom_ms = phases["waves"][0] / max(1, tm.passes)
     b_alg = algorithmic_bytes(batch)
-    achieved = b_alg / (pass_ms * 1e-3) / 1e9
+    achieved = b_alg / (dom_ms * 1e-3) / 1e9
+    achieved_pass = b_alg / (pass_ms * 1e-3) / 1e9
     traffic, tsrc = None, None
-    tpath = args.traffic_json or os.path.join(PROFILES, "r03_traffic_{}.json".format(args.config))
+    tpath = args.traffic_json or os.path.join(PROFILES, "r04", "traffic_{}.json".format(args.config))
     if os.path.exists(tpath):
         with open(tpath) as fh:
             tj = json.load(fh)
         if tj.get("config") == args.config and tj.get("contigs") == N:
-            traffic = tj.get("hbm_bytes_per_launch")
-            tsrc = {k: tj.get(k) for k in ("fetch_bytes_raw", "fetch_bytes_x2", "write_bytes",
-                                           "hbm_bytes_raw", "hbm_bytes_x2",
-                                           "dispatches_per_pass", "source")}
+            traffic = tj.get("dominant_hbm_bytes_raw")
+            tsrc = {k: tj.get(k) for k in ("dominant_kernel", "dominant_fetch_bytes_raw",
+                                           "dominant_write_bytes", "fetch_bytes_raw",
+                                           "fetch_bytes_x2", "write_bytes", "hbm_bytes_raw",
+                                           "hbm_bytes_x2", "dispatches_per_pass", "source")}
+    valu = None
+    if args.valu_pmc_json and os.path.exists(args.valu_pmc_json):
+        with open(args.valu_pmc_json) as fh:
+            vj = json.load(fh)
+        if vj.get("config") == args.config and vj.get("contigs") == N:
+            peak = vj.get("valu_peak_insts_per_s", 1.2288e12)
+            vi, vd = vj["valu_insts_per_pass"], vj["dominant_valu_insts_per_pass"]
+            valu = {"unit": "wave-instructions/s", "peak": peak,
+                    "pass": {"insts": vi, "achieved": vi / (pass_ms * 1e-3),
+                             "frac": vi / (pass_ms * 1e-3) / peak},
+                    "dominant": {"kernel": vj.get("dominant_kernel"), "insts": vd,
+                                 "achieved": vd / (dom_ms * 1e-3),
+                                 "frac": vd / (dom_ms * 1e-3) / peak,
+                                 "wait_frac": vj.get("dominant_wait_frac")},
+                    "source": vj.get("source")}
     spec = synth.CONFIGS[args.config]
     result = {
         "metric": "contigs scored/sec + k2 clade-pair evals/sec at 1/2/4/8 MI355X vs CPU ref",
         "value": value, "unit": "contigs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded generator, SURVEY §8(d) shapes)",
-        "config": {"workload": "{}: {} contigs x {} genes x {} clades, {} hits, {}"
-                               .format(args.config, n_total, spec["genes"], spec["clades"],
-                                       NH * world if world == 1 else "~{}".format(NH * world),
+        "config": {"workload": "{}: {} contigs x {} genes x {} clades per GPU, {} hits{}, {}"
+                               .format(args.config, n_per, spec["genes"], spec["clades"], NH,
+                                       "" if world == 1 else " on rank 0",
                                        "flags " + args.flags if args.flags else "default flags"),
                    "contigs_total": n_total, "contigs_per_gpu": N, "hits_per_gpu": NH,
-                   "parallelism": "dp{} (static contig split, no collective)".format(world)},
+                   "parallelism": "dp{} (each rank its own contigs, no data-path collective)"
+                                  .format(world)},
         "k2_pair_evals_per_sec": None,
         "k2_pair_evals_note": "reference-equivalent count: sum of P_pot(P_pot-1)/2 over "
                               "explain_two calls (orgscorer.py:606-608 score(c1,c2) calls), "
@@ -470,12 +512,23 @@ def main():
                              for k, v in tm.phases().items()}),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "wf_score pass (every kernel of one pass: wave kernels + "
-                               "staged remainder; HIP events on its stream)",
+                     "kernel": "k_wave<224, false, false>: the first wave form's level-0 launch "
+                               "(HIP events on its stream, wf_phase waves)",
+                     "kernel_ms": dom_ms,
                      "algorithmic_bytes_per_launch": b_alg,
                      "algorithmic_bytes_rule": "24 B/hit + 12 B/locus + 96 B/contig",
+                     "pass": {"ms": pass_ms, "achieved": achieved_pass,
+                              "frac": achieved_pass / HBM_PEAK_GBS,
+                              "note": "every kernel of one wf_score pass (level 0, hand-over, "
+                                      "roll-up levels, staged remainder)"},
+                     "valu": valu,
                      "traffic_detail": tsrc},
         "options": args.option or None,
+        "ranks": {"backend": args.backend if world > 1 else None,
+                  "devices": dmap[:world] if dmap else list(range(world)),
+                  "note": (None if not dmap or len(set(dmap[:world])) == world else
+                           "ranks share a device: a rehearsal of the N > 1 branch, not a "
+                           "scaling number")},
         "generate_s": t_gen,
         "cpu_baseline": None,
     }
@@ -484,7 +537,7 @@ def main():
             tk = engine.taxonomy_struct(ktax)
             chk(so.wf_set_taxonomy(h, C.byref(tk)))
         result["k2"] = k2_leg(so, h, chk, kbatch, k2_params, args.k2_steps, dist, dev, world,
-                              args.k2_pmc_json)
+                              args.k2_pmc_json, cdev)
         result["k2_pair_evals_per_sec"] = result["k2"]["k2_pair_evals_per_sec"]
     if rank == 0 and world == 1 and args.pcie:
         # scope (ii): host (pageable numpy) arrays in, host results out, second call timed

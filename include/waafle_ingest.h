@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define WF_INGEST_ABI_VERSION 1
+#define WF_INGEST_ABI_VERSION 2
 
 enum wf_ingest_status {
   WF_INGEST_OK = 0,
@@ -77,6 +77,9 @@ typedef struct wf_ingest_view {
   /* warnings (orgscorer.py:944-946 and the GFF equivalent) */
   const char* warn_gff_blob; const int64_t* warn_gff_off;
   const char* warn_blast_blob; const int64_t* warn_blast_off;
+  /* per contig: the LOCI output field, the kept loci's codes "start:end:strand" joined by
+     '|' (orgscorer.py:795-800), [n_contigs + 1] offsets */
+  const char* loci_blob; const int64_t* loci_off;
 } wf_ingest_view;
 
 int wf_ingest_abi_version(void);

@@ -18,10 +18,15 @@ import sys
 from collections import defaultdict
 
 
+DOMINANT = "k_wave<224, false, false>"   # the first wave form's level-0 launch
+
+
 def per_pass(d, counter, passes):
+    """(KB per pass over the pass's kernels, dispatches, KB per pass of the dominant kernel)"""
     files = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
     assert files, "no counter_collection.csv under " + d
     acc = defaultdict(float)
+    dom = 0.0
     for r in csv.DictReader(open(files[0])):
         if r["Counter_Name"] != counter:
             continue
@@ -29,15 +34,17 @@ def per_pass(d, counter, passes):
                 "wf::" in r["Kernel_Name"] or "rocprim" in r["Kernel_Name"]):
             continue     # pass = our kernels + device sorts/scans (runtime fills/copies not counted)
         acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
+        if DOMINANT in r["Kernel_Name"]:
+            dom += float(r["Counter_Value"])
     assert acc, "no {} rows".format(counter)
-    return sum(acc.values()) / passes, len(acc)
+    return sum(acc.values()) / passes, len(acc), dom / passes
 
 
 def main():
     fdir, wdir, config, contigs, out = sys.argv[1:6]
     passes = int(sys.argv[sys.argv.index("--pass") + 1])
-    f_kb, nf = per_pass(fdir, "FETCH_SIZE", passes)
-    w_kb, nw = per_pass(wdir, "WRITE_SIZE", passes)
+    f_kb, nf, f_dom = per_pass(fdir, "FETCH_SIZE", passes)
+    w_kb, nw, w_dom = per_pass(wdir, "WRITE_SIZE", passes)
     fetch_raw = f_kb * 1024.0
     write = w_kb * 1024.0
     res = {"config": config, "contigs": int(contigs),
@@ -48,6 +55,9 @@ def main():
            "write_bytes": write,
            "hbm_bytes_raw": fetch_raw + write, "hbm_bytes_x2": 2.0 * fetch_raw + write,
            "hbm_bytes_per_launch": fetch_raw + write,
+           "dominant_kernel": DOMINANT,
+           "dominant_fetch_bytes_raw": f_dom * 1024.0, "dominant_write_bytes": w_dom * 1024.0,
+           "dominant_hbm_bytes_raw": (f_dom + w_dom) * 1024.0,
            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate runs ({}, {})".format(
                fdir, wdir)}
     with open(out, "w") as fh:

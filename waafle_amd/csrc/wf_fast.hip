@@ -60,9 +60,12 @@ constexpr int kXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its 
 // Diagnostic build only (-DWF_STAMPS): per-phase shader-clock laps of the first form on
 // every 16th contig, plus counters (scripts/wave_stamps.py reads them).  Never in the
 // product build.
+#ifndef WF_STAMPS_ROLL
+#define WF_STAMPS_ROLL 0             // stamps of the roll-up launches instead of level 0
+#endif
 #ifdef WF_STAMPS
 __device__ unsigned long long g_wstamps[48];
-#define WLAP_MARK() unsigned long long wlap_ = __builtin_amdgcn_s_memtime(); const bool wsamp_ = !FULL && (c & 15) == 0
+#define WLAP_MARK() unsigned long long wlap_ = __builtin_amdgcn_s_memtime(); const bool wsamp_ = !FULL && (WF_STAMPS_ROLL ? ROLL : !ROLL) && (c & 15) == 0
 #define WLAP(i)                                                                     \
   do {                                                                              \
     const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
@@ -593,16 +596,19 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
   return (Pn == 0 || root) ? kDecStop : kDecRaise;
 }
 
-template <int CAP, bool FULL>
+template <int CAP, bool FULL, bool ROLL = false>
 // rollup (FULL): carry a contig through its roll-up levels in the slice; else hand it to
 // the staged kernels at its first raise (they run every contig of a level together,
 // which measured 3x faster per contig-level on cfg4 than one wave per contig here).
 // S_arg must stay the first parameter: kernarg_fresh reads the argument block at kernarg
-// offset 0.  start_level > 0 (first form only): roll-up level start_level of the contigs in
-// `list` (the wave levels, S.anc set).
+// offset 0.  ROLL (first form only): roll-up level start_level > 0 of the contigs in `list`
+// (the wave levels, S.anc set) -- its own instantiation, so profiles tell the level-0 pass
+// from the roll-up passes and level 0 carries none of their code.
 __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
                                              const int32_t* list, int n_list, const int64_t* n_dev, int rollup,
-                                             int start_level) {
+                                             int start_level_arg) {
+  static_assert(!(FULL && ROLL), "the roll-up passes are first-form launches");
+  const int start_level = ROLL ? start_level_arg : 0;
   if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WaveSmem<CAP, FULL>& F = *reinterpret_cast<WaveSmem<CAP, FULL>*>(smem);
@@ -1454,14 +1460,14 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
 // Resident k_wave workgroups per CU.  One value per process (every device is a gfx950 with
 // the same kernel image); the static's initialisation is thread-safe (C++11), so contexts on
 // several host threads may call this concurrently.
-template <int CAP, bool FULL>
+template <int CAP, bool FULL, bool ROLL = false>
 int blocks_per_cu() {
   static const int n = [] {
     const int bytes = (int)sizeof(WaveSmem<CAP, FULL>);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wave<CAP, FULL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wave<CAP, FULL, ROLL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_wave<CAP, FULL>), 64,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_wave<CAP, FULL, ROLL>), 64,
                                                      bytes) != hipSuccess || b < 1)
       b = 1;
     return b;
@@ -1470,11 +1476,11 @@ int blocks_per_cu() {
 }
 
 // n_list: the list length, or (n_dev set) an upper bound for the grid
-template <int CAP, bool FULL>
+template <int CAP, bool FULL, bool ROLL = false>
 hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
                       int n_list, const int64_t* n_dev, int cus, int rollup, hipStream_t s, int start_level = 0) {
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_list, (int64_t)cus * blocks_per_cu<CAP, FULL>()));
-  hipLaunchKernelGGL((k_wave<CAP, FULL>), dim3(grid), dim3(64), sizeof(WaveSmem<CAP, FULL>), s, sa, ccnt, cleaves, pend,
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(n_list, (int64_t)cus * blocks_per_cu<CAP, FULL, ROLL>()));
+  hipLaunchKernelGGL((k_wave<CAP, FULL, ROLL>), dim3(grid), dim3(64), sizeof(WaveSmem<CAP, FULL>), s, sa, ccnt, cleaves, pend,
                      list, n_list, n_dev, rollup, start_level);
   return hipGetLastError();
 }
@@ -1506,10 +1512,10 @@ hipError_t launch_level(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_
                         const int64_t* n_dev, int level, int max_hits, int cus, hipStream_t s) {
   const int N = sa.k.n_contigs;
 #ifndef WF_NO_CAP224
-  if (max_hits <= 224) return launch_cap<224, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
+  if (max_hits <= 224) return launch_cap<224, false, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
 #endif
-  return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level)
-                         : launch_cap<512, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
+  return max_hits <= 256 ? launch_cap<256, false, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level)
+                         : launch_cap<512, false, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
 }
 
 hipError_t launch_full(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,

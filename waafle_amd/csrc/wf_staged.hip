@@ -1631,8 +1631,8 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   // or HBM annotation slots are needed.
   // (the wave kernels' 32-bit keys hold clade ids below 2^17)
   const bool level0 = st->level0 && !det && (int64_t)max_loci * k.n_sys <= kAnnSlots && sa.key_tb <= 17;
-  int t_waves = level0 ? t_mark(st, s) : -1;
   hipLaunchKernelGGL(k_init, dim3(grid_for(N)), dim3(256), 0, s, sa.k);
+  int t_waves = level0 ? t_mark(st, s) : -1;          // (the waves span: the wave launches alone)
   if (level0) {
     ST_TRY(st->pend.ensure(s, (size_t)N * 4));
     ST_TRY(st->act0.ensure(s, (size_t)N * 4));

@@ -34,7 +34,8 @@ class WfIngestView(C.Structure):
                 ("loc_off", _P), ("loc_start", _P), ("loc_end", _P), ("loc_strand", _P),
                 ("loc_strand_blob", _P), ("loc_strand_off", _P),
                 ("warn_gff_blob", _P), ("warn_gff_off", _P),
-                ("warn_blast_blob", _P), ("warn_blast_off", _P)]
+                ("warn_blast_blob", _P), ("warn_blast_off", _P),
+                ("loci_blob", _P), ("loci_off", _P)]
 
 
 class IngestError(RuntimeError):
@@ -64,17 +65,35 @@ def load(path=LIB_PATH):
     so.wf_ingest_parse.restype = C.c_int
     so.wf_ingest_get_view.argtypes = [_P, C.POINTER(WfIngestView)]
     so.wf_ingest_get_view.restype = C.c_int
-    if so.wf_ingest_abi_version() != 1:
+    if so.wf_ingest_abi_version() != 2:
         raise IngestError("libwaafle_ingest.so ABI mismatch")
     _lib = so
     return so
 
 
-def _arr(ptr, n, dtype):
+class _Owner:
+    """Keeps a parsed wf_ingest object (and the arrays it owns) alive; the numpy arrays
+    handed out are views of its memory and hold a reference to it."""
+
+    def __init__(self, so, h):
+        self.so, self.h = so, h
+
+    def __del__(self):
+        if self.h:
+            self.so.wf_ingest_free(self.h)
+            self.h = None
+
+
+def _arr(ptr, n, dtype, owner=None):
+    """n elements at ptr as a numpy array: a view of the native memory kept alive by
+    `owner`, or a copy when there is none."""
     if n == 0 or not ptr:
         return np.zeros(0, dtype=dtype)
     buf = (C.c_char * (n * np.dtype(dtype).itemsize)).from_address(ptr)
-    return np.frombuffer(buf, dtype=dtype, count=n).copy()
+    if owner is None:
+        return np.frombuffer(buf, dtype=dtype, count=n).copy()
+    buf._owner = owner
+    return np.frombuffer(buf, dtype=dtype, count=n)
 
 
 class StringTable:
@@ -92,7 +111,7 @@ class StringTable:
             return [self[j] for j in range(*i.indices(len(self)))]
         if i < 0:
             i += len(self)
-        return self._blob[self._off[i]:self._off[i + 1]].decode("ascii")
+        return bytes(self._blob[self._off[i]:self._off[i + 1]]).decode("ascii")
 
     def __iter__(self):
         return (self[i] for i in range(len(self)))
@@ -101,9 +120,58 @@ class StringTable:
         return list(self) == list(other)
 
 
-def _table(blob, off_ptr, n):
+def _table(blob, off_ptr, n, owner=None):
     off = _arr(off_ptr, n + 1, np.int64) if n else np.zeros(1, dtype=np.int64)
+    if owner is not None and off[-1]:
+        raw = (C.c_char * int(off[-1])).from_address(blob)
+        raw._owner = owner
+        return StringTable(memoryview(raw).cast("B"), off)
     return StringTable(C.string_at(blob, int(off[-1])) if off[-1] else b"", off)
+
+
+class LociCodes:
+    """Per-locus codes "start:end:strand" (utils.py:312) of natively parsed loci, formatted
+    only when a per-locus list is asked for (the TSV writer takes the per-contig fields
+    the parser joined, HostBatch.loci_fields).  Slices stay lazy."""
+
+    def __init__(self, start, end, strands):
+        self._s, self._e, self._st = start, end, strands
+        self._list = None
+
+    def __len__(self):
+        return len(self._s)
+
+    def _all(self):
+        if self._list is None:
+            st = self._st
+            self._list = ["{}:{}:{}".format(a, b, st[i]) for i, (a, b) in
+                          enumerate(zip(self._s.tolist(), self._e.tolist()))]
+        return self._list
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            a, b, step = i.indices(len(self))
+            if step == 1:
+                return LociCodes(self._s[a:b], self._e[a:b], _Sliced(self._st, a, b))
+            return self._all()[i]
+        return self._all()[i]
+
+    def __iter__(self):
+        return iter(self._all())
+
+    def __eq__(self, other):
+        return list(self._all()) == list(other)
+
+
+class _Sliced:
+    def __init__(self, table, a, b):
+        self._t, self._a, self._n = table, a, b - a
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        return self._t[self._a + i]
 
 
 def _strings(blob, off_ptr, n):
@@ -122,6 +190,7 @@ def parse(contigs_path, blastout_path, gff_path, edges, min_gene_length, threads
     h = so.wf_ingest_new()
     if not h:
         raise MemoryError("wf_ingest_new failed")
+    owner = _Owner(so, h)       # frees the parse when the last array view is gone
     try:
         rc = so.wf_ingest_parse(h, os.fsencode(contigs_path), os.fsencode(blastout_path),
                                 os.fsencode(gff_path), float(min_gene_length), int(threads))
@@ -142,29 +211,32 @@ def parse(contigs_path, blastout_path, gff_path, edges, min_gene_length, threads
         names = _strings(v.contig_blob, v.contig_off, N)
         taxa = _strings(v.taxa_blob, v.taxa_off, v.n_taxa)
         systems = _strings(v.system_blob, v.system_off, v.n_systems)
-        strands = _strings(v.loc_strand_blob, v.loc_strand_off, L)
         S = max(1, v.n_systems)
         tax = TaxonomyTables(edges, extra_names=set(taxa))
         tmap = np.array([tax.index[t] for t in taxa], dtype=np.int32)
-        hit_taxon_local = _arr(v.hit_taxon, H, np.int32)
+        hit_taxon_local = _arr(v.hit_taxon, H, np.int32, owner)
         # value ids index one table shared by every system
-        values = _table(v.value_blob, v.value_off, v.n_values)
-        value_ids = _arr(v.hit_value, H * S, np.int32).reshape(H, S)
-        loc_start = _arr(v.loc_start, L, np.int32)
-        loc_end = _arr(v.loc_end, L, np.int32)
-        codes = ["{}:{}:{}".format(a, b, s) for a, b, s in
-                 zip(loc_start.tolist(), loc_end.tolist(), strands)]
+        values = _table(v.value_blob, v.value_off, v.n_values, owner)
+        value_ids = _arr(v.hit_value, H * S, np.int32, owner).reshape(H, S)
+        loc_start = _arr(v.loc_start, L, np.int32, owner)
+        loc_end = _arr(v.loc_end, L, np.int32, owner)
+        strands = _table(v.loc_strand_blob, v.loc_strand_off, L, owner)
         batch = HostBatch(
-            contig_names=names, contig_lengths=_arr(v.contig_length, N, np.int64),
-            hit_off=_arr(v.hit_off, N + 1, np.int64), hit_qlo=_arr(v.hit_qlo, H, np.int32),
-            hit_qhi=_arr(v.hit_qhi, H, np.int32),
+            contig_names=names, contig_lengths=_arr(v.contig_length, N, np.int64, owner),
+            hit_off=_arr(v.hit_off, N + 1, np.int64, owner),
+            hit_qlo=_arr(v.hit_qlo, H, np.int32, owner), hit_qhi=_arr(v.hit_qhi, H, np.int32, owner),
             hit_taxon=tmap[hit_taxon_local] if H else np.zeros(0, dtype=np.int32),
-            hit_strand=_arr(v.hit_strand, H, np.int8), hit_score=_arr(v.hit_score, H, np.float64),
-            hit_scov=_arr(v.hit_scov, H, np.float64), hit_sysmask=_arr(v.hit_sysmask, H, np.uint32),
-            loc_off=_arr(v.loc_off, N + 1, np.int64), loc_start=loc_start, loc_end=loc_end,
-            loc_strand=_arr(v.loc_strand, L, np.int8), loc_codes=codes, systems=systems,
+            hit_strand=_arr(v.hit_strand, H, np.int8, owner),
+            hit_score=_arr(v.hit_score, H, np.float64, owner),
+            hit_scov=_arr(v.hit_scov, H, np.float64, owner),
+            hit_sysmask=_arr(v.hit_sysmask, H, np.uint32, owner),
+            loc_off=_arr(v.loc_off, N + 1, np.int64, owner), loc_start=loc_start, loc_end=loc_end,
+            loc_strand=_arr(v.loc_strand, L, np.int8, owner),
+            loc_codes=LociCodes(loc_start, loc_end, strands), systems=systems,
             annot_value_ids=value_ids, annot_values=[values] * len(systems),
-            hit_row=_arr(v.hit_row, H, np.int64))
+            hit_row=_arr(v.hit_row, H, np.int64, owner),
+            loci_fields=_table(v.loci_blob, v.loci_off, N, owner))
         return batch, tax
-    finally:
-        so.wf_ingest_free(h)
+    except BaseException:
+        owner.__del__()
+        raise

@@ -57,6 +57,7 @@ class HostBatch:
     annot_value_ids: np.ndarray = None                 # [n_hits, n_systems] int32, -1 absent
     annot_values: list = field(default_factory=list)   # per system: list of value strings
     hit_row: np.ndarray = None                         # blastout row of each batch hit
+    loci_fields: object = None                         # per contig: LOCI field (native ingest)
 
     @property
     def n_contigs(self):
@@ -93,7 +94,23 @@ class HostBatch:
             loc_codes=self.loc_codes[l0:l1], systems=self.systems,
             annot_value_ids=None if self.annot_value_ids is None else self.annot_value_ids[h0:h1],
             annot_values=self.annot_values,
-            hit_row=None if self.hit_row is None else self.hit_row[h0:h1])
+            hit_row=None if self.hit_row is None else self.hit_row[h0:h1],
+            loci_fields=None if self.loci_fields is None else _ContigSlice(self.loci_fields, c0, c1))
+
+
+class _ContigSlice:
+    """Entries [c0, c1) of a per-contig string table, without copying it."""
+
+    def __init__(self, table, c0, c1):
+        self._t, self._a, self._n = table, c0, c1 - c0
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, i):
+        if i < 0:
+            i += self._n
+        return self._t[self._a + i]
 
 
 # ---------------------------------------------------------------------------

@@ -58,7 +58,8 @@ def render(batch, tax, res):
     names = batch.contig_names
     for c in sorted(range(N), key=lambda i: names[i]):
         l0, l1 = int(lo[c]), int(lo[c + 1])
-        loci = _e("|".join(batch.loc_codes[l0:l1]))
+        loci = _e(batch.loci_fields[c] if batch.loci_fields is not None
+                  else "|".join(batch.loc_codes[l0:l1]))
         call = int(res.call[c])
         length = str(int(batch.contig_lengths[c]))
         if call == CALL_NO_LGT:
