@@ -500,6 +500,7 @@ __device__ __forceinline__ bool attaches(const DevParams& P, int qlo, int qhi, i
   if (l1 > qhi || qlo > l2) return 0.0 >= P.min_overlap;   // calc_overlap -> int 0
   const int ov = min(qhi, l2) - max(qlo, l1) + 1;
   const int den = min(qhi - qlo + 1, l2 - l1 + 1);
+  if (ov == den) return 1.0 >= P.min_overlap;       // one interval inside the other: exactly 1.0
   return (double)ov / (double)den >= P.min_overlap;
 }
 

@@ -38,6 +38,11 @@
 #ifndef WF_LANE_MEANS6
 #define WF_LANE_MEANS6 0
 #endif
+// 1: every hit batch of a round finds its loci before the first takes its slots (the loci
+// searches of the batches overlap); 0: batch by batch (A/B variant)
+#ifndef WF_ATTACH_BATCHED
+#define WF_ATTACH_BATCHED 1
+#endif
 
 namespace wf {
 
@@ -604,7 +609,7 @@ template <int CAP, bool FULL, bool ROLL = false>
 // offset 0.  ROLL (first form only): roll-up level start_level > 0 of the contigs in `list`
 // (the wave levels, S.anc set) -- its own instantiation, so profiles tell the level-0 pass
 // from the roll-up passes and level 0 carries none of their code.
-__global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
+__global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
                                              const int32_t* list, int n_list, const int64_t* n_dev, int rollup,
                                              int start_level_arg) {
   static_assert(!(FULL && ROLL), "the roll-up passes are first-form launches");
@@ -714,43 +719,76 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
     int n_att = 0;
     long long nl_sum = 0;
     // kHB batches of 64 hits per round: every field of all of them is loaded up front (one
-    // global round trip per round instead of one per batch), then the batches are attached
-    // in order, each picking its fields from the round's registers by a uniform select
+    // global round trip per round instead of one per batch).  Each batch's loci are found
+    // first, for all batches at once (independent LDS reads in flight together; the loci
+    // are ascending and disjoint); then the batches take their slots in order, each picking
+    // its fields from the round's registers by a uniform select
     for (int64_t hq = h0; hq < h1; hq += 64 * kHB) {
       if (hq != h0) load_round(hq);
+      int r_n[kHB];
+      uint64_t r_am[kHB];
+      if (WF_ATTACH_BATCHED && ordered) {
+#pragma unroll
+        for (int b = 0; b < kHB; ++b) {
+          int n = 0;
+          uint64_t am = 0;
+          if (hq + 64 * b + lane < h1 && r_scv[b] >= P.min_scov) {
+            const int qlo = r_qlo[b], qhi = r_qhi[b];
+            int g = 0;                               // first locus ending at or after qlo
+#pragma unroll
+            for (int k = 32; k > 0; k >>= 1) {
+              const int i = min(g + k, Gs) - 1;
+              if (g + k <= Gs && F.lo[i] + F.len[i] - 1 < qlo) g += k;
+            }
+            for (; g < Gs; ++g) {
+              const int lo = F.lo[g], len = F.len[g];
+              if (lo > qhi) break;
+              if (attaches(P, qlo, qhi, r_hs[b], lo, len, F.st[g])) {
+                ++n;
+                nl_sum += len < kNpyBuf ? F.nl1[g] : leaves_for(S, len);
+                am |= 1ull << g;
+              }
+            }
+          }
+          r_n[b] = n;
+          r_am[b] = am;
+          if (start_level > 0 && n > 0) r_cl[b] = S.anc[r_cl[b]];   // parent^(jump + level), :431-445
+        }
+      }
     for (int bq = 0; bq < kHB && hq + 64 * bq < h1; ++bq) {
       const int64_t hb = hq + 64 * bq;
       const int64_t h = hb + lane;
       int qlo = r_qlo[0], qhi = r_qhi[0], hs = r_hs[0], clade = r_cl[0];
       double scv = r_scv[0], sc = r_sc[0];
       uint32_t m = r_m[0];
+      const bool pre = WF_ATTACH_BATCHED && ordered;   // (found above)
+      int n = pre ? r_n[0] : 0;
+      uint64_t am = pre ? r_am[0] : 0ull;
 #pragma unroll
       for (int b = 1; b < kHB; ++b)
         if (bq == b) {
           qlo = r_qlo[b]; qhi = r_qhi[b]; hs = r_hs[b]; clade = r_cl[b];
           scv = r_scv[b]; sc = r_sc[b]; m = r_m[b];
+          if (pre) { n = r_n[b]; am = r_am[b]; }
         }
-      int n = 0;
-      uint64_t am = 0;
-      if (ordered) {
-        if (h < h1 && scv >= P.min_scov) {
-          int g = 0;                                 // first locus ending at or after qlo
+      if (!pre && ordered && h < h1 && scv >= P.min_scov) {
+        int g = 0;                                   // first locus ending at or after qlo
 #pragma unroll
-          for (int b = 32; b > 0; b >>= 1) {
-            const int i = min(g + b, Gs) - 1;
-            if (g + b <= Gs && F.lo[i] + F.len[i] - 1 < qlo) g += b;
-          }
-          for (; g < Gs; ++g) {
-            const int lo = F.lo[g], len = F.len[g];
-            if (lo > qhi) break;
-            if (attaches(P, qlo, qhi, hs, lo, len, F.st[g])) {
-              ++n;
-              nl_sum += len < kNpyBuf ? F.nl1[g] : leaves_for(S, len);
-              am |= 1ull << g;
-            }
+        for (int k = 32; k > 0; k >>= 1) {
+          const int i = min(g + k, Gs) - 1;
+          if (g + k <= Gs && F.lo[i] + F.len[i] - 1 < qlo) g += k;
+        }
+        for (; g < Gs; ++g) {
+          const int lo = F.lo[g], len = F.len[g];
+          if (lo > qhi) break;
+          if (attaches(P, qlo, qhi, hs, lo, len, F.st[g])) {
+            ++n;
+            nl_sum += len < kNpyBuf ? F.nl1[g] : leaves_for(S, len);
+            am |= 1ull << g;
           }
         }
-      } else if (h < h1 && scv >= P.min_scov) {
+        if (start_level > 0 && n > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
+      } else if (!ordered && h < h1 && scv >= P.min_scov) {
         for (int g = 0; g < G; ++g) {
           int lo, len, st;
           if (g < kLoc0) {
@@ -765,12 +803,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
             if (g < kLoc0) am |= 1ull << g;
           }
         }
+        if (start_level > 0 && n > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
       }
       int total;
       const int o = wave_excl_scan(n, &total);
       if (!staged && n > 0 && n_att + o + n <= CAP) {
-        if (start_level > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
-        else
+        if (start_level == 0)
           for (int j = 0; j < P.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
         const bool ann = m != 0 && sc >= P.annot_ref;
         int slot = n_att + o;
@@ -1066,9 +1104,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
               if (kept == 0 && thread_ok) { lo = 0; hi = len; vv = Fw; one_run = true; }
             }
             if (one_run) {
-            } else if ((FULL || na <= kMultiAttL0) && nl <= 64 && len < kNpyBuf) {
+            } else if ((FULL || ROLL || na <= kMultiAttL0) && nl <= 64 && len < kNpyBuf) {
               multi = true;
-              big = na > kMultiAtt0;
+              big = na > (FULL ? kMultiAtt0 : kMultiAttL0);   // (beyond the envelope buffer)
             }
             else
               fail = true;                               // the staged leaf kernels take it
@@ -1078,8 +1116,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : 4) void k_wave(const SArgs S_arg, in
           if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
           WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));
           uint64_t mlist = __ballot(multi);
-          if ((FULL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
-            // several multi-attachment segments (roll-up levels): one lane each
+          if ((FULL || ROLL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
+            // several multi-attachment segments (roll-up levels, where a segment gathers the
+            // attachments of many clades): one lane each, not the whole wave per segment
             if (multi) {
               const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
               v[s] = lane_seg_mean(SliceSrc{F.key, F.lohi, F.sc}, kb, ke, PackedLut{F.lut + F.lbase[g]}, nl, len);

@@ -878,6 +878,7 @@ struct E2Shared {
                                              // listed parent
   unsigned long long pres[64], pm[64], hm[64], s1[64], s2[64];
   int len[64];                               // locus lengths (ambiguous fraction)
+  unsigned short cand[64 * 63 / 2];          // candidate pairs i | j << 8 (i < j)
 };
 
 // S[row][g] (0.0 without a segment)
@@ -1071,17 +1072,25 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
     if (lane < Pp) { sh.s1[lane] = s1; sh.s2[lane] = s2; }
     __syncthreads();
   }
-  // pass 1: the best candidate pair by (rank, pair index); crit >= k2 <=> (m_i | m_j) == um
+  // the candidate pairs, crit >= k2 <=> (m_i | m_j) == um, listed so that their ranks are
+  // taken 64 at a time (one pair per lane) rather than one potential clade per step
   const uint64_t my_pm = lane < Pp ? sh.pm[lane] : 0ull;
-  double pr = -__builtin_inf();
-  long long pk = -1;
+  int nc = 0;
   for (int i = 0; i + 1 < Pp; ++i) {
     const bool cand = lane > i && lane < Pp && (sh.pm[i] | my_pm) == um;
-    if (cand) {
-      const double r = e2_rank(sh, i, lane, um, Gu);
-      const long long key = (long long)i * Pp + lane;
-      if (better(r, key, pr, pk)) { pr = r; pk = key; }
-    }
+    const uint64_t cb = __ballot(cand);
+    if (cand) sh.cand[nc + __popcll(cb & below)] = (unsigned short)(i | (lane << 8));
+    nc += __popcll(cb);
+  }
+  __syncthreads();
+  // pass 1: the best candidate pair by (rank, pair index)
+  double pr = -__builtin_inf();
+  long long pk = -1;
+  for (int q = lane; q < nc; q += 64) {
+    const int i = sh.cand[q] & 0xFF, j = sh.cand[q] >> 8;
+    const double r = e2_rank(sh, i, j, um, Gu);
+    const long long key = (long long)i * Pp + j;
+    if (better(r, key, pr, pk)) { pr = r; pk = key; }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -1096,15 +1105,15 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
     int n_in = 0;
     bool all_ok = true, all_same = true;
     uint64_t b1 = 0, b2 = 0;
-    for (int i = 0; i + 1 < Pp; ++i) {
-      const bool cand = lane > i && lane < Pp && (sh.pm[i] | my_pm) == um;
-      if (cand && (pr - e2_rank(sh, i, lane, um, Gu)) <= P.range) {
-        const E2Eval e = e2_eval(K, sh, i, lane, um);
+    for (int q = lane; q < nc; q += 64) {
+      const int i = sh.cand[q] & 0xFF, j = sh.cand[q] >> 8;
+      if ((pr - e2_rank(sh, i, j, um, Gu)) <= P.range) {
+        const E2Eval e = e2_eval(K, sh, i, j, um);
         ++n_in;
         all_ok = all_ok && e.ok;
         all_same = all_same && e.mm == be.mm && e.mA == be.mA && e.mB == be.mB;
-        b1 |= 1ull << (e.swapped ? lane : i);
-        b2 |= 1ull << (e.swapped ? i : lane);
+        b1 |= 1ull << (e.swapped ? j : i);
+        b2 |= 1ull << (e.swapped ? i : j);
       }
     }
 #pragma unroll

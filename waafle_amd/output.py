@@ -41,6 +41,24 @@ def _tails(tax, ids, lca_id):
     return "; ".join(sorted(items))
 
 
+def _annotation_fields(batch, res, bit, nsys):
+    """Per contig: the ANNOTATIONS:<SYSTEM> field of system `bit` -- each locus's winning
+    hit's value (orgscorer.py:384-392, 790-800) or "None", joined by "|" -- built with one
+    table lookup per distinct value instead of one per locus."""
+    L = batch.n_loci
+    hits = res.annot_hit.reshape(-1, nsys)[:, bit] if L else np.zeros(0, np.int32)
+    vid = np.full(L, -1, dtype=np.int64)
+    m = hits >= 0
+    if m.any():
+        vid[m] = batch.annot_value_ids[hits[m], bit]
+    table = batch.annot_values[bit]
+    text = {int(i): table[int(i)] for i in np.unique(vid[m])} if m.any() else {}
+    text[-1] = MISSING
+    per_locus = [text[i] for i in vid.tolist()]
+    lo = batch.loc_off.tolist()
+    return [_e("|".join(per_locus[lo[c]:lo[c + 1]])) for c in range(batch.n_contigs)]
+
+
 def render(batch, tax, res):
     """-> {kind: [header, row, ...]} (tab-joined strings)."""
     N = batch.n_contigs
@@ -53,48 +71,63 @@ def render(batch, tax, res):
     for kind, cols in FORMATS.items():
         hdr = cols + [ANNOT_PREFIX + batch.systems[b] for b in used_bits]
         out[kind] = ["\t".join(c.upper() for c in hdr)]
-    lo = batch.loc_off
-    ho = batch.hit_off
+    lo = batch.loc_off.tolist()
+    ho = batch.hit_off.tolist()
     names = batch.contig_names
-    for c in sorted(range(N), key=lambda i: names[i]):
-        l0, l1 = int(lo[c]), int(lo[c + 1])
-        loci = _e(batch.loci_fields[c] if batch.loci_fields is not None
-                  else "|".join(batch.loc_codes[l0:l1]))
-        call = int(res.call[c])
-        length = str(int(batch.contig_lengths[c]))
+    calls = res.call.tolist()
+    crit, rank = res.crit.tolist(), res.rank.tolist()
+    c1s, c2s = res.clade1.tolist(), res.clade2.tolist()
+    nm1s, nm2s = res.n_meld1.tolist(), res.n_meld2.tolist()
+    dirs = res.direction.tolist()
+    lengths = batch.contig_lengths.tolist()
+    syn = res.synteny.tobytes().decode("latin-1")
+    meld = res.meld
+    fields = batch.loci_fields
+    codes = batch.loc_codes
+    ann = [_annotation_fields(batch, res, b, nsys) for b in used_bits]
+    tnames = tax.names
+    lin_cache, tail_cache = {}, {}
+
+    def lin(i):
+        s = lin_cache.get(i)
+        if s is None:
+            s = lin_cache[i] = _e("|".join(tax.lineage(i)))
+        return s
+
+    def tails(ids, c):
+        key = (c, tuple(sorted(ids.tolist())))
+        s = tail_cache.get(key)
+        if s is None:
+            s = tail_cache[key] = _e(_tails(tax, ids, c))
+        return s
+
+    lgt, no_lgt, uncl = out["lgt"], out["no_lgt"], out["unclassified"]
+    for c in sorted(range(N), key=names.__getitem__):
+        l0, l1 = lo[c], lo[c + 1]
+        loci = _e(fields[c] if fields is not None else "|".join(codes[l0:l1]))
+        call = calls[c]
+        length = str(lengths[c])
         if call == CALL_NO_LGT:
-            kind = "no_lgt"
-            c1 = int(res.clade1[c])
-            mbase = 2 * int(ho[c]) + 2 * c
-            meld = res.meld[mbase:mbase + int(res.n_meld1[c])]
-            vals = [names[c], "no_lgt", length, _f(res.crit[c]), _f(res.rank[c]),
-                    _e(res.synteny[l0:l1].tobytes().decode()), _e(tax.names[c1]),
-                    _e(_tails(tax, meld, c1)), _e("|".join(tax.lineage(c1))), loci]
+            c1 = c1s[c]
+            mbase = 2 * ho[c] + 2 * c
+            vals = [names[c], "no_lgt", length, _f(crit[c]), _f(rank[c]), _e(syn[l0:l1]),
+                    _e(tnames[c1]), tails(meld[mbase:mbase + nm1s[c]], c1), lin(c1), loci]
+            dest = no_lgt
         elif call == CALL_LGT:
-            kind = "lgt"
-            a, b = int(res.clade1[c]), int(res.clade2[c])
-            mbase = 2 * int(ho[c]) + 2 * c
-            n1, n2 = int(res.n_meld1[c]), int(res.n_meld2[c])
-            m1 = res.meld[mbase:mbase + n1]
-            m2 = res.meld[mbase + n1:mbase + n1 + n2]
-            vals = [names[c], "lgt", length, _f(res.crit[c]), _f(res.rank[c]),
-                    _e(res.synteny[l0:l1].tobytes().decode()),
-                    "B>A" if res.direction[c] else "A?B", _e(tax.names[a]), _e(tax.names[b]),
-                    _e(tax.lca([a, b])), _e(_tails(tax, m1, a)), _e(_tails(tax, m2, b)),
-                    _e("|".join(tax.lineage(a))), _e("|".join(tax.lineage(b))), loci]
+            a, b = c1s[c], c2s[c]
+            mbase = 2 * ho[c] + 2 * c
+            n1, n2 = nm1s[c], nm2s[c]
+            vals = [names[c], "lgt", length, _f(crit[c]), _f(rank[c]), _e(syn[l0:l1]),
+                    "B>A" if dirs[c] else "A?B", _e(tnames[a]), _e(tnames[b]),
+                    _e(tax.lca([a, b])), tails(meld[mbase:mbase + n1], a),
+                    tails(meld[mbase + n1:mbase + n1 + n2], b), lin(a), lin(b), loci]
+            dest = lgt
         else:
-            kind = "unclassified"
             vals = [names[c], "unclassified", length, loci]
-        for bit in used_bits:
-            items = []
-            for l in range(l0, l1):
-                h = int(annot[l, bit])
-                if h < 0:
-                    items.append(MISSING)
-                else:
-                    items.append(batch.annot_values[bit][int(batch.annot_value_ids[h, bit])])
-            vals.append(_e("|".join(items)))
-        out[kind].append("\t".join(vals))
+            dest = uncl
+        for col in ann:
+            vals.append(col[c])
+        dest.append("\t".join(vals))
     return out
 
 
