@@ -19,10 +19,13 @@ def main():
     for r in csv.DictReader(open(files[0])):
         m = re.search(r"(k_\w+(<[^>]*>)?)", r["Kernel_Name"])
         acc[m.group(1) if m else r["Kernel_Name"][:30]][r["Counter_Name"]] += float(r["Counter_Value"])
-    print("rocprofv3 --pmc " + " ".join(COLS) + " summed over the 4 passes (1 warmup + 3 timed) of (" + d + ")")
-    print("%-24s" % "kernel" + "".join("%20s" % c for c in COLS))
-    for k, v in sorted(acc.items(), key=lambda x: -x[1]["SQ_WAVE_CYCLES"])[:14]:
-        print("%-24s" % k[:24] + "".join("%20.4g" % v[c] for c in COLS))
+    seen = sorted({c for v in acc.values() for c in v})
+    cols = [c for c in COLS if c in seen] or seen        # (another counter group: its own columns)
+    key = cols[0] if "SQ_WAVE_CYCLES" not in cols else "SQ_WAVE_CYCLES"
+    print("rocprofv3 --pmc " + " ".join(cols) + " summed over the 4 passes (1 warmup + 3 timed) of (" + d + ")")
+    print("%-30s" % "kernel" + "".join("%22s" % c for c in cols))
+    for k, v in sorted(acc.items(), key=lambda x: -x[1][key])[:16]:
+        print("%-30s" % k[:30] + "".join("%22.4g" % v[c] for c in cols))
 
 
 if __name__ == "__main__":

@@ -14,9 +14,11 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+# (laps 7, 11, 14: the closed-form one-run means; 12, 13: the multi-attachment means --
+# wave per segment, lane per segment or leaf per lane; 32-35 the explain_one split)
 PHASES = ["loci+lut", "hits/attach", "annotations", "sort", "segments", "prune setup",
-          "pass select", "means", "post-pass/explain_one", "dump/level end", "record/end",
-          "means lane p6", "means multi p0", "means multi p1/7/6", "means lane p1/7/2",
+          "pass select", "one-run means p0", "post-pass", "dump/level end", "record/end",
+          "one-run means p6", "multi means p0", "multi means p1/7/6/2/4/5", "one-run means p1/7/2/4/5",
           "means prep (all passes)"]
 STATS = {16: "contigs", 17: "attachments", 18: "segments", 19: "pass iterations",
          20: "segments listed", 21: "dumps", 22: "handed on", 23: "hits"}
@@ -55,7 +57,7 @@ def main():
     st = (C.c_ulonglong * 48)()
     so.wf_stamps_read_fast(st, 48)
     v = [int(x) for x in st]
-    tot = sum(v[:16])
+    tot = sum(v[:16]) + sum(v[32:36])                # (the explain_one laps are their own)
     nc = max(1, v[16])
     out = {"config": args.config, "contigs": n, "flags": args.flags, "sampled": v[16],
            "cycles_per_contig": tot / nc,

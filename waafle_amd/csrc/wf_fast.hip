@@ -39,9 +39,15 @@
 #define WF_LANE_MEANS6 0
 #endif
 // 1: every hit batch of a round finds its loci before the first takes its slots (the loci
-// searches of the batches overlap); 0: batch by batch (A/B variant)
+// searches of the batches overlap); 0: batch by batch.  Same-box A/B at cfg4 (r4c): 0 is
+// 0.15 ms faster per pass (the batched form's registers spill), so 0 is the default.
+// roll-up levels: multi-attachment segment means one numpy leaf per lane (flat_leaf_means);
+// 0: one segment per lane (lane_seg_mean)
+#ifndef WF_FLAT_LEAVES
+#define WF_FLAT_LEAVES 1
+#endif
 #ifndef WF_ATTACH_BATCHED
-#define WF_ATTACH_BATCHED 1
+#define WF_ATTACH_BATCHED 0
 #endif
 
 namespace wf {
@@ -273,6 +279,62 @@ __device__ __noinline__ double lane_seg_mean(SliceSrc src, int kb, int ke, LT lt
     for (int a = 0; a < e.z; ++a) stk.add_top();
   }
   return (0.0 + stk.s0) / (double)len;
+}
+
+// Exact means of the multi-attachment segments of one 64-segment chunk (lanes of `mlist`,
+// each with its segment's sorted attachments [kb, ke), leaf count nl <= 64, locus length
+// len and packed leaf table lut), one numpy LEAF per lane rather than one segment per lane:
+// whole segments are packed into rounds of at most 64 leaves (a lane-order prefix sum of
+// nl), lane i of a round evaluates leaf i - start of the segment whose leaves start at or
+// below it (SegAttT::leaf, as lane_seg_mean), and the segment's own lane folds its leaves in
+// tree order (SumStack) from W.lv.  Same leaf values, same fold, so the same bits as
+// lane_seg_mean; a round costs one leaf per lane instead of a whole segment.  W.z maps a
+// round's start position to its segment's lane.  Returns the mean on the segment's lane.
+template <int R>
+__device__ __noinline__ double flat_leaf_means(SliceSrc src, const uint32_t* lut, uint64_t mlist, int kb, int ke,
+                                               int nl, int len, WaveRunsT<R>& W) {
+  const int lane = lane_id();
+  double mean = 0.0;
+  for (uint64_t rem = mlist; rem;) {
+    const bool mine = (rem >> lane) & 1ull;
+    const int my_nl = mine ? nl : 0;
+    int total = 0;
+    const int start = wave_excl_scan_dpp(my_nl, &total);
+    const bool take = mine && start + my_nl <= 64;
+    const uint64_t tk = __ballot(take);
+    if (take) W.z[start] = lane;
+    const uint64_t starts = wave_or_dpp(take ? 1ull << start : 0ull);
+    const int last = 63 - __clzll(tk);
+    const int used = lane_bcast(start + my_nl, last);  // leaves of this round
+    wave_sync();
+    const uint64_t le = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
+    const uint64_t st_le = starts & le;
+    const int p = st_le ? 63 - __clzll(st_le) : 0;
+    const int own = lane < used ? W.z[p] : last;
+    // the owner's segment (all lanes active for the permutes)
+    const int okb = __shfl(kb, own, 64), oke = __shfl(ke, own, 64);
+    const uintptr_t olut = (uintptr_t)__shfl((long long)(uintptr_t)lut, own, 64);
+    if (lane < used) {
+      const int4 e = PackedLut{reinterpret_cast<const uint32_t*>(olut)}(lane - p);
+      SegAttT<SliceSrc> at;
+      at.load(src, okb, oke);
+      W.lv[lane] = at.leaf(src, e.x, e.y);
+    }
+    wave_sync();
+    if (take) {
+      SumStack stk;
+      const PackedLut lt{lut};
+      for (int q = 0; q < nl; ++q) {
+        stk.push(W.lv[start + q]);
+        const int z = lt(q).z;
+        for (int a = 0; a < z; ++a) stk.add_top();
+      }
+      mean = (0.0 + stk.s0) / (double)len;
+    }
+    wave_sync();                                      // (W.lv, W.z: the next round's)
+    rem &= ~tk;
+  }
+  return mean;
 }
 
 // Contig.score of the clade run starting at segment t (orgscorer.py:447-461): crit = min
@@ -1116,9 +1178,17 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
           if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
           WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));
           uint64_t mlist = __ballot(multi);
-          if ((FULL || ROLL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
-            // several multi-attachment segments (roll-up levels, where a segment gathers the
-            // attachments of many clades): one lane each, not the whole wave per segment
+          if (ROLL && WF_FLAT_LEAVES && mlist != 0ull) {
+            // roll-up levels, where a segment gathers the attachments of many clades: one
+            // numpy leaf per lane over all of the chunk's multi-attachment segments
+            int kb = 0, ke = 0;
+            if (multi) { kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att; }
+            const double m = flat_leaf_means(SliceSrc{F.key, F.lohi, F.sc}, F.lut + F.lbase[multi ? g : 0], mlist,
+                                             kb, ke, nl, len, F.runs());
+            if (multi) v[s] = m;
+            mlist = 0;
+          } else if ((FULL || ROLL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
+            // several multi-attachment segments: one lane each, not the whole wave per segment
             if (multi) {
               const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
               v[s] = lane_seg_mean(SliceSrc{F.key, F.lohi, F.sc}, kb, ke, PackedLut{F.lut + F.lbase[g]}, nl, len);

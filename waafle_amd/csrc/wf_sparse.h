@@ -872,13 +872,18 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
 // threshold: the pair's other clade is removed with one bit operation (sp_sisters'
 // saturating counts, restated for one parent per clade).
 struct E2Shared {
-  int2 cg[kE2Seg];                           // (clade, locus), clade then locus order
+  union {                                    // (9,920 bytes in all: 16 waves per CU)
+    struct {                                 // the scans of the table ...
+      int2 cg[kE2Seg];                       // (clade, locus), clade then locus order
+      unsigned long long pm[64];             // potential clade i: ">= k2" on unmasked loci
+    };
+    unsigned short cand[64 * 63 / 2];        // ... then the candidate pairs i | j << 8 (i < j)
+  };
   double v[kE2Seg];                          // gene score
   int t[64], cl[64], par[64], sibp[64];      // potential clade i: run start, clade, parent,
                                              // listed parent
-  unsigned long long pres[64], pm[64], hm[64], s1[64], s2[64];
+  unsigned long long pres[64], hm[64], s1[64], s2[64];
   int len[64];                               // locus lengths (ambiguous fraction)
-  unsigned short cand[64 * 63 / 2];          // candidate pairs i | j << 8 (i < j)
 };
 
 // S[row][g] (0.0 without a segment)
@@ -977,14 +982,13 @@ __device__ __forceinline__ int e2_wave_lca(const KArgs& K, int acc) {
 // One compact slot (table [so, se), contig c, the roll-up level): writes the contig's
 // result or its roll-up bookkeeping (as sp_level).  False: the table breaks the compact
 // form's limits (the dense decision takes the contig; never expected).
-__device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int so, int se, uint64_t hdr, int level) {
+// (h0, l0, G: the contig's hit and locus offsets and locus count, loaded with the slot)
+__device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int so, int se, uint64_t hdr,
+                                       int64_t h0, int64_t l0, int G, int level) {
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const int lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
-  const int64_t h0 = K.hit_off[c];
-  const int64_t l0 = K.loc_off[c];
-  const int G = (int)(K.loc_off[c + 1] - l0);
   const int ns = se - so;
   if (G > kE2MaxG || ns > kE2Seg) return false;
   const uint64_t um = hdr & ~(1ull << 63);
@@ -1035,6 +1039,7 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
   }
   if (Pp > 64) return false;
   __syncthreads();
+  const uint64_t my_pm = lane < Pp ? sh.pm[lane] : 0ull;   // (cand overwrites pm and cg)
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
   if (P.sister_on) {
     // per potential clade, the present clades listed under its parent (itself excluded) at
@@ -1074,10 +1079,10 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
   }
   // the candidate pairs, crit >= k2 <=> (m_i | m_j) == um, listed so that their ranks are
   // taken 64 at a time (one pair per lane) rather than one potential clade per step
-  const uint64_t my_pm = lane < Pp ? sh.pm[lane] : 0ull;
+  __syncthreads();                                   // (every read of cg done)
   int nc = 0;
   for (int i = 0; i + 1 < Pp; ++i) {
-    const bool cand = lane > i && lane < Pp && (sh.pm[i] | my_pm) == um;
+    const bool cand = lane > i && lane < Pp && (lane_bcast(my_pm, i) | my_pm) == um;
     const uint64_t cb = __ballot(cand);
     if (cand) sh.cand[nc + __popcll(cb & below)] = (unsigned short)(i | (lane << 8));
     nc += __popcll(cb);
@@ -1227,49 +1232,84 @@ __global__ __launch_bounds__(64) void k_big_sparse(const SArgs S, int level, int
 
 // Level 0 of the contigs the first wave form handed over with their segment tables
 // (S.dump_*: slot i holds entries [dump_first[i], dump_first[i + 1]) of contig
-// dump_list[2 i + 1]).  S.seed_pend / ccnt / cleaves: decided -> pend 0 and no staged
+// dump_list[2 i + 1], dump_list[2 i] its form: 1 compact (explain_two only, sp_two), 0 the
+// whole table (sp_level)).  S.seed_pend / ccnt / cleaves: decided -> pend 0 and no staged
 // attachments; raised -> pend 2 (level-1 seed); declined (> 63 loci, class or pair tables
 // outgrown) -> pend 1, the staged kernels take level 0.
 //
 // Wave levels (S.roll_next set): level `level` of the contigs the first form handed over at
-// that level; a raised contig is appended to the next level's list.  The kernel also sets up
-// the next level: its table counter (S.dump_ctr_next) and the ancestors one level up
-// (S.anc: parent^(jump + level + 1) of every name; k_wave of this level is done with them).
-__global__ __launch_bounds__(64) void k_dump_sparse(const SArgs S, int64_t* ccnt, int64_t* cleaves, int level) {
-  constexpr size_t kShBytes = sizeof(SpShared) > sizeof(E2Shared) ? sizeof(SpShared) : sizeof(E2Shared);
-  __shared__ __attribute__((aligned(16))) char sh_raw[kShBytes];
-  SpShared& sh = *reinterpret_cast<SpShared*>(sh_raw);
-  E2Shared& sh2 = *reinterpret_cast<E2Shared*>(sh_raw);
-  if (S.dump_ctr_next && blockIdx.x == 0 && threadIdx.x == 0) *S.dump_ctr_next = 0ull;
-  if (S.anc) {
-    const int up = level == 0 ? S.k.p.jump + 1 : 1;
-    for (int t = blockIdx.x * 64 + threadIdx.x; t < S.n_tax; t += gridDim.x * 64) {
-      int x = level == 0 ? t : S.anc[t];
-      for (int j = 0; j < up; ++j) x = S.k.parent[x];
-      S.anc[t] = x;
-    }
-  }
-  char* ws = S.sp_ws + (int64_t)blockIdx.x * kSpSlot;
-  const int count = (int)(*S.dump_ctr >> 40);
-  for (int i = blockIdx.x; i < count; i += gridDim.x) {
-    const int c = S.dump_list[2 * i + 1];
-    if (c < 0) continue;                             // (its table did not fit: pend 1 stands)
-    const bool ok = S.dump_list[2 * i] == 1
-                        ? sp_two(S, sh2, c, S.dump_first[i], S.dump_first[i + 1], S.dump_um[i], level)
-                        : sp_level(S, sh, ws, c, i, level, 1);
-    if (threadIdx.x == 0) {
-      const int pd = S.seed_pend[c];
-      if (!ok) {
-        S.seed_pend[c] = 1;
-        if (S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);
-      } else if (pd == 3) {
-        S.seed_pend[c] = 0;
-        ccnt[c] = 0;
-        cleaves[c] = 0;
-      } else if (pd == 2 && S.roll_next) {
-        S.roll_next[atomicAdd(S.roll_next_n, 1ull)] = c;
+// that level; a raised contig is appended to the next level's list.  The compact kernel
+// (launched first) also sets up the next level: its table counter (S.dump_ctr_next) and the
+// ancestors one level up (S.anc: parent^(jump + level + 1) of every name; k_wave of this
+// level is done with them, and neither decision body reads them).
+//
+// KIND 1 takes the compact slots, KIND 0 the whole tables: two kernels, so that sp_two's
+// smaller register file gives it twice the resident waves of sp_level.  A wave reads the
+// headers of 64 of its slots (stride gridDim.x, as one slot per step would) at once.
+template <int KIND>
+__global__ __launch_bounds__(64, KIND ? 4 : 2) void k_dump_sparse(const SArgs S, int64_t* ccnt, int64_t* cleaves,
+                                                                  int level) {
+  using Sh = typename std::conditional<KIND == 1, E2Shared, SpShared>::type;
+  __shared__ Sh sh;
+  const int lane = threadIdx.x & 63;
+  if (KIND == 1) {
+    if (S.dump_ctr_next && blockIdx.x == 0 && lane == 0) *S.dump_ctr_next = 0ull;
+    if (S.anc) {
+      const int up = level == 0 ? S.k.p.jump + 1 : 1;
+      for (int t = blockIdx.x * 64 + lane; t < S.n_tax; t += gridDim.x * 64) {
+        int x = level == 0 ? t : S.anc[t];
+        for (int j = 0; j < up; ++j) x = S.k.parent[x];
+        S.anc[t] = x;
       }
     }
-    __syncthreads();
+  }
+  char* ws = KIND ? nullptr : S.sp_ws + (int64_t)blockIdx.x * kSpSlot;
+  const int count = (int)(*S.dump_ctr >> 40);
+  const int stride = (int)gridDim.x;
+  for (int base = blockIdx.x; base < count; base += 64 * stride) {
+    const int my = base + lane * stride;
+    int mc = -1, so = 0, se = 0, G = 0;
+    uint64_t hdr = 0;
+    int64_t h0 = 0, l0 = 0;
+    if (my < count) {
+      const int2 dl = reinterpret_cast<const int2*>(S.dump_list)[my];
+      if (dl.x == KIND && dl.y >= 0) {               // (c < 0: its table did not fit, pend 1 stands)
+        mc = dl.y;
+        if (KIND == 1) {
+          so = S.dump_first[my];
+          se = S.dump_first[my + 1];
+          hdr = S.dump_um[my];
+          h0 = S.k.hit_off[mc];
+          l0 = S.k.loc_off[mc];
+          G = (int)(S.k.loc_off[mc + 1] - l0);
+        }
+      }
+    }
+    for (uint64_t m = __ballot(mc >= 0); m; m &= m - 1) {
+      const int src = __builtin_ctzll(m);
+      const int c = lane_bcast(mc, src);
+      bool ok;
+      if constexpr (KIND == 1) {
+        ok = sp_two(S, sh, c, lane_bcast(so, src), lane_bcast(se, src), lane_bcast(hdr, src),
+                    (int64_t)lane_bcast((uint64_t)h0, src), (int64_t)lane_bcast((uint64_t)l0, src),
+                    lane_bcast(G, src), level);
+      } else {
+        ok = sp_level(S, sh, ws, c, base + src * stride, level, 1);
+      }
+      if (lane == 0) {
+        const int pd = S.seed_pend[c];
+        if (!ok) {
+          S.seed_pend[c] = 1;
+          if (S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);
+        } else if (pd == 3) {
+          S.seed_pend[c] = 0;
+          ccnt[c] = 0;
+          cleaves[c] = 0;
+        } else if (pd == 2 && S.roll_next) {
+          S.roll_next[atomicAdd(S.roll_next_n, 1ull)] = c;
+        }
+      }
+      __syncthreads();
+    }
   }
 }

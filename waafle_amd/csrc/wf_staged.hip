@@ -1238,6 +1238,7 @@ struct StagedState {
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
   int sparse_big = 3;                // WF_OPT_SPARSE_BIG (0 dense, 1 overflow, 2 all, 3 decisions)
   int sparse_res = -1;               // resident k_big_sparse waves per CU
+  int two_res = -1;                  // resident k_dump_sparse<1> (compact tables) waves per CU
   int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
   int wave_two = 1;                  // WF_OPT_WAVE_TWO: explain_two + roll-up levels in the wave form
   int64_t dump_cap = 0;              // WF_OPT_DUMP_CAP (0: max(32 N, 65536))
@@ -1549,19 +1550,26 @@ __global__ void k_rekey_seeds(const int32_t* list, int n, const int64_t* catt_of
 // k_dump_sparse: the same sp_level body) from the kernel's own VGPR and LDS use (the
 // occupancy query returned 4 here: SQ_WAVES of the round-3 cfg5 profile): waves per SIMD =
 // 512 / VGPRs (granule 8, at most 8), 4 SIMDs; LDS 160 KB per CU
-static int sparse_waves(StagedState* st) {
-  if (st->sparse_res < 0) {
-    hipFuncAttributes fa{};
-    int b = 8;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_big_sparse)) == hipSuccess) {
-      const int vg = std::max(8, (fa.numRegs + 7) & ~7);
-      const int by_vgpr = 4 * std::min(8, 512 / vg);
-      const int by_lds = (int)((160 * 1024) / std::max<size_t>(1, fa.sharedSizeBytes));
-      b = std::max(1, std::min(by_vgpr, by_lds));
-    }
-    st->sparse_res = b;
+static int resident_waves(const void* fn) {
+  hipFuncAttributes fa{};
+  int b = 8;
+  if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
+    const int vg = std::max(8, (fa.numRegs + 7) & ~7);
+    const int by_vgpr = 4 * std::min(8, 512 / vg);
+    const int by_lds = (int)((160 * 1024) / std::max<size_t>(1, fa.sharedSizeBytes));
+    b = std::max(1, std::min(by_vgpr, by_lds));
   }
+  return b;
+}
+
+static int sparse_waves(StagedState* st) {
+  if (st->sparse_res < 0) st->sparse_res = resident_waves(reinterpret_cast<const void*>(&k_big_sparse));
   return st->sparse_res;
+}
+
+static int two_waves(StagedState* st) {
+  if (st->two_res < 0) st->two_res = resident_waves(reinterpret_cast<const void*>(&k_dump_sparse<1>));
+  return st->two_res;
 }
 
 template <class It>
@@ -1689,7 +1697,11 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         da.anc = st->anc.as<int32_t>();               // (k_dump_sparse: ancestors of level 1)
         da.dump_ctr_next = da.dump_ctr + 1;
       }
-      hipLaunchKernelGGL(k_dump_sparse, dim3(grid), dim3(64), 0, s, da, st->cnt.as<int64_t>(),
+      const int grid2 = st->cus * two_waves(st);
+      if (levels)                                       // compact tables (and the level set-up)
+        hipLaunchKernelGGL(k_dump_sparse<1>, dim3(grid2), dim3(64), 0, s, da, st->cnt.as<int64_t>(),
+                           st->cnt_leaves.as<int64_t>(), 0);
+      hipLaunchKernelGGL(k_dump_sparse<0>, dim3(grid), dim3(64), 0, s, da, st->cnt.as<int64_t>(),
                          st->cnt_leaves.as<int64_t>(), 0);
       ST_TRY(hipGetLastError());
       const int t_h1 = t_mark(st, s);
@@ -1713,7 +1725,9 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
             la.roll_next_n = rcnt + L + 1;
             ST_TRY(launch_level(la, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                                 roll[L & 1], reinterpret_cast<const int64_t*>(rcnt + L), L, max_hits, st->cus, s));
-            hipLaunchKernelGGL(k_dump_sparse, dim3(grid), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
+            hipLaunchKernelGGL(k_dump_sparse<1>, dim3(grid2), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
+                               st->cnt_leaves.as<int64_t>(), L);
+            hipLaunchKernelGGL(k_dump_sparse<0>, dim3(grid), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
                                st->cnt_leaves.as<int64_t>(), L);
             ST_TRY(hipGetLastError());
           }
