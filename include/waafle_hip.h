@@ -55,10 +55,10 @@ enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
  *   3 (default): explain_one by one wave per contig (k_one), and every contig it leaves
  *   open (explain_two, more segments than its LDS holds, --weak-loci assign-unknown) takes
  *   the decision straight from the segment table, one wave per contig (k_big_sparse);
- *   1: only contigs whose gene-score matrix outgrows the LDS arena go there, the others
- *   to the dense workgroup decision; 0: the dense matrix, in an HBM slot when it outgrows
- *   the arena (the only form for > 63 loci); 2: every staged decision in the segment-table
- *   form (a test setting: it exercises that form on every input).
+ *   2: every staged decision in the segment-table form (a test setting: it exercises that
+ *   form on every input).  The dense matrix decision remains for > 63 loci and for a table
+ *   the segment-table form declines (its class or pair tables outgrown).  The values 0 and 1
+ *   (dense decisions for <= 63 loci) are retired: WF_E_BADINPUT.
  * WF_OPT_ATT_LIMIT: hit-locus attachments one wf_score call accepts (default and maximum
  *   2^31 - 1; more -> WF_E_TOOBIG, nothing scored).
  * WF_OPT_WAVE_TWO (WF_MODE_LEVEL0): 1 (default) the first wave form also decides explain_two

@@ -36,10 +36,8 @@ FORMS = {
     "staged": dict(mode="staged"),
     # every staged decision from the segment table (k_big_sparse, wf_sparse.h)
     "sparse": dict(mode="staged", options={lib.OPT_SPARSE_BIG: 2}),
-    # the dense workgroup decision, k_big_sparse only for contigs outgrowing its arena
-    "overflow": dict(mode="staged", options={lib.OPT_SPARSE_BIG: 1}),
-    # every staged decision that outgrows a 4 KB arena in an HBM slot (k_decide_big)
-    "dense_big": dict(mode="staged", lds_bytes=4096, options={lib.OPT_SPARSE_BIG: 0}),
+    # a 4 KB dense arena: the > 63-loci decisions that outgrow it in an HBM slot (k_decide_big)
+    "small_arena": dict(mode="staged", lds_bytes=4096),
 }
 
 
@@ -50,8 +48,21 @@ def scorer(request):
     staged kernels, and those with every decision in the segment-table form or in the
     dense HBM-slot form."""
     s = engine.GpuScorer(0, **FORMS[request.param])
+    s.form = request.param
     yield s
     s.close()
+
+
+# The oracle's results per case, computed once for all forms (the CPU oracle, not the GPU,
+# is most of this module's time): case key -> Results
+_ORACLE = {}
+
+
+def oracle_for(key, paths, flags, batch, tax):
+    if key not in _ORACLE:
+        contigs, _ = run_oracle(paths, list(flags))
+        _ORACLE[key] = oracle_results(contigs, batch, tax)
+    return _ORACLE[key]
 
 
 def gpu_score(scorer, batch, tax, flags):
@@ -127,8 +138,7 @@ def test_gpu_matches_goldens_and_oracle(name, scorer, tmp_path):
     assert_matches_dump(fx, batch, res)
     if name in gc.HEAVY:       # cfg5 stress: the fixture is the only reference
         return
-    contigs, _ = run_oracle(paths, fx["flags"])
-    want = oracle_results(contigs, batch, tax)
+    want = oracle_for(("golden", name), paths, fx["flags"], batch, tax)
     assert_same_results(res, want, batch)
 
 
@@ -149,6 +159,8 @@ def test_gpu_deep_taxonomy_and_runaway(name, scorer, tmp_path):
         gpu_score(scorer, batch, tax, fx["flags"])
     assert exc.value.code == lib.WF_E_RUNAWAY
     assert batch.contig_names[int(exc.value.contigs[0])] in fx["stderr"]
+    if scorer.form != "level0":   # the CLI runs the default form: once
+        return
     cmd = [sys.executable, "-m", "waafle_amd.orgscorer"] + paths + \
           ["--outdir", str(tmp_path), "--quiet"] + fx["flags"]
     run = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
@@ -159,13 +171,20 @@ def test_gpu_deep_taxonomy_and_runaway(name, scorer, tmp_path):
     assert run.stderr.strip().splitlines()[-2:] == want
 
 
+_SYNTH = {}
+
+
 def synth_case(tmp_path, flags=(), **kw):
-    data = synth.generate(**kw)
-    paths = synth.write_text(data, str(tmp_path), "s")
-    args = cli.parse_flags(list(flags))
-    batch, tax = inputs.load_inputs(*paths, args.min_gene_length, warn=None)
-    contigs, _ = run_oracle(paths, list(flags))
-    return batch, tax, oracle_results(contigs, batch, tax)
+    """(batch, taxonomy, oracle results) of a synthetic case, built once for all forms."""
+    key = (tuple(sorted(kw.items())), tuple(flags))
+    if key not in _SYNTH:
+        data = synth.generate(**kw)
+        paths = synth.write_text(data, str(tmp_path), "s")
+        args = cli.parse_flags(list(flags))
+        batch, tax = inputs.load_inputs(*paths, args.min_gene_length, warn=None)
+        contigs, _ = run_oracle(paths, list(flags))
+        _SYNTH[key] = (batch, tax, oracle_results(contigs, batch, tax))
+    return _SYNTH[key]
 
 
 @pytest.mark.parametrize("kw,flags", [
@@ -205,8 +224,7 @@ def test_long_locus_uses_numpy_buffered_sum(scorer, tmp_path):
     for flags in ([], ["-k1", "0.95", "-k2", "0.9"]):
         batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
         got = gpu_score(scorer, batch, tax, flags)
-        contigs, _ = run_oracle(paths, flags)
-        assert_same_results(got, oracle_results(contigs, batch, tax), batch)
+        assert_same_results(got, oracle_for(("long_locus",) + tuple(flags), paths, flags, batch, tax), batch)
 
 
 def test_empty_and_degenerate_contigs(scorer, tmp_path):
@@ -224,25 +242,27 @@ def test_empty_and_degenerate_contigs(scorer, tmp_path):
     for flags in ([], ["--weak-loci", "assign-unknown"], ["--weak-loci", "penalize"]):
         batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
         got = gpu_score(scorer, batch, tax, flags)
-        contigs, _ = run_oracle(paths, flags)
-        assert_same_results(got, oracle_results(contigs, batch, tax), batch)
+        assert_same_results(got, oracle_for(("degenerate",) + tuple(flags), paths, flags, batch, tax), batch)
 
 
-def test_full_size_cfg2_properties(scorer):
+def test_full_size_cfg2_properties():
     """BASELINE config 2 at full size: deterministic, shard-invariant, LDS-budget
-    invariant (forcing the HBM-workspace kernel), and equal to the oracle on a sample."""
+    invariant (forcing the HBM-workspace kernel), equal across every execution form, and
+    equal to the oracle on a sample.  (Not per form: it builds every form itself.)"""
     data = synth.generate_config("cfg2")
     batch, tax = synth.to_batch(data)
     params = cli.param_dict(cli.parse_flags([]))
+    scorer = engine.GpuScorer(0)
     scorer.set_taxonomy(tax)
     a = scorer.score(batch, params)
     b = scorer.score(batch, params)
     assert_same_results(a, b, batch)
     for kw in (dict(lds_bytes=8192),          # small decision arena: HBM decision slots
-               dict(lds_bytes=8192, options={lib.OPT_SPARSE_BIG: 0}),   # ... dense form only
                dict(mode="staged", options={lib.OPT_SPARSE_BIG: 2}),   # segment-table form
                dict(lds_bytes=65536),         # large arena: every contig in LDS
                dict(mode="staged"), dict(mode="level0"), dict(mode="waves"),
+               dict(options={lib.OPT_WAVE_TWO: 0}),      # round-3 hand-over flow
+               dict(options={lib.OPT_DUMP_CAP: 4096}),   # hand-over buffer overflow
                dict()):
         small = engine.GpuScorer(0, **kw)
         small.set_taxonomy(tax)
@@ -264,6 +284,7 @@ def test_full_size_cfg2_properties(scorer):
     contigs = orc.score_contigs(lengths, loci, hits, otax, opar)
     want = oracle_results(contigs, sub, tax)
     got = scorer.score(sub, params)
+    scorer.close()
     assert_same_results(got, want, sub)
 
 

@@ -138,7 +138,8 @@ def test_attachment_limit_splits_batch_like_unsplit():
 
 def test_option_validation():
     s = engine.GpuScorer(0)
-    for opt, val in ((lib.OPT_ATT_LIMIT, 0), (lib.OPT_ATT_LIMIT, 1 << 31), (lib.OPT_SPARSE_BIG, 4), (99, 1)):
+    for opt, val in ((lib.OPT_ATT_LIMIT, 0), (lib.OPT_ATT_LIMIT, 1 << 31), (lib.OPT_SPARSE_BIG, 4),
+                     (lib.OPT_SPARSE_BIG, 0), (lib.OPT_SPARSE_BIG, 1), (99, 1)):   # (0, 1: retired)
         assert s.lib.wf_set_option(s.h, opt, val) == lib.WF_E_BADINPUT
     s.close()
 
@@ -154,8 +155,8 @@ def test_cfg4_full_size(cfg4_full):
     """cfg4 at full size (1 M contigs, 210 M hits, one call): no contig errors, the same
     records on a second pass, from four cost-balanced shards, with a 16 KB decision arena
     (round 2: WF_DEC_LDS=16384 produced WF_E_EMPTYMASK at this shape), with the dense
-    workgroup decision for the contigs k_one leaves open, and with the dense HBM-slot decision
-    only; and the oracle's records on a 200-contig sample."""
+    workgroup decision's arena, with every staged decision in the segment-table form, and
+    with the round-3 hand-over flow; and the oracle's records on a 200-contig sample."""
     batch, tax = cfg4_full
     s = engine.GpuScorer(0)
     s.set_taxonomy(tax)
@@ -167,8 +168,8 @@ def test_cfg4_full_size(cfg4_full):
     parts = [s.score(batch.slice(x, y), PARAMS) for x, y in bounds]
     s.close()
     assert_same(engine.Results.concat(parts, [int(batch.hit_off[x]) for x, _ in bounds]), a, batch)
-    for kw in (dict(lds_bytes=16384), dict(options={lib.OPT_SPARSE_BIG: 1}),
-               dict(options={lib.OPT_SPARSE_BIG: 0})):
+    for kw in (dict(lds_bytes=16384), dict(options={lib.OPT_SPARSE_BIG: 2}),
+               dict(options={lib.OPT_WAVE_TWO: 0})):
         c = score(batch, tax, **kw)
         assert not c.status.any(), kw
         assert_same(c, a, batch)
@@ -180,7 +181,7 @@ def test_cfg4_full_size(cfg4_full):
 
 def test_cfg5_shard_and_embedded_fixture(tmp_path):
     """The cfg5 per-GPU share at 8 GPUs (6,250 stress contigs, ~31 M hits, 5,000 clades):
-    equal to its two halves and to the dense HBM-slot decision; the reference-generated
+    equal to its two halves and to the all-segment-table staged form; the reference-generated
     syn_cfg5 fixture contigs (same taxonomy) placed in front of the shard give the
     fixture's TSV rows."""
     batch, tax = synth.generate_batch("cfg5", 0, 6250)
@@ -191,8 +192,8 @@ def test_cfg5_shard_and_embedded_fixture(tmp_path):
     mid = 3125
     halves = [score(batch.slice(0, mid), tax), score(batch.slice(mid, 6250), tax)]
     assert_same(engine.Results.concat(halves, [0, int(batch.hit_off[mid])]), whole, batch)
-    dense = score(batch.slice(0, 400), tax, options={lib.OPT_SPARSE_BIG: 0})
-    assert_same(dense, slice_results(whole, batch, 0, 400), batch.slice(0, 400))
+    sparse = score(batch.slice(0, 400), tax, mode="staged", options={lib.OPT_SPARSE_BIG: 2})
+    assert_same(sparse, slice_results(whole, batch, 0, 400), batch.slice(0, 400))
     # the fixture's contigs in front of the shard
     fx = gc.load("syn_cfg5_default")
     paths = gc.materialize(fx, tmp_path)

@@ -115,8 +115,37 @@ def run_leaf(lo, hi, v, st, ln):
     return res
 
 
+def run_leaf_code(lo, hi, st, ln):
+    """wf_device.h run_leaf_code: (kmin, 2 bits per accumulator | tail << 16 | (m > 0) << 20)"""
+    m = ln >> 3; be = st + (m << 3)
+    hi = max(hi, lo)
+    def below(base, bound, m):
+        d = bound - base
+        return 0 if d <= 0 else min(m, (d + 7) >> 3)
+    k = [below(st + c, hi, m) - below(st + c, lo, m) for c in range(8)]
+    kmin = min([m] + k)
+    code = 0
+    for c in range(8):
+        code |= min(k[c] - kmin, 2) << (2 * c)
+    tail = max(0, min(st + ln, hi) - max(be, lo))
+    return kmin, code | (tail << 16) | ((1 << 20) if m > 0 else 0)
+
+
+def run_leaf_value(v, lc, s0):
+    kmin, code = lc
+    res = 0.0
+    if (code >> 20) & 1:
+        s1 = s0 + v; s2 = s1 + v
+        r = [(s0, s1, s2)[(code >> (2 * c)) & 3] for c in range(8)]
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+    for _ in range((code >> 16) & 15):
+        res += v
+    return res
+
+
 def pw_run_sum(n, lo, hi, v):
-    """Line-by-line restatement of wf_device.h pw_run_sum (bitmask bookkeeping, one ascent)."""
+    """Line-by-line restatement of wf_device.h pw_run_sum (integer walks, one seqsum chain
+    feeding the pair chain and the two boundary leaves, bitmask bookkeeping, one ascent)."""
     lo = max(lo, 0); hi = min(hi, n)
     if hi <= lo: return 0.0
     a0 = n >> 4; K = 0; m = n; sel = 0
@@ -137,28 +166,28 @@ def pw_run_sum(n, lo, hi, v):
         x = size >> 3; xl = x >> 1; Bt = a0 >> t
         return (s + 8 * xl, 8 * (x - xl), 1, (x - xl) - Bt, t + 1) if right else (s, 8 * xl, 1, xl - Bt, t + 1)
     s, size, kind, cls, t = 0, n, 0, 0, 0
-    mode = 0   # 0 split, 1 whole
+    mode = 0   # 0 two paths, 1 whole node, 2 one leaf
     while True:
         if lo <= s and hi >= s + size: mode = 1; break
-        if size <= 128: return run_leaf(lo, hi, v, s, size)
+        if size <= 128: mode = 2; break
         nl = 8 * (size >> 4) if kind == 0 else 8 * ((size >> 3) >> 1)
         if hi <= s + nl: s, size, kind, cls, t = child(s, size, kind, cls, t, False)
         elif lo >= s + nl: s, size, kind, cls, t = child(s, size, kind, cls, t, True)
         else: break
     ts = t
     W_t = t; W_kind = kind; W_cls = cls
-    # walks: per path (term depth, term type: 0 full spine, 1 full pair, 2 leaf), cls, value; ev bits
-    P = []
+    # paths: [term depth, term type (0 full spine, 1 full pair, 2 leaf), cls, ev, evk, evc, leaf]
+    P = [[0, 0, 0, 0, 0, 0, None], [0, 0, 0, 0, 0, 0, None]]
     if mode == 0:
-        for suffix in (True, False):
+        for i, suffix in enumerate((True, False)):
             s2, sz2, k2, c2, t2 = child(s, size, kind, cls, t, not suffix)
             ev = evk = evc = 0
             while True:
                 if (suffix and lo <= s2) or ((not suffix) and hi >= s2 + sz2):
-                    P.append([t2, 0 if k2 == 0 else 1, c2, 0.0, ev, evk, evc]); break
+                    P[i] = [t2, 0 if k2 == 0 else 1, c2, ev, evk, evc, None]; break
                 if sz2 <= 128:
-                    lv = run_leaf(lo, s2 + sz2, v, s2, sz2) if suffix else run_leaf(s2, hi, v, s2, sz2)
-                    P.append([t2, 2, 0, lv, ev, evk, evc]); break
+                    lc = run_leaf_code(lo, s2 + sz2, s2, sz2) if suffix else run_leaf_code(s2, hi, s2, sz2)
+                    P[i] = [t2, 2, 0, ev, evk, evc, lc]; break
                 L = child(s2, sz2, k2, c2, t2, False); R = child(s2, sz2, k2, c2, t2, True)
                 if suffix:
                     if lo < R[0]:
@@ -170,14 +199,26 @@ def pw_run_sum(n, lo, hi, v):
                         ev |= 1 << (t2 + 1); evc |= L[3] << (t2 + 1)
                         s2, sz2, k2, c2, t2 = R
                     else: s2, sz2, k2, c2, t2 = L
+    elif mode == 2:
+        P[0] = [0, 2, 0, 0, 0, 0, run_leaf_code(lo, hi, s, size)]
+    k0 = P[0][6][0] if P[0][1] == 2 else 0
+    k1 = P[1][6][0] if P[1][1] == 2 else 0
     mL = m if m < 8 else m >> 3
-    imax = max(xB, mL, 16 if need16 else 0)
-    tt = 0.0; sB = sC = sL = 0.0
+    imax = k0 if mode == 2 else max(xB, mL, 16 if need16 else 0, k0, k1)
+    tt = 0.0; sB = sC = sL = s0a = s0b = 0.0
     for i in range(1, imax + 1):
         tt += v
         if i == xB: sB = tt
         if i == xC: sC = tt
         if i == mL: sL = tt
+        if i == k0: s0a = tt
+        if i == k1: s0b = tt
+    lv = [0.0, 0.0]
+    if P[0][1] == 2:
+        lv[0] = run_leaf_value(v, P[0][6], s0a)
+    if mode == 2: return lv[0]
+    if P[1][1] == 2:
+        lv[1] = run_leaf_value(v, P[1][6], s0b)
     if m < 8: Rv = sL
     else:
         Rv = 8.0 * sL
@@ -200,9 +241,9 @@ def pw_run_sum(n, lo, hi, v):
             return Rv if W_kind == 0 else (q1 if W_cls else q0)
         if mode == 0:
             for i in (0, 1):
-                tu, ty, tc, lv, ev, evk, evc = P[i]
+                tu, ty, tc, ev, evk, evc, _ = P[i]
                 if u == tu:
-                    acc[i] = lv if ty == 2 else (Rv if ty == 0 else (q1 if tc else q0))
+                    acc[i] = lv[i] if ty == 2 else (Rv if ty == 0 else (q1 if tc else q0))
                 if u <= tu and (ev >> u) & 1:
                     sib = Rv if (evk >> u) & 1 else (q1 if (evc >> u) & 1 else q0)
                     acc[i] = acc[i] + sib if i == 0 else sib + acc[i]

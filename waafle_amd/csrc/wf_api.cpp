@@ -259,7 +259,8 @@ int wf_set_option(wf_ctx* ctx, int option, int64_t value) {
   if (!ctx) return WF_E_BADINPUT;
   switch (option) {
     case WF_OPT_SPARSE_BIG:
-      if (value < 0 || value > 3) return fail(ctx, WF_E_BADINPUT, "WF_OPT_SPARSE_BIG is 0, 1, 2 or 3");
+      // (0 and 1, the dense decision forms for <= 63 loci, are retired: round 4)
+      if (value < 2 || value > 3) return fail(ctx, WF_E_BADINPUT, "WF_OPT_SPARSE_BIG is 2 or 3");
       ctx->sparse_big = (int)value;
       return WF_OK;
     case WF_OPT_ATT_LIMIT:

@@ -639,17 +639,58 @@ __device__ __forceinline__ double pw_const_sum(int n, double v) {
   return R;
 }
 
+// run_leaf in two steps, for callers that share one seqsum chain: the leaf's shape from
+// integers alone -- kmin, then per accumulator 2 bits (k_c - kmin, 2 meaning "or more" as
+// run_leaf's select), the in-run tail sites (bits 16-19; a 0.0 tail site adds nothing to
+// a non-negative sum) and m > 0 (bit 20) -- then its value from s0 = seqsum(v, kmin).
+// Same operations as run_leaf, with two registers of state between the steps.
+struct LeafCode { int kmin, code; };
+__device__ __forceinline__ LeafCode run_leaf_code(int lo, int hi, int st, int ln) {
+  const int m = ln >> 3, be = st + (m << 3);
+  hi = max(hi, lo);
+  int k[8], kmin = m;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    k[c] = below(st + c, hi, m) - below(st + c, lo, m);
+    kmin = min(kmin, k[c]);
+  }
+  int code = 0;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) code |= min(k[c] - kmin, 2) << (2 * c);
+  const int tail = max(0, min(st + ln, hi) - max(be, lo));
+  return LeafCode{kmin, code | (tail << 16) | (m > 0 ? 1 << 20 : 0)};
+}
+__device__ __forceinline__ double run_leaf_value(double v, LeafCode lc, double s0) {
+  double res = 0.0;
+  if ((lc.code >> 20) & 1) {
+    const double s1 = s0 + v, s2 = s1 + v;
+    double r[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int d = (lc.code >> (2 * c)) & 3;
+      r[c] = d == 0 ? s0 : (d == 1 ? s1 : s2);
+    }
+    res = leaf_tree(r[0], r[1], r[2], r[3], r[4], r[5], r[6], r[7]);
+  }
+  for (int x = (lc.code >> 16) & 15; x > 0; --x) res += v;
+  return res;
+}
+
 // numpy's pairwise sum of n sites (n < kNpyBuf) holding v on [lo, hi) and 0.0 elsewhere,
 // from registers alone.  A node disjoint from the run sums to 0.0 and x + 0.0 = x, so above
 // the split node (the deepest one holding the whole run) every node passes its child's sum
 // up; below it the run is a suffix of the left child and a prefix of the right one.  A
 // suffix (prefix) node whose boundary falls in its left (right) child adds the whole other
 // child, else it passes the child holding the boundary up; each path ends at a node inside
-// the run or at a leaf (run_leaf).  Whole nodes are the spine or pair nodes of
-// pw_const_sum, so one ascent of its pair chain supplies every whole node's sum at its
-// depth, and the two paths' additions (recorded as bits per depth on the way down) are
-// applied in the same ascent.  tests/test_pw_const.py restates this line by line and checks
-// it against numpy's tree on explicit arrays.
+// the run or at a leaf.  Whole nodes are the spine or pair nodes of pw_const_sum, so one
+// ascent of its pair chain supplies every whole node's sum at its depth, and the two paths'
+// additions (recorded as bits per depth on the way down) are applied in the same ascent.
+// The walks are integer bookkeeping only: the (at most two) boundary leaves take their
+// seqsum values from the chain that also feeds the pair chain, so every lane runs the same
+// straight sequence -- one chain, two closed-form leaves, one ascent -- whatever its run's
+// shape (the leaf evaluations used to sit in three divergent branches, each with its own
+// chain).  tests/test_pw_const.py restates this line by line and checks it against numpy's
+// tree on explicit arrays.
 __device__ __forceinline__ double pw_run_sum(int n, int lo, int hi, double v) {
   lo = max(lo, 0);
   hi = min(hi, n);
@@ -683,26 +724,27 @@ __device__ __forceinline__ double pw_run_sum(int n, int lo, int hi, double v) {
     return right ? Nd{x.s + 8 * xl, 8 * (xx - xl), 1, (xx - xl) - Bt, x.t + 1} : Nd{x.s, 8 * xl, 1, xl - Bt, x.t + 1};
   };
   Nd nd{0, n, 0, 0, 0};
-  bool whole = false;
+  int mode = 0;                                      // 0 two paths, 1 a whole node, 2 one leaf
   for (;;) {                                         // down to the split node
-    if (lo <= nd.s && hi >= nd.s + nd.z) { whole = true; break; }
-    if (nd.z <= 128) return run_leaf(lo, hi, v, nd.s, nd.z);
+    if (lo <= nd.s && hi >= nd.s + nd.z) { mode = 1; break; }
+    if (nd.z <= 128) { mode = 2; break; }
     const int nl = nd.kind == 0 ? 8 * (nd.z >> 4) : 8 * ((nd.z >> 3) >> 1);
     if (hi <= nd.s + nl) nd = child(nd, false);
     else if (lo >= nd.s + nl) nd = child(nd, true);
     else break;
   }
-  // the two paths: terminal depth / type (0 whole spine, 1 whole pair, 2 leaf) / class /
-  // leaf sum, and per depth: a whole sibling to add, is it the spine, its class
-  struct Path { int tu, ty, tc; unsigned ev, evk, evc; double lv; };
+  // the two paths: terminal depth / type (0 whole spine, 1 whole pair, 2 leaf) / class, per
+  // depth a whole sibling to add (is it the spine, its class), and a leaf end's run and span.
+  // One leaf holding the whole run (mode 2) is path 0's leaf at the split depth.
+  struct Path { int tu, ty, tc; unsigned ev, evk, evc; LeafCode lc; };
   auto walk = [&](bool suffix) -> Path {
-    Path q{0, 0, 0, 0u, 0u, 0u, 0.0};
+    Path q{0, 0, 0, 0u, 0u, 0u, LeafCode{0, 0}};
     Nd x = child(nd, !suffix);
     for (;;) {
       if (suffix ? lo <= x.s : hi >= x.s + x.z) { q.tu = x.t; q.ty = x.kind; q.tc = x.cls; return q; }
       if (x.z <= 128) {
         q.tu = x.t; q.ty = 2;
-        q.lv = suffix ? run_leaf(lo, x.s + x.z, v, x.s, x.z) : run_leaf(x.s, hi, v, x.s, x.z);
+        q.lc = suffix ? run_leaf_code(lo, x.s + x.z, x.s, x.z) : run_leaf_code(x.s, hi, x.s, x.z);
         return q;
       }
       const Nd L = child(x, false), R = child(x, true);
@@ -717,20 +759,29 @@ __device__ __forceinline__ double pw_run_sum(int n, int lo, int hi, double v) {
       }
     }
   };
-  Path p0{0, 0, 0, 0u, 0u, 0u, 0.0}, p1{0, 0, 0, 0u, 0u, 0u, 0.0};
-  if (!whole) {
+  Path p0{0, 0, 0, 0u, 0u, 0u, LeafCode{0, 0}}, p1{0, 0, 0, 0u, 0u, 0u, LeafCode{0, 0}};
+  if (mode == 0) {
     p0 = walk(true);
     p1 = walk(false);
+  } else if (mode == 2) {
+    p0.ty = 2;
+    p0.lc = run_leaf_code(lo, hi, nd.s, nd.z);
   }
+  const int k0 = p0.lc.kmin, k1 = p1.lc.kmin;         // (0 without a leaf end)
   const int mL = m < 8 ? m : m >> 3;
-  const int imax = max(max(xB, mL), need16 ? 16 : 0);
-  double t = 0.0, sB = 0.0, sC = 0.0, sL = 0.0;
-  for (int i = 1; i <= imax; ++i) {
+  const int imax = mode == 2 ? k0 : max(max(max(xB, mL), need16 ? 16 : 0), max(k0, k1));   // (<= 16)
+  double t = 0.0, sB = 0.0, sC = 0.0, sL = 0.0, s0a = 0.0, s0b = 0.0;
+  for (int i = 1; i <= imax; ++i) {                  // seqsum(v, i), captured where needed
     t += v;
     sB = i == xB ? t : sB;
     sC = i == xC ? t : sC;
     sL = i == mL ? t : sL;
+    s0a = i == k0 ? t : s0a;
+    s0b = i == k1 ? t : s0b;
   }
+  const double lv0 = p0.ty == 2 ? run_leaf_value(v, p0.lc, s0a) : 0.0;
+  if (mode == 2) return lv0;
+  const double lv1 = p1.ty == 2 ? run_leaf_value(v, p1.lc, s0b) : 0.0;
   double R;                                          // the spine below the current depth
   if (m < 8) {
     R = sL;
@@ -751,16 +802,16 @@ __device__ __forceinline__ double pw_run_sum(int n, int lo, int hi, double v) {
         const double c0 = q0, c1 = q1;
         q0 = (B & 1) ? c0 + c1 : c0 + c0;
         q1 = (B & 1) ? c1 + c1 : c0 + c1;
-        if (B == 16) q0 = 8.0 * t;
+        if (B == 16) q0 = 8.0 * t;                   // t = seqsum(v, 16) (imax = 16)
       }
     }
-    if (whole) {
+    if (mode == 1) {
       if (u == nd.t) return nd.kind == 0 ? R : (nd.cls ? q1 : q0);
     } else {
-      if (u == p0.tu) acc0 = p0.ty == 2 ? p0.lv : (p0.ty == 0 ? R : (p0.tc ? q1 : q0));
+      if (u == p0.tu) acc0 = p0.ty == 2 ? lv0 : (p0.ty == 0 ? R : (p0.tc ? q1 : q0));
       if (u <= p0.tu && ((p0.ev >> u) & 1u))
         acc0 = acc0 + (((p0.evk >> u) & 1u) ? R : (((p0.evc >> u) & 1u) ? q1 : q0));
-      if (u == p1.tu) acc1 = p1.ty == 2 ? p1.lv : (p1.ty == 0 ? R : (p1.tc ? q1 : q0));
+      if (u == p1.tu) acc1 = p1.ty == 2 ? lv1 : (p1.ty == 0 ? R : (p1.tc ? q1 : q0));
       if (u <= p1.tu && ((p1.ev >> u) & 1u))
         acc1 = (((p1.evc >> u) & 1u) ? q1 : q0) + acc1;
       if (u == nd.t + 1) return acc0 + acc1;
@@ -936,7 +987,12 @@ constexpr int kRegAtt = 4;   // attachments of a segment held in registers
 // max(0, max{score_a : lo_a <= x < hi_a}).
 // Where a segment's attachments come from: the fused kernel's sorted LDS keys (attachment
 // index in the low 24 bits) or the staged path's sorted (key, attachment index) pairs.
+// Attachment sources for SegAttT.  kDesc: the attachments of a segment come in descending
+// order of their scores' top 53 bits (desc_tb), which lets SegAttT stop a scan once the
+// scores fall below the cover it found (see SegAttT::classify).
+__device__ __forceinline__ long long desc_tb(double v) { return __double_as_longlong(v) >> 9; }
 struct KeySrc {
+  static constexpr bool kDesc = false;
   const uint64_t* keys;
   const int *alo, *ahi;
   const double* asc;
@@ -946,6 +1002,7 @@ struct KeySrc {
   }
 };
 struct SortedSrc {                       // attachments gathered into sorted order
+  static constexpr bool kDesc = false;
   const int2* lohi;
   const double* sc;
   __device__ __forceinline__ int idx(int t) const { return t; }
@@ -955,6 +1012,7 @@ struct SortedSrc {                       // attachments gathered into sorted ord
   }
 };
 struct ValSrc {
+  static constexpr bool kDesc = false;
   const int* vals;
   const int *alo, *ahi;
   const double* asc;
@@ -995,9 +1053,15 @@ struct SegAttT {
       for (int i = 0; i < kRegAtt; ++i)
         if (x >= lo[i] && x < hi[i]) v = sc[i] > v ? sc[i] : v;
     } else {
+      long long vtb = -1;                  // (kDesc: top bits of the first cover's score)
       for (int t = kb; t < ke; ++t) {
         int l, h; double s;
         get(C, t, l, h, s);
+        if (Src::kDesc) {
+          const long long tb = desc_tb(s);
+          if (vtb >= 0 && tb < vtb) break;   // every later score is below the cover's
+          if (x >= l && x < h && vtb < 0) vtb = tb;
+        }
         if (x >= l && x < h) v = s > v ? s : v;
       }
     }
@@ -1023,12 +1087,21 @@ struct SegAttT {
   __device__ __forceinline__ int classify(const Src& C, int st, int m, double& F, int& plo,
                                           int& phi, double& ps) const {
     const int be = st + (m << 3);
-    const int na = REG ? kRegAtt : ke - kb;
+    int na = REG ? kRegAtt : ke - kb;
     F = 0.0;
+    long long ftb = -1;
 #pragma unroll
     for (int i = 0; i < na; ++i) {
       int l, h; double v;
       att<REG>(C, i, l, h, v);
+      if (!REG && Src::kDesc) {
+        // descending scores: past the first whole-body cover, once the scores drop below
+        // its (top bits) nothing later covers higher or exceeds F, so the partial-overlap
+        // scan below stops there too
+        const long long tb = desc_tb(v);
+        if (ftb >= 0 && tb < ftb) { na = i; break; }
+        if (l < h && l <= st && be <= h && ftb < 0) ftb = tb;
+      }
       if (l < h && l <= st && be <= h) F = v > F ? v : F;
     }
     int npos = 0;
@@ -1119,10 +1192,19 @@ struct SegAttT {
     for (int x = st; x < be;) {
       double v = 0.0;
       int nx = be;
+      long long vtb = -1;
 #pragma unroll
       for (int i = 0; i < na; ++i) {
         int l, h; double s;
         att<REG>(C, i, l, h, s);
+        if (!REG && Src::kDesc) {
+          // descending scores: the attachments past the first cover of x, once below its
+          // score, neither raise the envelope on [x, nx) nor start a higher run inside it
+          // (a run split at a lower attachment's end would add the same values in order)
+          const long long tb = desc_tb(s);
+          if (vtb >= 0 && tb < vtb) break;
+          if (l < h && l <= x && x < h && vtb < 0) vtb = tb;
+        }
         if (l < h) {
           if (l <= x && x < h) { v = s > v ? s : v; nx = min(nx, h); }
           else if (l > x) nx = min(nx, l);

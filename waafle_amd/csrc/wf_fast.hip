@@ -41,6 +41,12 @@
 // 1: every hit batch of a round finds its loci before the first takes its slots (the loci
 // searches of the batches overlap); 0: batch by batch.  Same-box A/B at cfg4 (r4c): 0 is
 // 0.15 ms faster per pass (the batched form's registers spill), so 0 is the default.
+// resident waves per SIMD of the roll-up launches: 4 (128 VGPRs, some spilled) beat 3 (168,
+// none) by 0.35 ms of roll-up per cfg4 pass on one box (r4f: their few contigs per wave
+// want occupancy more than registers)
+#ifndef WF_ROLL_WAVES
+#define WF_ROLL_WAVES 4
+#endif
 // roll-up levels: multi-attachment segment means one numpy leaf per lane (flat_leaf_means);
 // 0: one segment per lane (lane_seg_mean)
 #ifndef WF_FLAT_LEAVES
@@ -221,8 +227,16 @@ __device__ __forceinline__ void wave_sort(T (&x)[R]) {
   }
 }
 
-// The slice's keys in sorted order (one network of 64 * R 32-bit keys, lane-major).
-template <int R, class SM>
+// The slice's keys in sorted order (one network of 64 * R 32-bit keys, lane-major), and the
+// attachments' ranges and scores moved along: afterwards attachment t's lohi / sc sit at t
+// and its key's slot field is t, so every later read goes straight to position t (no
+// key -> slot hop: the loads of a segment's attachments issue together).  Nothing reads
+// the insertion order after the first sort (F.hit / F.sm: annotation pass 2, before it).
+//
+// PERMUTE = false (the roll-up launches): keys only.  Their slot fields are then data
+// positions in descending-score order (rank_slice), so within each segment the sorted
+// attachments come best first (SegAttT's kDesc early exits).
+template <int R, bool PERMUTE = true, class SM>
 __device__ __forceinline__ void sort_slice(SM& F, int n_att) {
   const int lane = lane_id();
   uint32_t y[R];
@@ -232,11 +246,78 @@ __device__ __forceinline__ void sort_slice(SM& F, int n_att) {
     y[r] = t < n_att ? F.key[t] : ~0u;
   }
   wave_sort<R>(y);
+  if (!PERMUTE) {
+    wave_sync();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int t = R * lane + r;
+      if (t < n_att) F.key[t] = y[r];
+    }
+    wave_sync();
+    return;
+  }
+  uint32_t lh[R];
+  double sv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = R * lane + r;
+    lh[r] = 0u;
+    sv[r] = 0.0;
+    if (t < n_att) {
+      const int slot = (int)(y[r] & kSlotMask);
+      lh[r] = F.lohi[slot];
+      sv[r] = F.sc[slot];
+    }
+  }
   wave_sync();
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int t = R * lane + r;
-    if (t < n_att) F.key[t] = y[r];
+    if (t < n_att) {
+      F.key[t] = (y[r] & ~kSlotMask) | (uint32_t)t;
+      F.lohi[t] = lh[r];
+      F.sc[t] = sv[r];
+    }
+  }
+  wave_sync();
+}
+
+// The roll-up launches' data order: attachments moved to positions of descending score
+// (64-bit bitonic sort on the complemented top 53 score bits, then the insertion slot), and
+// each key's slot field set to its attachment's new position.  Keys stay unsorted (the
+// level's sort_slice<R, false> sorts them); F.hit / F.sm are not used past this point.
+template <int R, class SM>
+__device__ __forceinline__ void rank_slice(SM& F, int n_att) {
+  const int lane = lane_id();
+  uint64_t y[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = R * lane + r;
+    y[r] = t < n_att ? ((((1ull << 53) - 1ull - (uint64_t)desc_tb(F.sc[t])) << 9) | (uint64_t)t) : ~0ull;
+  }
+  wave_sort<R>(y);
+  uint32_t kk[R], lh[R];
+  double sv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = R * lane + r;
+    kk[r] = 0u; lh[r] = 0u; sv[r] = 0.0;
+    if (t < n_att) {
+      const int slot = (int)(y[r] & kSlotMask);
+      kk[r] = F.key[slot];
+      lh[r] = F.lohi[slot];
+      sv[r] = F.sc[slot];
+    }
+  }
+  wave_sync();
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int t = R * lane + r;
+    if (t < n_att) {
+      F.key[t] = (kk[r] & ~kSlotMask) | (uint32_t)t;
+      F.lohi[t] = lh[r];
+      F.sc[t] = sv[r];
+    }
   }
   wave_sync();
 }
@@ -252,8 +333,23 @@ __device__ __forceinline__ int seg_first(SM& F, int s) { return (int)(F.seg[s] &
 __device__ __forceinline__ int lo16(uint32_t w) { return (int)(w & 0xFFFFu); }
 __device__ __forceinline__ int hi16(uint32_t w) { return (int)(w >> 16); }
 
-// The slice's attachments for SegAttT (wf_device.h): sorted position -> slot -> range, score.
+// The slice's attachments for SegAttT (wf_device.h): sorted position t -> range, score (at
+// t since sort_slice).
 struct SliceSrc {
+  static constexpr bool kDesc = false;
+  const uint32_t* key;
+  const uint32_t* lohi;
+  const double* sc;
+  __device__ __forceinline__ int idx(int t) const { return t; }
+  __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
+    const uint32_t w = lohi[a];
+    l = lo16(w); h = hi16(w); v = sc[a];
+  }
+};
+// The roll-up launches' attachments (rank_slice): sorted position t -> its key's slot field
+// -> range, score; a segment's attachments come in descending score order.
+struct SliceSrcDesc {
+  static constexpr bool kDesc = true;
   const uint32_t* key;
   const uint32_t* lohi;
   const double* sc;
@@ -268,9 +364,9 @@ struct SliceSrc {
 // numpy leaf by SegAttT::leaf (closed forms, else the envelope's runs), folded in tree
 // order on a register stack.  For the roll-up levels, where many segments per block have
 // several attachments and one lane each beats one wave each.
-template <class LT>
-__device__ __noinline__ double lane_seg_mean(SliceSrc src, int kb, int ke, LT lt, int nl, int len) {
-  SegAttT<SliceSrc> at;
+template <class Src, class LT>
+__device__ __noinline__ double lane_seg_mean(Src src, int kb, int ke, LT lt, int nl, int len) {
+  SegAttT<Src> at;
   at.load(src, kb, ke);
   SumStack stk;
   for (int q = 0; q < nl; ++q) {
@@ -290,8 +386,8 @@ __device__ __noinline__ double lane_seg_mean(SliceSrc src, int kb, int ke, LT lt
 // tree order (SumStack) from W.lv.  Same leaf values, same fold, so the same bits as
 // lane_seg_mean; a round costs one leaf per lane instead of a whole segment.  W.z maps a
 // round's start position to its segment's lane.  Returns the mean on the segment's lane.
-template <int R>
-__device__ __noinline__ double flat_leaf_means(SliceSrc src, const uint32_t* lut, uint64_t mlist, int kb, int ke,
+template <int R, class Src>
+__device__ __noinline__ double flat_leaf_means(Src src, const uint32_t* lut, uint64_t mlist, int kb, int ke,
                                                int nl, int len, WaveRunsT<R>& W) {
   const int lane = lane_id();
   double mean = 0.0;
@@ -316,7 +412,7 @@ __device__ __noinline__ double flat_leaf_means(SliceSrc src, const uint32_t* lut
     const uintptr_t olut = (uintptr_t)__shfl((long long)(uintptr_t)lut, own, 64);
     if (lane < used) {
       const int4 e = PackedLut{reinterpret_cast<const uint32_t*>(olut)}(lane - p);
-      SegAttT<SliceSrc> at;
+      SegAttT<Src> at;
       at.load(src, okb, oke);
       W.lv[lane] = at.leaf(src, e.x, e.y);
     }
@@ -671,7 +767,7 @@ template <int CAP, bool FULL, bool ROLL = false>
 // offset 0.  ROLL (first form only): roll-up level start_level > 0 of the contigs in `list`
 // (the wave levels, S.anc set) -- its own instantiation, so profiles tell the level-0 pass
 // from the roll-up passes and level 0 carries none of their code.
-__global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
+__global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
                                              const int32_t* list, int n_list, const int64_t* n_dev, int rollup,
                                              int start_level_arg) {
   static_assert(!(FULL && ROLL), "the roll-up passes are first-form launches");
@@ -922,6 +1018,11 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
     pair_evals = lane_bcast((uint64_t)pair_evals, 0);
     bool seed = false;                                 // raised at level 0: staged level 1 seed
     bool dumped = false;                               // segment table handed to k_dump_sparse
+    // roll-up launches: attachments at descending-score positions (rank_slice), addressed
+    // through their keys' slot fields from here on; level 0 sorts them into key order
+    using Src = typename std::conditional<ROLL, SliceSrcDesc, SliceSrc>::type;
+    if (ROLL && !staged && n_att > 0) rank_slice<(CAP + 63) / 64>(F, n_att);
+    auto slot_at = [&](int t) -> int { return ROLL ? (int)(F.key[t] & kSlotMask) : t; };
     for (int level = start_level; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
       const int iteration = level + 1;
       if (level > start_level) {                     // roll up (:431-445): re-key to the parent clade
@@ -932,7 +1033,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
         }
         wave_sync();
       }
-      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64>(F, n_att);   // one network: code size
+      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64, !ROLL>(F, n_att);   // one network: code size
       WLAP(3);
       // ---- segments = runs of equal (clade, locus) ----
       int ns = 0;
@@ -1005,7 +1106,16 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
       auto best_score = [&](int t) -> double {       // upper bound of segment t's mean
         const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
         double ub = 0.0;
-        for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[F.key[q] & kSlotMask]);
+        if (ROLL) {                                  // best first: past its top bits, nothing higher
+          const long long tb0 = desc_tb(F.sc[slot_at(kb)]);
+          for (int q = kb; q < ke; ++q) {
+            const double x = F.sc[slot_at(q)];
+            if (desc_tb(x) < tb0) break;
+            ub = fmax(ub, x);
+          }
+          return ub;
+        }
+        for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[slot_at(q)]);
         return ub;
       };
       int n_pass0 = -1;                                // pass 0's list, built with the run sizes
@@ -1145,21 +1255,21 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
             const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
             if (na == 1) {
               if (thread_ok) {
-                const int slot = (int)(F.key[kb] & kSlotMask);
+                const int slot = slot_at(kb);
                 lo = lo16(F.lohi[slot]); hi = hi16(F.lohi[slot]); vv = F.sc[slot];
                 one_run = true;
               }
             } else if (na <= kPruneMax) {
               double Fw = 0.0;                           // best whole-locus attachment
               for (int t = kb; t < ke; ++t) {
-                const int slot = (int)(F.key[t] & kSlotMask);
+                const int slot = slot_at(t);
                 const uint32_t x = F.lohi[slot];
                 const double sc = F.sc[slot];
                 if (lo16(x) <= 0 && hi16(x) >= len && sc > Fw) Fw = sc;
               }
               int kept = 0;                              // attachments the envelope still needs
               for (int t = kb; t < ke; ++t) {
-                const int slot = (int)(F.key[t] & kSlotMask);
+                const int slot = slot_at(t);
                 const uint32_t x = F.lohi[slot];
                 kept += (lo16(x) < hi16(x) && F.sc[slot] > Fw) ? 1 : 0;
               }
@@ -1183,7 +1293,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
             // numpy leaf per lane over all of the chunk's multi-attachment segments
             int kb = 0, ke = 0;
             if (multi) { kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att; }
-            const double m = flat_leaf_means(SliceSrc{F.key, F.lohi, F.sc}, F.lut + F.lbase[multi ? g : 0], mlist,
+            const double m = flat_leaf_means(Src{F.key, F.lohi, F.sc}, F.lut + F.lbase[multi ? g : 0], mlist,
                                              kb, ke, nl, len, F.runs());
             if (multi) v[s] = m;
             mlist = 0;
@@ -1191,7 +1301,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
             // several multi-attachment segments: one lane each, not the whole wave per segment
             if (multi) {
               const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
-              v[s] = lane_seg_mean(SliceSrc{F.key, F.lohi, F.sc}, kb, ke, PackedLut{F.lut + F.lbase[g]}, nl, len);
+              v[s] = lane_seg_mean(Src{F.key, F.lohi, F.sc}, kb, ke, PackedLut{F.lut + F.lbase[g]}, nl, len);
             }
             mlist = 0;
           }
@@ -1203,7 +1313,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? 3 : 4)) void k_wave(const SA
             int lo = 0, hi = 0;
             double sc = 0.0;
             if (lane < na) {
-              const int slot = (int)(F.key[kb + lane] & kSlotMask);
+              const int slot = slot_at(kb + lane);
               const uint32_t x = F.lohi[slot];
               if (lo16(x) < hi16(x)) { lo = lo16(x); hi = hi16(x); sc = F.sc[slot]; }
             }

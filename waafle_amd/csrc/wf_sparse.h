@@ -997,19 +997,46 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
   const uint64_t allG = (1ull << G) - 1ull;
   const int iteration = level + 1;
   int64_t pair_evals = level == 0 ? 0 : K.pair_evals[c];
-  for (int q = lane; q < ns; q += 64) {
-    sh.cg[q] = S.dump_cg[so + q];
-    sh.v[q] = S.dump_mean[so + q];
-  }
-  if (lane < G) {
-    const int ls = K.lstart[l0 + lane], le = K.lend[l0 + lane];
-    sh.len[lane] = max(ls, le) - min(ls, le) + 1;
+  // Global loads in two rounds for the whole table (not one round trip per 64 segments):
+  // the table and the loci, then the parents / listed parents of the clades it names.
+  constexpr int kCh = kE2Seg / 64;
+  {
+    int2 cgr[kCh];
+    double vr[kCh];
+#pragma unroll
+    for (int k = 0; k < kCh; ++k) {
+      const int q = 64 * k + lane;
+      cgr[k] = make_int2(-1, 0);
+      vr[k] = 0.0;
+      if (q < ns) {
+        cgr[k] = S.dump_cg[so + q];
+        vr[k] = S.dump_mean[so + q];
+      }
+    }
+    int ln = 0;
+    if (lane < G) {
+      const int ls = K.lstart[l0 + lane], le = K.lend[l0 + lane];
+      ln = max(ls, le) - min(ls, le) + 1;
+    }
+#pragma unroll
+    for (int k = 0; k < kCh; ++k) {
+      const int q = 64 * k + lane;
+      if (q < ns) {
+        sh.cg[q] = cgr[k];
+        sh.v[q] = vr[k];
+      }
+    }
+    if (lane < G) sh.len[lane] = ln;
   }
   __syncthreads();
-  // potential clades (a locus >= k2, missing loci scoring 0.0; :603-605)
+  // clade runs (one per run head): potential clades (a locus >= k2, missing loci scoring
+  // 0.0; :603-605) and, for the sister checks, the loci at or above the threshold
   int Pp = 0;
-  for (int t0 = 0; t0 < ns; t0 += 64) {
-    const int t = t0 + lane;
+  int hcl[kCh];
+  uint64_t hh[kCh];
+#pragma unroll
+  for (int k = 0; k < kCh; ++k) {
+    const int t = 64 * k + lane;
     bool pot = false;
     uint64_t pres = 0, mk2 = 0, hm = 0;
     int cl = -1;
@@ -1027,47 +1054,49 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
         if (0.0 >= P.k2) mk2 |= miss;
         if (0.0 >= P.sister_thr) hm |= miss;
         pot = mk2 != 0ull;
+      } else {
+        cl = -1;                                       // (not a run head)
       }
     }
+    hcl[k] = cl;
+    hh[k] = hm;
     const uint64_t pb = __ballot(pot);
     const int i = Pp + __popcll(pb & below);
     if (pot && i < 64) {
-      sh.t[i] = t; sh.cl[i] = cl; sh.par[i] = K.parent[cl]; sh.sibp[i] = K.sibp[cl];
+      sh.t[i] = t; sh.cl[i] = cl;
       sh.pres[i] = pres; sh.pm[i] = mk2 & um; sh.hm[i] = hm; sh.s1[i] = 0; sh.s2[i] = 0;
     }
     Pp += __popcll(pb);
   }
   if (Pp > 64) return false;
   __syncthreads();
+  int hsp[kCh];                                        // listed parents of the runs' clades
+#pragma unroll
+  for (int k = 0; k < kCh; ++k) hsp[k] = (P.sister_on && hcl[k] >= 0 && hh[k] != 0ull) ? K.sibp[hcl[k]] : -1;
+  const int my_cl = lane < Pp ? sh.cl[lane] : -1;
+  const int my_par = lane < Pp ? K.parent[my_cl] : -2;
+  if (lane < Pp) {
+    sh.par[lane] = my_par;
+    sh.sibp[lane] = K.sibp[my_cl];
+  }
   const uint64_t my_pm = lane < Pp ? sh.pm[lane] : 0ull;   // (cand overwrites pm and cg)
+  __syncthreads();
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
   if (P.sister_on) {
     // per potential clade, the present clades listed under its parent (itself excluded) at
     // or above the threshold (a segment left out of the table scores below it)
-    const int my_par = lane < Pp ? sh.par[lane] : -2, my_cl = lane < Pp ? sh.cl[lane] : -1;
     uint64_t s1 = 0, s2 = 0;
-    for (int t0 = 0; t0 < ns; t0 += 64) {
-      const int t = t0 + lane;
-      int sp = -1, cl = -1;
-      uint64_t h = 0;
-      if (t < ns) {
-        cl = sh.cg[t].x;
-        if (t == 0 || sh.cg[t - 1].x != cl) {
-          uint64_t pres = 0;
-          for (int q = t; q < ns && sh.cg[q].x == cl; ++q) {
-            pres |= 1ull << sh.cg[q].y;
-            if (sh.v[q] >= P.sister_thr) h |= 1ull << sh.cg[q].y;
-          }
-          if (0.0 >= P.sister_thr) h |= allG & ~pres;
-          if (h) sp = K.sibp[cl];
-        }
-      }
+#pragma unroll
+    for (int k = 0; k < kCh; ++k) {
+      if (64 * k >= ns) break;
+      const int sp = hsp[k], cl = hcl[k];
+      const uint64_t h = hh[k];
       bool match = false;
       for (int i = 0; i < Pp; ++i) match = match || (sp >= 0 && sp == sh.par[i]);
       for (uint64_t mb = __ballot(match); mb; mb &= mb - 1) {
         const int src = __builtin_ctzll(mb);
-        const int sp_r = __shfl(sp, src, 64), cl_r = __shfl(cl, src, 64);
-        const uint64_t h_r = (uint64_t)__shfl((long long)h, src, 64);
+        const int sp_r = lane_bcast(sp, src), cl_r = lane_bcast(cl, src);
+        const uint64_t h_r = lane_bcast(h, src);
         if (my_par == sp_r && my_cl != cl_r) {
           s2 |= s1 & h_r;
           s1 |= h_r;

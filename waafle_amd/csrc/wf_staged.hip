@@ -1236,7 +1236,7 @@ struct StagedState {
   Buf span_cnt, spans;                              // --write-details only
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
-  int sparse_big = 3;                // WF_OPT_SPARSE_BIG (0 dense, 1 overflow, 2 all, 3 decisions)
+  int sparse_big = 3;                // WF_OPT_SPARSE_BIG (2 all, 3 the open decisions; 0/1 retired)
   int sparse_res = -1;               // resident k_big_sparse waves per CU
   int two_res = -1;                  // resident k_dump_sparse<1> (compact tables) waves per CU
   int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
@@ -1258,8 +1258,6 @@ struct StagedState {
   bool lut_ready = false;
   int64_t dec_lds = 32 * 1024;       // decision arena (grows with the data, see staged_score)
   bool dec_lds_fixed = false;        // set by wf_set_lds_bytes / WF_DEC_LDS
-  int wide_res = -1;                 // resident k_decide<3, 256> workgroups per CU ...
-  int64_t wide_res_lds = -1;         // ... at this arena size
   unsigned long long* host_counters = nullptr;   // pinned
   // host-coherent mailbox: k_publish writes counts + a sequence word, the host spins on it
   unsigned long long* mbox = nullptr;
@@ -1945,11 +1943,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     static const hipError_t attr3 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3>),
                                                         hipFuncAttributeMaxDynamicSharedMemorySize,
                                                         160 * 1024 - 1024);
-    static const hipError_t attr5 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_decide<3, 256>),
-                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                        160 * 1024 - 1024);
     ST_TRY(attr3);
-    ST_TRY(attr5);
   }
   for (int level = start; n_act > 0 && level <= kMaxIter; ++level) {
     sa.counters = lvl_ctr + 8 * level;
@@ -2039,30 +2033,14 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     const unsigned dgrid = (unsigned)std::min<int64_t>(n_act, (int64_t)st->cus * 16);
     hipLaunchKernelGGL(k_one, dim3(std::min<int64_t>(n_act, (int64_t)st->cus * 32)), dim3(64), 0, s, sa,
                        n_act, level, n_keys);
-    // explain_two for the contigs k_one left open and the whole level for the ones it handed
-    // over (counts on the device: a grid of rank-independent size, idle blocks exit at once)
-    // as many one-wave decision workgroups as the arena and 3 waves/SIMD (VGPRs) allow: the
-    // explain_two contigs are latency chains, so they should all be in flight at once
+    // the dense decision for what k_one handed over whole (> 63 loci, more segments than it
+    // holds, --weak-loci assign-unknown) and the > 63-loci contigs it left open (counts on
+    // the device: a grid of rank-independent size, idle blocks exit at once): as many
+    // one-wave workgroups as the arena and 3 waves/SIMD (VGPRs) allow
     const unsigned dec_per_cu =
         (unsigned)std::max<int64_t>(1, std::min<int64_t>(12, (160 * 1024) / std::max<int64_t>(st->dec_lds, 1)));
-    // the four-wave form (roll-up levels: few open contigs, four waves each) gets at most the
-    // workgroups resident at once (VGPRs allow 3 per CU at 137): each workgroup walks its
-    // contigs grid-stride, so a second, partial round only lengthens the tail
-    if (st->wide_res_lds != st->dec_lds) {           // per context: no shared host state
-      int b = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_decide<3, 256>), 256,
-                                                       (size_t)st->dec_lds) != hipSuccess || b < 1)
-        b = (int)dec_per_cu;
-      st->wide_res = b;
-      st->wide_res_lds = st->dec_lds;
-    }
-    const unsigned wide_per_cu = std::min<unsigned>(dec_per_cu, (unsigned)st->wide_res);
-    if (level > 0)
-      hipLaunchKernelGGL((k_decide<3, 256>), dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * wide_per_cu)),
-                         dim3(256), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
-    else
-      hipLaunchKernelGGL(k_decide<3>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
-                         dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
+    hipLaunchKernelGGL(k_decide<3>, dim3(std::min<unsigned>(dgrid, (unsigned)st->cus * dec_per_cu)),
+                       dim3(kDecNT), (size_t)st->dec_lds, s, sa, n_act, level, n_keys);
     ST_TRY(hipGetLastError());
     t_span(st, WF_PHASE_DECIDE, t_dec, t_mark(st, s));
     if (mailbox) {
