@@ -34,8 +34,10 @@ enum wf_status {
   WF_E_NOMEM = -4,     /* per-contig workspace too small (see wf_result.need_bytes) */
   WF_E_STATE = -5,     /* call order (e.g. wf_score before wf_set_taxonomy) */
   WF_E_EMPTYMASK = -6, /* every locus masked at a roll-up level (np.min of empty) */
-  WF_E_TOOBIG = -7     /* the batch's hit-locus attachments exceed one call's limit
-                          (WF_OPT_ATT_LIMIT, at most 2^31 - 1): score it in parts */
+  WF_E_TOOBIG = -7     /* the hit-locus attachments the staged kernels would hold in HBM
+                          (the contigs the wave forms hand them; every contig in
+                          WF_MODE_STAGED) exceed one call's limit (WF_OPT_ATT_LIMIT, at
+                          most 2^31 - 1): score the batch in parts */
 };
 
 enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
@@ -59,8 +61,9 @@ enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
  *   form on every input).  The dense matrix decision remains for > 63 loci and for a table
  *   the segment-table form declines (its class or pair tables outgrown).  The values 0 and 1
  *   (dense decisions for <= 63 loci) are retired: WF_E_BADINPUT.
- * WF_OPT_ATT_LIMIT: hit-locus attachments one wf_score call accepts (default and maximum
- *   2^31 - 1; more -> WF_E_TOOBIG, nothing scored).
+ * WF_OPT_ATT_LIMIT: hit-locus attachments the staged kernels accept in one wf_score call
+ *   (default and maximum 2^31 - 1; more -> WF_E_TOOBIG and the call's records are not
+ *   valid: score the batch in parts).  The wave forms hold a contig's attachments in LDS.
  * WF_OPT_WAVE_TWO (WF_MODE_LEVEL0): 1 (default) the first wave form also decides explain_two
  *   (up to 64 potential clades, <= 63 loci) and carries the roll-up levels, one pass per level
  *   over the contigs still open; the rest goes to the segment-table decision (k_dump_sparse);

@@ -52,11 +52,16 @@ def main():
         if i == args.steps - 1:
             torch.cuda.synchronize()
             so.wf_stamps_reset_fast()
+            so.wf_stamps_reset_sparse()
         assert so.wf_score(h, C.byref(db.bs), C.byref(params), C.byref(db.rs)) == 0
     torch.cuda.synchronize()
     st = (C.c_ulonglong * 48)()
     so.wf_stamps_read_fast(st, 48)
     v = [int(x) for x in st]
+    sp = (C.c_ulonglong * 16)()
+    so.wf_stamps_read_sparse.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    so.wf_stamps_read_sparse(sp, 16)
+    w = [int(x) for x in sp]
     tot = sum(v[:16]) + sum(v[32:36])                # (the explain_one laps are their own)
     nc = max(1, v[16])
     out = {"config": args.config, "contigs": n, "flags": args.flags, "sampled": v[16],
@@ -66,7 +71,15 @@ def main():
            "stats_per_contig": {name: v[i] / nc for i, name in STATS.items()},
            "pass_entries_per_contig": {str(p): v[24 + p] / nc for p in range(8)},
            "explain_one": {k: v[32 + i] / nc for i, k in enumerate(
-               ["sure bits/pass choice", "option scan", "reduction", "meld_one+LCA"])}}
+               ["sure bits/pass choice", "option scan", "reduction", "meld_one+LCA"])},
+           # sp_two (k_dump_sparse<1>, every launch of the pass), every 8th contig
+           "sp_two": {"sampled": w[8],
+                      "cycles_per_contig": sum(w[:6]) / max(1, w[8]),
+                      "phases": {k: w[i] / max(1, w[8]) for i, k in enumerate(
+                          ["table + loci loads", "run heads / potentials", "parents + sister masks",
+                           "candidate pairs", "pass 1 ranks", "pass 2, eval_two, meld, record"])},
+                      "per_contig": {"segments": w[9] / max(1, w[8]), "potential clades": w[10] / max(1, w[8]),
+                                     "candidate pairs": w[11] / max(1, w[8])}}}
     print(json.dumps(out))
     for p, d in out["phases"].items():
         print("{:24s} {:10.0f} cyc  {:5.1f}%".format(p, d["cycles_per_contig"], 100 * d["frac"]),

@@ -120,13 +120,15 @@ def oracle_chunk_sample(name, k, n, tax):
 
 
 def test_attachment_limit_splits_batch_like_unsplit():
-    """WF_OPT_ATT_LIMIT makes wf_score return WF_E_TOOBIG for a batch above the limit;
-    GpuScorer.score then scores contig halves (recursively): the records equal the unsplit
-    call's field by field (annotation winners rebased, meld slots in place)."""
+    """WF_OPT_ATT_LIMIT makes wf_score return WF_E_TOOBIG for a batch whose staged
+    attachments exceed the limit (the staged form: every contig's attachments go to HBM;
+    the wave forms keep theirs in LDS); GpuScorer.score then scores contig halves
+    (recursively): the records equal the unsplit call's field by field (annotation winners
+    rebased, meld slots in place)."""
     data = synth.generate(n=3000, genes=8, clades=200, seed=81)
     batch, tax = synth.to_batch(data)
     want = score(batch, tax)
-    s = engine.GpuScorer(0, options={lib.OPT_ATT_LIMIT: 20000})
+    s = engine.GpuScorer(0, mode="staged", options={lib.OPT_ATT_LIMIT: 20000})
     s.set_taxonomy(tax)
     with pytest.raises(lib.WaafleHipError) as ei:
         s._score_once(batch, PARAMS)

@@ -988,9 +988,9 @@ constexpr int kRegAtt = 4;   // attachments of a segment held in registers
 // Where a segment's attachments come from: the fused kernel's sorted LDS keys (attachment
 // index in the low 24 bits) or the staged path's sorted (key, attachment index) pairs.
 // Attachment sources for SegAttT.  kDesc: the attachments of a segment come in descending
-// order of their scores' top 53 bits (desc_tb), which lets SegAttT stop a scan once the
-// scores fall below the cover it found (see SegAttT::classify).
-__device__ __forceinline__ long long desc_tb(double v) { return __double_as_longlong(v) >> 9; }
+// order of their scores' top 23 bits (desc_tb; ties in any order), which lets SegAttT stop a
+// scan once those bits fall below the cover it found (see SegAttT::classify).
+__device__ __forceinline__ long long desc_tb(double v) { return __double_as_longlong(v) >> 40; }
 struct KeySrc {
   static constexpr bool kDesc = false;
   const uint64_t* keys;

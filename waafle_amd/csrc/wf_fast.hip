@@ -47,6 +47,12 @@
 #ifndef WF_ROLL_WAVES
 #define WF_ROLL_WAVES 4
 #endif
+// roll-up launches: 1 keeps attachments in descending-score order (rank_slice, SegAttT's
+// early exits); 0 (default): sorted-order data as level 0.  Same-box A/B at cfg4 (r4j):
+// 16.04 / 16.09 ms with, 16.05 without -- the extra sort eats what the early exits save.
+#ifndef WF_ROLL_DESC
+#define WF_ROLL_DESC 0
+#endif
 // roll-up levels: multi-attachment segment means one numpy leaf per lane (flat_leaf_means);
 // 0: one segment per lane (lane_seg_mean)
 #ifndef WF_FLAT_LEAVES
@@ -283,17 +289,18 @@ __device__ __forceinline__ void sort_slice(SM& F, int n_att) {
 }
 
 // The roll-up launches' data order: attachments moved to positions of descending score
-// (64-bit bitonic sort on the complemented top 53 score bits, then the insertion slot), and
-// each key's slot field set to its attachment's new position.  Keys stay unsorted (the
-// level's sort_slice<R, false> sorts them); F.hit / F.sm are not used past this point.
+// (one 32-bit bitonic sort: the complemented top 23 score bits (desc_tb) over the insertion
+// slot), and each key's slot field set to its attachment's new position.  Keys stay
+// unsorted (the level's sort_slice<R, false> sorts them); F.hit / F.sm are not used past
+// this point.
 template <int R, class SM>
 __device__ __forceinline__ void rank_slice(SM& F, int n_att) {
   const int lane = lane_id();
-  uint64_t y[R];
+  uint32_t y[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const int t = R * lane + r;
-    y[r] = t < n_att ? ((((1ull << 53) - 1ull - (uint64_t)desc_tb(F.sc[t])) << 9) | (uint64_t)t) : ~0ull;
+    y[r] = t < n_att ? ((((1u << 23) - 1u - (uint32_t)desc_tb(F.sc[t])) << 9) | (uint32_t)t) : ~0u;
   }
   wave_sort<R>(y);
   uint32_t kk[R], lh[R];
@@ -349,7 +356,7 @@ struct SliceSrc {
 // The roll-up launches' attachments (rank_slice): sorted position t -> its key's slot field
 // -> range, score; a segment's attachments come in descending score order.
 struct SliceSrcDesc {
-  static constexpr bool kDesc = true;
+  [[maybe_unused]] static constexpr bool kDesc = true;
   const uint32_t* key;
   const uint32_t* lohi;
   const double* sc;
@@ -1020,9 +1027,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
     bool dumped = false;                               // segment table handed to k_dump_sparse
     // roll-up launches: attachments at descending-score positions (rank_slice), addressed
     // through their keys' slot fields from here on; level 0 sorts them into key order
-    using Src = typename std::conditional<ROLL, SliceSrcDesc, SliceSrc>::type;
-    if (ROLL && !staged && n_att > 0) rank_slice<(CAP + 63) / 64>(F, n_att);
-    auto slot_at = [&](int t) -> int { return ROLL ? (int)(F.key[t] & kSlotMask) : t; };
+    constexpr bool kDescOrder = ROLL && WF_ROLL_DESC;
+    using Src = typename std::conditional<kDescOrder, SliceSrcDesc, SliceSrc>::type;
+    if (kDescOrder && !staged && n_att > 0) rank_slice<(CAP + 63) / 64>(F, n_att);
+    auto slot_at = [&](int t) -> int { return kDescOrder ? (int)(F.key[t] & kSlotMask) : t; };
     for (int level = start_level; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
       const int iteration = level + 1;
       if (level > start_level) {                     // roll up (:431-445): re-key to the parent clade
@@ -1033,7 +1041,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         }
         wave_sync();
       }
-      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64, !ROLL>(F, n_att);   // one network: code size
+      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64, !kDescOrder>(F, n_att);   // one network: code size
       WLAP(3);
       // ---- segments = runs of equal (clade, locus) ----
       int ns = 0;
@@ -1106,7 +1114,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
       auto best_score = [&](int t) -> double {       // upper bound of segment t's mean
         const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
         double ub = 0.0;
-        if (ROLL) {                                  // best first: past its top bits, nothing higher
+        if (kDescOrder) {                            // best first: past its top bits, nothing higher
           const long long tb0 = desc_tb(F.sc[slot_at(kb)]);
           for (int q = kb; q < ke; ++q) {
             const double x = F.sc[slot_at(q)];

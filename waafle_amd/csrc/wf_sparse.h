@@ -991,6 +991,9 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
   const uint64_t below = (1ull << lane) - 1ull;
   const int ns = se - so;
   if (G > kE2MaxG || ns > kE2Seg) return false;
+  SLAP_MARK(c);
+  SSTAT(8, 1);
+  SSTAT(9, ns);
   const uint64_t um = hdr & ~(1ull << 63);
   const bool root = (hdr >> 63) != 0ull;
   const int Gu = __popcll(um);
@@ -1029,6 +1032,7 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
     if (lane < G) sh.len[lane] = ln;
   }
   __syncthreads();
+  SLAP(0);
   // clade runs (one per run head): potential clades (a locus >= k2, missing loci scoring
   // 0.0; :603-605) and, for the sister checks, the loci at or above the threshold
   int Pp = 0;
@@ -1070,6 +1074,8 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
   }
   if (Pp > 64) return false;
   __syncthreads();
+  SLAP(1);
+  SSTAT(10, Pp);
   int hsp[kCh];                                        // listed parents of the runs' clades
 #pragma unroll
   for (int k = 0; k < kCh; ++k) hsp[k] = (P.sister_on && hcl[k] >= 0 && hh[k] != 0ull) ? K.sibp[hcl[k]] : -1;
@@ -1092,7 +1098,7 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
       const int sp = hsp[k], cl = hcl[k];
       const uint64_t h = hh[k];
       bool match = false;
-      for (int i = 0; i < Pp; ++i) match = match || (sp >= 0 && sp == sh.par[i]);
+      for (int i = 0; i < Pp; ++i) match = match || (sp >= 0 && sp == lane_bcast(my_par, i));
       for (uint64_t mb = __ballot(match); mb; mb &= mb - 1) {
         const int src = __builtin_ctzll(mb);
         const int sp_r = lane_bcast(sp, src), cl_r = lane_bcast(cl, src);
@@ -1106,32 +1112,48 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
     if (lane < Pp) { sh.s1[lane] = s1; sh.s2[lane] = s2; }
     __syncthreads();
   }
+  SLAP(2);
   // the candidate pairs, crit >= k2 <=> (m_i | m_j) == um, listed so that their ranks are
-  // taken 64 at a time (one pair per lane) rather than one potential clade per step
+  // taken 64 at a time (one pair per lane): the Pp (Pp - 1) / 2 pairs are tested 64 at a
+  // time too, pair p = j (j - 1) / 2 + i (i < j) on lane p mod 64, the two masks fetched
+  // from lanes i and j (the list order does not matter: pass 1 selects by (rank, pair
+  // index), pass 2 only aggregates)
   __syncthreads();                                   // (every read of cg done)
   int nc = 0;
-  for (int i = 0; i + 1 < Pp; ++i) {
-    const bool cand = lane > i && lane < Pp && (lane_bcast(my_pm, i) | my_pm) == um;
+  const int n_pairs = Pp * (Pp - 1) / 2;
+  for (int p0 = 0; p0 < n_pairs; p0 += 64) {
+    const int p = min(p0 + lane, n_pairs - 1);
+    int j = (int)((1.0f + __fsqrt_rn(1.0f + 8.0f * (float)p)) * 0.5f);
+    j -= j * (j - 1) / 2 > p ? 1 : 0;                 // (float rounding at the row ends)
+    j += (j + 1) * j / 2 <= p ? 1 : 0;
+    const int i = p - j * (j - 1) / 2;
+    const uint64_t mi = (uint64_t)__shfl((long long)my_pm, i, 64), mj = (uint64_t)__shfl((long long)my_pm, j, 64);
+    const bool cand = p0 + lane < n_pairs && (mi | mj) == um;
     const uint64_t cb = __ballot(cand);
-    if (cand) sh.cand[nc + __popcll(cb & below)] = (unsigned short)(i | (lane << 8));
+    if (cand) sh.cand[nc + __popcll(cb & below)] = (unsigned short)(i | (j << 8));
     nc += __popcll(cb);
   }
   __syncthreads();
+  SLAP(3);
+  SSTAT(11, nc);
   // pass 1: the best candidate pair by (rank, pair index)
   double pr = -__builtin_inf();
   long long pk = -1;
-  for (int q = lane; q < nc; q += 64) {
-    const int i = sh.cand[q] & 0xFF, j = sh.cand[q] >> 8;
-    const double r = e2_rank(sh, i, j, um, Gu);
-    const long long key = (long long)i * Pp + j;
-    if (better(r, key, pr, pk)) { pr = r; pk = key; }
+  if (nc > 0) {
+    for (int q = lane; q < nc; q += 64) {
+      const int i = sh.cand[q] & 0xFF, j = sh.cand[q] >> 8;
+      const double r = e2_rank(sh, i, j, um, Gu);
+      const long long key = (long long)i * Pp + j;
+      if (better(r, key, pr, pk)) { pr = r; pk = key; }
+    }
+    each_stride([&](auto J) {
+      constexpr int js = decltype(J)::value;
+      const double r2 = xor_lanes<js>(pr);
+      const long long k2 = xor_lanes<js>(pk);
+      if (better(r2, k2, pr, pk)) { pr = r2; pk = k2; }
+    });
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double r2 = __shfl_xor(pr, off, 64);
-    const long long k2 = __shfl_xor(pk, off, 64);
-    if (better(r2, k2, pr, pk)) { pr = r2; pk = k2; }
-  }
+  SLAP(4);
   if (pk >= 0) {
     const int bi = (int)(pk / Pp), bj = (int)(pk % Pp);
     const E2Eval be = e2_eval(K, sh, bi, bj, um);
@@ -1220,9 +1242,11 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
         K.iters[c] = (int16_t)iteration;
         K.pair_evals[c] = pair_evals;
       }
+      SLAP(5);
       return true;
     }
   }
+  SLAP(5);
   // no explanation at this level (:570-583): raise, or stop at r__Root (the table is never
   // empty: explain_one ran on this contig's segments)
   if (!root && iteration + 1 <= kMaxIter) {

@@ -291,9 +291,13 @@ __global__ void k_keys_active(const SArgs S, int n_act, uint64_t* keys, int32_t*
 // sit in rank order (level 0: attachment order; later levels: act_base is handed out in
 // rank order), so sorting each contig's (key, attachment) pairs on its own -- in LDS, one
 // workgroup per contig -- gives the same sequence as one global radix sort of the level.
-// Ties keep attachment order (the pair is the sort key).  Keys are built here (no separate
-// key kernel).  Dynamic LDS: sort_cap x (8 + 4) bytes.
-constexpr int kSortMax = 4096;   // 48 KiB of LDS; larger contigs (cfg5 stress) sort faster with the radix sort
+// Ties keep attachment order.  Keys are built here (no separate key kernel).  In LDS one
+// 64-bit word per attachment: its key without the contig-rank bits (constant within the
+// contig) over its 13-bit index in the contig, so the word order is the (key, attachment)
+// order and the full key is rebuilt on the way out.  Dynamic LDS: sort_cap x 8 bytes.
+constexpr int kSortMax = 8192;   // 64 KiB of LDS (the cfg5 stress contigs, ~5,000 attachments)
+constexpr int kSortIdxBits = 13;
+static_assert(kSortMax <= (1 << kSortIdxBits), "contig-local index field");
 
 template <int NT>
 __global__ __launch_bounds__(NT) void k_sort_contig(const SArgs S, int n_act,
@@ -302,8 +306,8 @@ __global__ __launch_bounds__(NT) void k_sort_contig(const SArgs S, int n_act,
   lvl_counts(S, n_act, n_keys_);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint64_t* sk = reinterpret_cast<uint64_t*>(smem);
-  int32_t* sv = reinterpret_cast<int32_t*>(sk + S.sort_cap);
   __shared__ int s_red[NT / 64];
+  const uint64_t rank_shift = (uint64_t)(S.key_tb + S.key_lb);
   const int tid = threadIdx.x;
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const int c = S.act ? S.act[cr] : cr;
@@ -316,10 +320,8 @@ __global__ __launch_bounds__(NT) void k_sort_contig(const SArgs S, int n_act,
     const int64_t base = S.act_base ? S.act_base[cr] : a0;   // level 0: own offsets
     int n2 = 2;
     while (n2 < n) n2 <<= 1;
-    for (int t = tid; t < n2; t += NT) {
-      sk[t] = t < n ? make_key(S, cr, (int)(a0 + t)) : ~0ull;
-      sv[t] = t < n ? (int)(a0 + t) : 0x7fffffff;
-    }
+    for (int t = tid; t < n2; t += NT)
+      sk[t] = t < n ? (make_key(S, 0, (int)(a0 + t)) << kSortIdxBits) | (uint64_t)t : ~0ull;
     __syncthreads();
     for (int k = 2; k <= n2; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
@@ -328,18 +330,18 @@ __global__ __launch_bounds__(NT) void k_sort_contig(const SArgs S, int n_act,
           const int hi = lo | j;
           const bool up = (lo & k) == 0;
           const uint64_t ka = sk[lo], kb = sk[hi];
-          const int32_t va = sv[lo], vb = sv[hi];
-          const bool gt = ka > kb || (ka == kb && va > vb);
-          if (gt == up) { sk[lo] = kb; sk[hi] = ka; sv[lo] = vb; sv[hi] = va; }
+          if ((ka > kb) == up) { sk[lo] = kb; sk[hi] = ka; }
         }
         __syncthreads();
       }
     }
     int ns = 0;                                      // distinct keys = segments
+    const uint64_t crank_bits = (uint64_t)cr << rank_shift;
     for (int t = tid; t < n; t += NT) {
-      keys[base + t] = sk[t];
-      vals[base + t] = sv[t];
-      ns += (t == 0 || sk[t] != sk[t - 1]) ? 1 : 0;
+      const uint64_t w = sk[t];
+      keys[base + t] = crank_bits | (w >> kSortIdxBits);
+      vals[base + t] = (int)(a0 + (int64_t)(w & ((1u << kSortIdxBits) - 1)));
+      ns += (t == 0 || (w >> kSortIdxBits) != (sk[t - 1] >> kSortIdxBits)) ? 1 : 0;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off, 64);
@@ -1189,7 +1191,34 @@ __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int lev
   }
 }
 
+// Diagnostic build only (-DWF_STAMPS): shader-clock laps of sp_two (the compact hand-over's
+// explain_two) on every 8th contig it decides (scripts/wave_stamps.py reads them).
+#ifdef WF_STAMPS
+__device__ unsigned long long g_sstamps[16];
+#define SLAP_MARK(c) unsigned long long slap_ = __builtin_amdgcn_s_memtime(); const bool ssamp_ = ((c) & 7) == 0
+#define SLAP(i)                                                                     \
+  do {                                                                              \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
+    if (ssamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_sstamps[i], n_ - slap_);    \
+    slap_ = n_;                                                                     \
+  } while (0)
+#define SSTAT(i, v) do { if (ssamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_sstamps[i], (unsigned long long)(v)); } while (0)
+#else
+#define SLAP_MARK(c) do {} while (0)
+#define SLAP(i) do {} while (0)
+#define SSTAT(i, v) do {} while (0)
+#endif
 #include "wf_sparse.h"
+#ifdef WF_STAMPS
+extern "C" int wf_stamps_read_sparse(unsigned long long* out, int n) {
+  if (n > 16) n = 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
+}
+extern "C" int wf_stamps_reset_sparse(void) {
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sstamps), z, sizeof z) == hipSuccess ? 0 : -2;
+}
+#endif
 
 int bits_for(int64_t v) {   // bits to hold values 0..v
   int b = 1;
@@ -1827,7 +1856,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   // per-contig LDS sort when every contig's attachments fit one workgroup's LDS (else a
   // device radix sort of the whole level)
   sa.sort_cap = 0;
-  if (max_att <= kSortMax) {
+  if (max_att <= kSortMax && sa.key_tb + sa.key_lb + kSortIdxBits <= 64) {
     sa.sort_cap = 2;
     while (sa.sort_cap < max_att) sa.sort_cap <<= 1;
   }
@@ -1963,21 +1992,12 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     if (n_keys > 0) {
       size_t need = st->tmp.n;
       if (sa.sort_cap > 0) {
-        const size_t lds = (size_t)sa.sort_cap * 12;
-        if (lds > 64 * 1024) {
-          static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<64>),
-                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                             (int)(kSortMax * 12));
-          static const hipError_t attr4 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_contig<256>),
-                                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                              (int)(kSortMax * 12));
-          ST_TRY(attr);
-          ST_TRY(attr4);
-        }
+        const size_t lds = (size_t)sa.sort_cap * 8;
         const int per_cu = std::min(32, std::max(1, (int)((160 * 1024) / lds)));
-        // level 0: one wave per contig (10^4+ contigs fill the chip); later levels have
-        // few contigs, so four waves shorten each contig's sort
-        if (level == 0)
+        // level 0: one wave per contig (10^4+ contigs fill the chip) unless the contigs are
+        // long (> 2,048 attachments: the cfg5 stress shape); later levels have few contigs,
+        // so four waves shorten each contig's sort
+        if (level == 0 && sa.sort_cap <= 2048)
           hipLaunchKernelGGL(k_sort_contig<64>, dim3(std::min(n_act, st->cus * per_cu)), dim3(64), lds, s,
                              sa, n_act, level, kbuf.Current(), vbuf.Current());
         else
