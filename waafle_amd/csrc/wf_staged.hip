@@ -295,7 +295,10 @@ __global__ void k_keys_active(const SArgs S, int n_act, uint64_t* keys, int32_t*
 // 64-bit word per attachment: its key without the contig-rank bits (constant within the
 // contig) over its 13-bit index in the contig, so the word order is the (key, attachment)
 // order and the full key is rebuilt on the way out.  Dynamic LDS: sort_cap x 8 bytes.
-constexpr int kSortMax = 8192;   // 64 KiB of LDS (the cfg5 stress contigs, ~5,000 attachments)
+// 32 KiB of LDS.  8,192 (the cfg5 stress contigs, ~5,000 attachments) measured slower than
+// the device radix sort at cfg5 (r4k: 14.1 against 12.0 ms per 6,250-contig pass: 2 workgroups
+// per CU, 91 barrier-separated LDS stages, then k_seg_build's wave walking 5,000 keys)
+constexpr int kSortMax = 4096;
 constexpr int kSortIdxBits = 13;
 static_assert(kSortMax <= (1 << kSortIdxBits), "contig-local index field");
 
@@ -1994,10 +1997,9 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       if (sa.sort_cap > 0) {
         const size_t lds = (size_t)sa.sort_cap * 8;
         const int per_cu = std::min(32, std::max(1, (int)((160 * 1024) / lds)));
-        // level 0: one wave per contig (10^4+ contigs fill the chip) unless the contigs are
-        // long (> 2,048 attachments: the cfg5 stress shape); later levels have few contigs,
-        // so four waves shorten each contig's sort
-        if (level == 0 && sa.sort_cap <= 2048)
+        // level 0: one wave per contig (10^4+ contigs fill the chip); later levels have
+        // few contigs, so four waves shorten each contig's sort
+        if (level == 0)
           hipLaunchKernelGGL(k_sort_contig<64>, dim3(std::min(n_act, st->cus * per_cu)), dim3(64), lds, s,
                              sa, n_act, level, kbuf.Current(), vbuf.Current());
         else
