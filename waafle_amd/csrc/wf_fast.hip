@@ -394,7 +394,7 @@ __device__ __noinline__ double lane_seg_mean(Src src, int kb, int ke, LT lt, int
 // lane_seg_mean; a round costs one leaf per lane instead of a whole segment.  W.z maps a
 // round's start position to its segment's lane.  Returns the mean on the segment's lane.
 template <int R, class Src>
-__device__ __noinline__ double flat_leaf_means(Src src, const uint32_t* lut, uint64_t mlist, int kb, int ke,
+__device__ __forceinline__ double flat_leaf_means(Src src, const uint32_t* lut, uint64_t mlist, int kb, int ke,
                                                int nl, int len, WaveRunsT<R>& W) {
   const int lane = lane_id();
   double mean = 0.0;
@@ -1296,14 +1296,17 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
           WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));
           uint64_t mlist = __ballot(multi);
-          if (ROLL && WF_FLAT_LEAVES && mlist != 0ull) {
+          constexpr bool kFlat = ROLL && WF_FLAT_LEAVES;   // (its only multi path: the others compile out)
+          if constexpr (kFlat) {
             // roll-up levels, where a segment gathers the attachments of many clades: one
             // numpy leaf per lane over all of the chunk's multi-attachment segments
-            int kb = 0, ke = 0;
-            if (multi) { kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att; }
-            const double m = flat_leaf_means(Src{F.key, F.lohi, F.sc}, F.lut + F.lbase[multi ? g : 0], mlist,
-                                             kb, ke, nl, len, F.runs());
-            if (multi) v[s] = m;
+            if (mlist != 0ull) {
+              int kb = 0, ke = 0;
+              if (multi) { kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att; }
+              const double m = flat_leaf_means(Src{F.key, F.lohi, F.sc}, F.lut + F.lbase[multi ? g : 0], mlist,
+                                               kb, ke, nl, len, F.runs());
+              if (multi) v[s] = m;
+            }
             mlist = 0;
           } else if ((FULL || ROLL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
             // several multi-attachment segments: one lane each, not the whole wave per segment
@@ -1313,6 +1316,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
             }
             mlist = 0;
           }
+          if constexpr (!kFlat)
           for (uint64_t mm = mlist; mm; mm &= mm - 1) {  // the wave, one segment each
             const int src = __builtin_ctzll(mm);
             const int s2 = lane_bcast(s, src);
