@@ -778,7 +778,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
                                              const int32_t* list, int n_list, const int64_t* n_dev, int rollup,
                                              int start_level_arg) {
   static_assert(!(FULL && ROLL), "the roll-up passes are first-form launches");
-  const int start_level = ROLL ? start_level_arg : 0;
+  const int start_level = ROLL ? start_level_arg : 0;   // (ROLL: always >= 1)
   if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WaveSmem<CAP, FULL>& F = *reinterpret_cast<WaveSmem<CAP, FULL>*>(smem);
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
     const KArgs& K = S.k;
     const DevParams& P = K.p;
     const int nsys = K.n_sys;
-    const bool ann_on = start_level == 0 && nsys > 0;  // annotations: level 0 only (never raised, :383-392)
+    const bool ann_on = !ROLL && nsys > 0;            // annotations: level 0 only (never raised, :383-392)
     // --weak-loci assign-unknown: the second form leaves every contig the first one handed
     // over to the staged kernels (its pend / counts stand); they carry the virtual row
     if (FULL && P.weak == 2) continue;
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           }
           r_n[b] = n;
           r_am[b] = am;
-          if (start_level > 0 && n > 0) r_cl[b] = S.anc[r_cl[b]];   // parent^(jump + level), :431-445
+          if (ROLL && n > 0) r_cl[b] = S.anc[r_cl[b]];   // parent^(jump + level), :431-445
         }
       }
     for (int bq = 0; bq < kHB && hq + 64 * bq < h1; ++bq) {
@@ -952,7 +952,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
             am |= 1ull << g;
           }
         }
-        if (start_level > 0 && n > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
+        if (ROLL && n > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
       } else if (!ordered && h < h1 && scv >= P.min_scov) {
         for (int g = 0; g < G; ++g) {
           int lo, len, st;
@@ -968,12 +968,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
             if (g < kLoc0) am |= 1ull << g;
           }
         }
-        if (start_level > 0 && n > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
+        if (ROLL && n > 0) clade = S.anc[clade];   // parent^(jump + level), :431-445
       }
       int total;
       const int o = wave_excl_scan(n, &total);
       if (!staged && n > 0 && n_att + o + n <= CAP) {
-        if (start_level == 0)
+        if (!ROLL)
           for (int j = 0; j < P.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
         const bool ann = m != 0 && sc >= P.annot_ref;
         int slot = n_att + o;
@@ -1021,7 +1021,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
     }
     WLAP(2);
     // ---- levels: sort, segments, means, explain_one [, explain_two, roll-up] ----
-    int64_t pair_evals = (start_level > 0 && lane == 0) ? K.pair_evals[c] : 0;
+    int64_t pair_evals = (ROLL && lane == 0) ? K.pair_evals[c] : 0;
     pair_evals = lane_bcast((uint64_t)pair_evals, 0);
     bool seed = false;                                 // raised at level 0: staged level 1 seed
     bool dumped = false;                               // segment table handed to k_dump_sparse
