@@ -1111,7 +1111,13 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         b = wave_or_dpp(b);
         return b;
       };
-      auto best_score = [&](int t) -> double {       // upper bound of segment t's mean
+      // Upper bound of segment t's mean.  The roll-up launches, which run several pruned
+      // passes over segments of several attachments each, compute it once per segment in
+      // the prune setup and keep it in the not-evaluated marker, v[t] = -1 - ub (any v < 0
+      // is "not evaluated"; -1 - (-1 - ub) may lose ub's bits below 2^-52, far inside the
+      // bounds' 1e-12 slack); level 0 scans the attachments when asked (most of its
+      // contigs never ask).
+      auto scan_best = [&](int t) -> double {
         const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
         double ub = 0.0;
         if (kDescOrder) {                            // best first: past its top bits, nothing higher
@@ -1125,6 +1131,9 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         }
         for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[slot_at(q)]);
         return ub;
+      };
+      auto best_score = [&](int t) -> double {       // (callers: v[t] < 0)
+        return ROLL ? -1.0 - v[t] : scan_best(t);
       };
       int n_pass0 = -1;                                // pass 0's list, built with the run sizes
       if (prune) {
@@ -1156,7 +1165,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           carry = hd[i] ? 64 * i + __ffsll((unsigned long long)hd[i]) - 1 : carry;
           rsz[i] = re - rs[i];
           if (t < ns) {
-            v[t] = -1.0;                               // not evaluated
+            v[t] = ROLL ? -1.0 - scan_best(t) : -1.0;  // not evaluated
             rc[t] = (uint8_t)rsz[i];
           }
         }
