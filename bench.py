@@ -79,7 +79,7 @@ def parse_args():
     ap.add_argument("--traffic-json", default=None)
     ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r04", "cfg4_valu.json"),
                     help="PMC VALU counts of the main pass (scripts/pmc_main.py, optional)")
-    ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r03_k2_pmc.json"),
+    ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r04", "k2_pmc.json"),
                     help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
     return ap.parse_args()
 
