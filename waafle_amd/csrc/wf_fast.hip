@@ -47,6 +47,12 @@
 #ifndef WF_ROLL_WAVES
 #define WF_ROLL_WAVES 4
 #endif
+// level 0: 1 moves ranges and scores into sorted order with the keys (as the roll-up
+// launches do); 0 (default) sorts the keys alone.  Same box, alternating (r4w): level-0
+// launch 9.19 / 9.25 ms keys alone against 9.25 / 9.26 moved.
+#ifndef WF_L0_PERMUTE
+#define WF_L0_PERMUTE 0
+#endif
 // roll-up launches: 1 keeps attachments in descending-score order (rank_slice, SegAttT's
 // early exits); 0 (default): sorted-order data as level 0.  Same-box A/B at cfg4 (r4j):
 // 16.04 / 16.09 ms with, 16.05 without -- the extra sort eats what the early exits save.
@@ -348,6 +354,18 @@ struct SliceSrc {
   const uint32_t* lohi;
   const double* sc;
   __device__ __forceinline__ int idx(int t) const { return t; }
+  __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
+    const uint32_t w = lohi[a];
+    l = lo16(w); h = hi16(w); v = sc[a];
+  }
+};
+// Level 0 without the data move: sorted position t -> its key's slot field -> range, score.
+struct SliceSrcKey {
+  [[maybe_unused]] static constexpr bool kDesc = false;
+  const uint32_t* key;
+  const uint32_t* lohi;
+  const double* sc;
+  __device__ __forceinline__ int idx(int t) const { return (int)(key[t] & kSlotMask); }
   __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
     const uint32_t w = lohi[a];
     l = lo16(w); h = hi16(w); v = sc[a];
@@ -1028,9 +1046,13 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
     // roll-up launches: attachments at descending-score positions (rank_slice), addressed
     // through their keys' slot fields from here on; level 0 sorts them into key order
     constexpr bool kDescOrder = ROLL && WF_ROLL_DESC;
-    using Src = typename std::conditional<kDescOrder, SliceSrcDesc, SliceSrc>::type;
+    // level 0 (WF_L0_PERMUTE 0): keys sorted alone, attachments reached through the keys'
+    // slot fields (its few multi-attachment segments do not repay moving the data)
+    constexpr bool kKeyOrder = !kDescOrder && !FULL && !ROLL && !WF_L0_PERMUTE;
+    using Src = typename std::conditional<kDescOrder, SliceSrcDesc,
+                                          typename std::conditional<kKeyOrder, SliceSrcKey, SliceSrc>::type>::type;
     if (kDescOrder && !staged && n_att > 0) rank_slice<(CAP + 63) / 64>(F, n_att);
-    auto slot_at = [&](int t) -> int { return kDescOrder ? (int)(F.key[t] & kSlotMask) : t; };
+    auto slot_at = [&](int t) -> int { return (kDescOrder || kKeyOrder) ? (int)(F.key[t] & kSlotMask) : t; };
     for (int level = start_level; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
       const int iteration = level + 1;
       if (level > start_level) {                     // roll up (:431-445): re-key to the parent clade
@@ -1041,7 +1063,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         }
         wave_sync();
       }
-      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64, !kDescOrder>(F, n_att);   // one network: code size
+      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64, !kDescOrder && !kKeyOrder>(F, n_att);   // one network: code size
       WLAP(3);
       // ---- segments = runs of equal (clade, locus) ----
       int ns = 0;
