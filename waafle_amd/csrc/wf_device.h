@@ -1022,18 +1022,20 @@ struct ValSrc {
   }
 };
 
-template <class Src>
+// NREG: attachments held in registers (segments of at most NREG attachments; the rest are
+// read from the source each time)
+template <class Src, int NREG = kRegAtt>
 struct SegAttT {
   int kb, ke;
   bool reg;
-  int lo[kRegAtt], hi[kRegAtt];
-  double sc[kRegAtt];
+  int lo[NREG], hi[NREG];
+  double sc[NREG];
 
   __device__ __forceinline__ void load(const Src& C, int kb_, int ke_) {
     kb = kb_; ke = ke_;
-    reg = ke - kb <= kRegAtt;
+    reg = ke - kb <= NREG;
 #pragma unroll
-    for (int i = 0; i < kRegAtt; ++i) {
+    for (int i = 0; i < NREG; ++i) {
       const bool use = reg && kb + i < ke;
       int l = 0, h = 0;
       double v = 0.0;
@@ -1050,7 +1052,7 @@ struct SegAttT {
     double v = 0.0;
     if (reg) {
 #pragma unroll
-      for (int i = 0; i < kRegAtt; ++i)
+      for (int i = 0; i < NREG; ++i)
         if (x >= lo[i] && x < hi[i]) v = sc[i] > v ? sc[i] : v;
     } else {
       long long vtb = -1;                  // (kDesc: top bits of the first cover's score)
@@ -1087,7 +1089,7 @@ struct SegAttT {
   __device__ __forceinline__ int classify(const Src& C, int st, int m, double& F, int& plo,
                                           int& phi, double& ps) const {
     const int be = st + (m << 3);
-    int na = REG ? kRegAtt : ke - kb;
+    int na = REG ? NREG : ke - kb;
     F = 0.0;
     long long ftb = -1;
 #pragma unroll
@@ -1134,7 +1136,7 @@ struct SegAttT {
   // Stride accumulator c of the body [st, st+8m): sequential sum of its m sites.
   template <bool REG>
   __device__ __forceinline__ double stride_sum_t(const Src& C, int st, int m, int c) const {
-    const int be = st + (m << 3), na = REG ? kRegAtt : ke - kb;
+    const int be = st + (m << 3), na = REG ? NREG : ke - kb;
     double r = 0.0;
     for (int x = st; x < be;) {
       double v = 0.0;
@@ -1185,7 +1187,7 @@ struct SegAttT {
   // the eight independent chains interleave.
   template <bool REG>
   __device__ __forceinline__ double runs_body(const Src& C, int st, int m) const {
-    const int be = st + (m << 3), na = REG ? kRegAtt : ke - kb;
+    const int be = st + (m << 3), na = REG ? NREG : ke - kb;
     double r[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) r[c] = 0.0;

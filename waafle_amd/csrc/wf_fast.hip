@@ -437,7 +437,7 @@ __device__ __forceinline__ double flat_leaf_means(Src src, const uint32_t* lut, 
     const uintptr_t olut = (uintptr_t)__shfl((long long)(uintptr_t)lut, own, 64);
     if (lane < used) {
       const int4 e = PackedLut{reinterpret_cast<const uint32_t*>(olut)}(lane - p);
-      SegAttT<Src> at;
+      SegAttT<Src, 1> at;                             // (multi segments: read from LDS)
       at.load(src, okb, oke);
       W.lv[lane] = at.leaf(src, e.x, e.y);
     }
