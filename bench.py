@@ -4,16 +4,20 @@ Main line (`value`): BASELINE.json configs[3], the north-star configuration -- s
 1,000,000 contigs x 10 genes x 2000 clades, 20 decoy hits per gene (210 M hits), default
 waafle_orgscorer parameters, roll-up enabled, one wf_score pass over the whole batch with
 inputs resident in HBM.  For N GPUs (torch.distributed.run, one process per GPU) the SAME
-1M-contig batch is split into N contiguous contig ranges (strong scaling); contigs are
-independent, so there is no data-path collective -- only the barrier and the max-over-ranks
-timing.
+1M-contig batch is split into N contiguous contig ranges, rank r scoring contigs
+[r n / N, (r + 1) n / N) (strong scaling, `value` = 1M / the slowest rank's pass time);
+contigs are independent, so there is no data-path collective -- only the barrier, the
+max-over-ranks timing and the sums of the call counts.  At N > 1 the line also carries
+`weak`: every rank its own 1M contigs (rank r: [r n, (r + 1) n) of one N n-contig stream),
+value = N n / the slowest rank's pass time.
 
 k2 leg (`k2`, top-level `k2_pair_evals_per_sec`): BASELINE.json configs[4], the explain_two
 stress set (20 genes, 5000 clades, ~12.5 M reference clade pairs per contig).  Every rank
-times its 6,250-contig share of the 50,000 contigs (the per-GPU share at 8 GPUs: at N = 8
+times a 6,250-contig share of the 50,000 contigs (the per-GPU share at 8 GPUs: at N = 8
 the leg is the whole config), with the per-phase HIP-event timing of the library
 (wf_timing.phase_ms): the explain_two kernels' time, the B_k2 bytes they stand for, and
-the whole pass.
+the whole pass.  Its HBM fraction is per GPU: the bytes of all ranks / the slowest rank's
+explain_two time / (N x 8 TB/s).
 
 Each rank generates its contig ranges before the GPU is touched (synth.generate_batch:
 every chunk from its own seed, in parallel worker processes).  cfg2 / cfg3 / cfg5 stay
@@ -76,6 +80,8 @@ def parse_args():
     ap.add_argument("--device-map", default=None,
                     help="device of each local rank, e.g. '0,0' (two ranks on device 0: a "
                          "rehearsal of the N > 1 branch on one GPU, not a scaling number)")
+    ap.add_argument("--weak", type=int, default=1,
+                    help="N > 1: also time the weak-scaling workload (every rank its own n contigs)")
     ap.add_argument("--traffic-json", default=None)
     ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r04", "cfg4_valu.json"),
                     help="PMC VALU counts of the main pass (scripts/pmc_main.py, optional)")
@@ -318,10 +324,12 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
         t = torch.tensor(v, device=cdev)
         dist.all_reduce(t)
         v = t.cpu().numpy()
-    k2_s = np.array([k2_ms * 1e-3])
-    k2_max = float(wdist_max(k2_s[0], dist, cdev))
+    k2_max = float(wdist_max(k2_ms * 1e-3, dist, cdev))
     pass_s = elapsed / steps
-    achieved = v[1] / k2_max / 1e9
+    # per GPU: every rank's B_k2 over the slowest rank's explain_two time, against the
+    # peak of the `world` devices that moved them
+    achieved = v[1] / k2_max / 1e9 / world
+    own = counts["b_k2_bytes"] / max(k2_ms * 1e-3, 1e-12) / 1e9
     out = {
         "source": "this run: {} timed passes, HIP events per phase (wf_timing)".format(steps),
         "workload": "cfg5 stress: {} contigs per GPU x {} GPUs (rank r: contigs "
@@ -339,7 +347,10 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
         "b_k2_bytes": v[1], "b_k2_rule": "sum over explain_two contigs of P_pot * G * 8 "
                                         "(SURVEY 8(d): the potential clades' score rows)",
         "hbm": {"achieved_GBs": achieved, "peak_GBs": HBM_PEAK_GBS,
-                "frac": achieved / HBM_PEAK_GBS},
+                "frac": achieved / HBM_PEAK_GBS,
+                "rule": "sum of B_k2 over ranks / max explain_two time over ranks / "
+                        "n_gpus: per GPU",
+                "rank0": {"achieved_GBs": own, "frac": own / HBM_PEAK_GBS}},
         "p_pot_max": counts["p_pot_max"],
     }
     if pmc_json and os.path.exists(pmc_json):
@@ -368,14 +379,18 @@ def main():
     workers = max(1, min(16, cores // world))
 
     # ---- generate this rank's contigs BEFORE touching the GPU (fork-safe) ----
-    # Weak scaling (contigs are independent, no data-path collective): every rank scores the
-    # configuration's full per-GPU workload, rank r the contigs [r n, (r + 1) n) of one
-    # seeded stream of world * n contigs
-    n_per = args.contigs or synth.CONFIGS[args.config]["n"]
-    n_total = n_per * world
-    a, b = rank * n_per, (rank + 1) * n_per
+    # Strong scaling (the headline): the configuration's n contigs split over the ranks,
+    # rank r the contigs [r n / N, (r + 1) n / N).  Weak scaling (N > 1, `weak`): every rank
+    # its own n contigs, [r n, (r + 1) n) of one seeded stream of N n contigs.
+    n_cfg = args.contigs or synth.CONFIGS[args.config]["n"]
+    n_total = n_cfg
+    a, b = rank * n_cfg // world, (rank + 1) * n_cfg // world
     t_gen = time.perf_counter()
-    batch, tax = synth.generate_batch(args.config, a, b, workers=workers, n_total=n_total)
+    batch, tax = synth.generate_batch(args.config, a, b, workers=workers, n_total=n_cfg)
+    wbatch = None
+    if world > 1 and args.weak:
+        wbatch, _ = synth.generate_batch(args.config, rank * n_cfg, (rank + 1) * n_cfg,
+                                         workers=workers, n_total=world * n_cfg)
     kbatch = ktax = None
     if args.k2_contigs > 0:
         k0 = (rank * args.k2_contigs) % synth.CONFIGS["cfg5"]["n"]
@@ -437,6 +452,19 @@ def main():
     calls, pe, iters = db.host("call"), db.host("pair_evals"), db.host("iterations")
     del db
     torch.cuda.empty_cache()
+    weak = None
+    if wbatch is not None:
+        wdb = DeviceBatch(wbatch, dev)
+        w_el, _ = timed_passes(so, h, chk, wdb, params, args.steps, args.warmup, dist, dev, cdev)
+        del wdb
+        torch.cuda.empty_cache()
+        weak = {"value": world * n_cfg / (w_el / args.steps), "unit": "contigs/s",
+                "ms_per_step": w_el / args.steps * 1e3, "contigs_total": world * n_cfg,
+                "contigs_per_gpu": wbatch.n_contigs, "hits_per_gpu": wbatch.n_hits,
+                "scaling": "weak",
+                "workload": "every rank its own {} contigs ([r n, (r + 1) n) of one {}-contig "
+                            "stream), same flags, same timing".format(n_cfg, world * n_cfg)}
+        del wbatch
     pairs = float(pe.sum())
     k2_counts = k2_algorithmic(pe, batch)
     if dist:          # whole-job counts
@@ -490,15 +518,17 @@ def main():
         "metric": "contigs scored/sec + k2 clade-pair evals/sec at 1/2/4/8 MI355X vs CPU ref",
         "value": value, "unit": "contigs/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded generator, SURVEY §8(d) shapes)",
-        "config": {"workload": "{}: {} contigs x {} genes x {} clades per GPU, {} hits{}, {}"
-                               .format(args.config, n_per, spec["genes"], spec["clades"], NH,
-                                       "" if world == 1 else " on rank 0",
+        "config": {"workload": "{}: {} contigs x {} genes x {} clades{}, {} hits{}, {}"
+                               .format(args.config, n_cfg, spec["genes"], spec["clades"],
+                                       "" if world == 1 else " split over {} GPUs".format(world),
+                                       NH, "" if world == 1 else " on rank 0",
                                        "flags " + args.flags if args.flags else "default flags"),
                    "contigs_total": n_total, "contigs_per_gpu": N, "hits_per_gpu": NH,
-                   "parallelism": "dp{} (each rank its own contigs, no data-path collective)"
-                                  .format(world)},
+                   "parallelism": "dp{} (contig ranges [r n/N, (r+1) n/N), no data-path "
+                                  "collective)".format(world)},
+        "weak": weak,
         "k2_pair_evals_per_sec": None,
         "k2_pair_evals_note": "reference-equivalent count: sum of P_pot(P_pot-1)/2 over "
                               "explain_two calls (orgscorer.py:606-608 score(c1,c2) calls), "

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 3
+#define WF_ABI_VERSION 4   /* 4: WF_OPT_SPARSE_BIG 0/1 retired, WF_PHASE_ROLLUP, WF_OPT_WAVE_TWO / _DUMP_CAP */
 
 enum wf_status {
   WF_OK = 0,
@@ -43,10 +43,14 @@ enum wf_status {
 enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
 
 /* Execution form of wf_score (the results are identical).
- * WF_MODE_LEVEL0 (default): per-contig wave kernels carry level 0 (explain_one, then
- *   explain_two) in LDS; contigs that roll up, or exceed a wave's LDS slice, continue in the
- *   staged kernels.
- * WF_MODE_WAVES: as LEVEL0, but the wave kernel also carries the roll-up levels.
+ * WF_MODE_LEVEL0 (default): per-contig wave kernels carry level 0 in LDS (explain_one in
+ *   the wave; explain_two from the segment table it hands over, k_dump_sparse), and every
+ *   roll-up level is one more launch of the same wave form over the contigs the level before
+ *   raised (WF_OPT_WAVE_TWO 1).  Only contigs that exceed a wave's LDS slice (attachments,
+ *   loci, leaf tables) or the hand-over tables continue in the second wave form and then
+ *   the staged kernels.
+ * WF_MODE_WAVES: the second (FULL) wave form carries explain_two and the roll-up levels in
+ *   its LDS slice.
  * WF_MODE_STAGED: every contig through the staged kernels (one kernel per phase over all
  *   contigs: attachments, per-contig sort, segment means, decisions; one pass per level).
  * The ABI-1 WF_MODE_FUSED form (1) stays retired; wf_set_mode rejects it. */

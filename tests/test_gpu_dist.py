@@ -79,7 +79,9 @@ def test_two_ranks_one_device_match_one_call(tmp_path):
 
 def test_bench_two_ranks_on_one_device(tmp_path):
     """bench.py's N > 1 branch under torch.distributed.run with gloo and --device-map 0,0:
-    one JSON line from rank 0, labelled as a rehearsal (not a scaling number)."""
+    one JSON line from rank 0, labelled as a rehearsal (not a scaling number); the headline
+    splits the configuration's contigs over the ranks (strong scaling), `weak` gives every
+    rank its own, and the k2 leg's HBM fraction is per GPU."""
     out = tmp_path / "bench2.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
@@ -93,12 +95,20 @@ def test_bench_two_ranks_on_one_device(tmp_path):
     assert len(lines) == 1
     d = json.loads(lines[0])
     out.write_text(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak"
-    assert d["config"]["contigs_total"] == 40000 and d["config"]["contigs_per_gpu"] == 20000
+    # strong scaling: the 20,000 contigs split 10,000 / 10,000; weak: each rank its own 20,000
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["contigs_total"] == 20000 and d["config"]["contigs_per_gpu"] == 10000
     assert d["ranks"]["backend"] == "gloo" and d["ranks"]["devices"] == [0, 0]
     assert "not a scaling number" in d["ranks"]["note"]
-    assert d["calls"]["lgt"] + d["calls"]["no_lgt"] + d["calls"]["unclassified"] == 40000
-    assert d["k2"]["contigs"] == 400
+    assert d["calls"]["lgt"] + d["calls"]["no_lgt"] + d["calls"]["unclassified"] == 20000
+    assert abs(d["value"] - 20000 / (d["ms_per_step"] * 1e-3)) <= 1e-6 * d["value"]
+    w = d["weak"]
+    assert w["scaling"] == "weak" and w["contigs_total"] == 40000 and w["contigs_per_gpu"] == 20000
+    # the k2 leg: per-GPU fraction = all ranks' bytes / slowest explain_two time / (2 x peak)
+    k = d["k2"]
+    assert k["contigs"] == 400
+    want = k["b_k2_bytes"] / (k["explain_two_ms_per_pass"] * 1e-3) / 1e9 / 2 / k["hbm"]["peak_GBs"]
+    assert abs(k["hbm"]["frac"] - want) <= 1e-9 * max(want, 1e-30)
     if os.environ.get("WAAFLE_KEEP_BENCH2"):
         with open(os.environ["WAAFLE_KEEP_BENCH2"], "w") as fh:
             fh.write(lines[0] + "\n")

@@ -138,6 +138,31 @@ def test_attachment_limit_splits_batch_like_unsplit():
     assert_same(got, want, batch)
 
 
+def test_attachment_limit_default_mode_oversized_contigs():
+    """The default form (WF_MODE_LEVEL0) with contigs past the wave slice's capacity
+    (8 genes x 71 hits = 568 attachments > 512): the wave form hands them to the staged
+    kernels, whose attachments then exceed a low WF_OPT_ATT_LIMIT -> WF_E_TOOBIG; the split
+    records equal the unsplit call's (the path the full 50,000-contig cfg5 batch takes)."""
+    small = synth.generate(n=600, genes=8, clades=200, seed=83)
+    big = synth.generate(n=120, genes=8, clades=200, seed=83, decoys=70)
+    (b1, tax), (b2, tax2) = synth.to_batch(small), synth.to_batch(big)
+    assert list(tax.names) == list(tax2.names)
+    batch = concat_batches([b1, b2, b1.slice(0, 200)])
+    assert batch.max_hits > 512
+    want = score(batch, tax)
+    assert not want.status.any()
+    s = engine.GpuScorer(0, options={lib.OPT_ATT_LIMIT: 20000})
+    s.set_taxonomy(tax)
+    with pytest.raises(lib.WaafleHipError) as ei:
+        s._score_once(batch, PARAMS)
+    assert ei.value.code == lib.WF_E_TOOBIG
+    got = s.score(batch, PARAMS)
+    s.close()
+    assert_same(got, want, batch)
+    staged = score(batch, tax, mode="staged")
+    assert_same(staged, want, batch)
+
+
 def test_option_validation():
     s = engine.GpuScorer(0)
     for opt, val in ((lib.OPT_ATT_LIMIT, 0), (lib.OPT_ATT_LIMIT, 1 << 31), (lib.OPT_SPARSE_BIG, 4),

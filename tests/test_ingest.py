@@ -175,3 +175,16 @@ def test_empty_inputs(tmp_path):
     a, b = both(paths, 100)
     assert_same(a, b)
     assert a[0].n_contigs == 0 and a[0].n_hits == 0
+
+
+def test_dense_short_annotations_match(tmp_path):
+    """Annotation items as short as "|=" (an empty system and value, utils.py:239-241): a
+    row dense with them fills the annotation buffer at 2 bytes per item; the native parser
+    must hold every one of them (a 4-byte-per-item reservation dropped them)."""
+    dense = "g1|s__A" + "|=" * 400 + "|a=" * 50
+    blast = _row("c1", dense) + _row("c1", "g2|s__B|=|=") + _row("c2", "g5|s__B" + "|=" * 300)
+    paths = _write(tmp_path, FNA, blast, GFF)
+    native_only(paths, 100)                            # the native path (no fallback)
+    a, b = both(paths, 100)
+    assert_same(a, b)
+    assert a[0].systems == ["", "a"]

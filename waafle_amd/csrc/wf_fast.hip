@@ -16,12 +16,15 @@
 //                       LGT checks and meld_two (:633-744, eval_two of wf_device.h), and the
 //                       roll-up loop (:431-445, :566-583) -- attachments re-keyed to the parent
 //                       clade in LDS, level after level
-// A contig neither can finish (more attachments than a slice holds, more than 64 loci, a
-// leaf table, segment or explain_two state the slice cannot hold) is handed to the staged
-// path (wf_staged.hip) with its attachment and leaf counts; the staged level 0 then runs on
-// those contigs only.  A contig k_wave<CAP, true> evaluated and raised at level 0 (roll-up
-// not carried here) is handed over as a seed of the staged level 1.  Contigs finished here never write attachments, keys or segment
-// records to HBM: their traffic is the hits and loci read once plus the result record.
+//   k_wave<CAP, false, true> (ROLL)  roll-up level L >= 1 of the contigs the level before
+//                       raised (WF_MODE_LEVEL0): hits re-attached with clade anc[taxon]
+// In WF_MODE_LEVEL0 the first form hands a contig explain_one leaves open to k_dump_sparse
+// with its segment table (explain_two there; a raised contig joins the next ROLL launch's
+// list).  A contig no wave form can finish (more attachments than a slice holds, more
+// than 64 loci, a leaf table, segment or explain_two state the slice cannot hold) is handed
+// to the staged path (wf_staged.hip) with its attachment and leaf counts; the staged level
+// 0 then runs on those contigs only.  Contigs finished here never write attachments, keys
+// or segment records to HBM: their traffic is the hits and loci read once plus the record.
 #include <algorithm>
 #include <cstdlib>
 
@@ -785,9 +788,10 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
 }
 
 template <int CAP, bool FULL, bool ROLL = false>
-// rollup (FULL): carry a contig through its roll-up levels in the slice; else hand it to
-// the staged kernels at its first raise (they run every contig of a level together,
-// which measured 3x faster per contig-level on cfg4 than one wave per contig here).
+// rollup (FULL, WF_MODE_WAVES): carry a contig through its roll-up levels in the slice;
+// else (the FULL form's fallback duty in WF_MODE_LEVEL0) hand a raised contig to the staged
+// kernels as a level-1 seed.  In WF_MODE_LEVEL0 the roll-up levels run as first-form ROLL
+// launches (below), one per level.
 // S_arg must stay the first parameter: kernarg_fresh reads the argument block at kernarg
 // offset 0.  ROLL (first form only): roll-up level start_level > 0 of the contigs in `list`
 // (the wave levels, S.anc set) -- its own instantiation, so profiles tell the level-0 pass

@@ -467,7 +467,7 @@ bool parse_blast_row(const sv (&f)[15], Chunk& ck) {
       const int32_t s = ck.last_sys_id;
       const int32_t v = ck.values.get(val, s);
       if (v == (int32_t)ck.value_sys.size()) ck.value_sys.push_back(s);   // (a new value)
-      ck.ann.push(std::make_pair(s, v));
+      if (!ck.ann.push(std::make_pair(s, v))) { ck.err = "BLAST chunk annotation capacity"; return false; }
       ++r.ann_n;
       p2 = p3;
     }
@@ -495,7 +495,7 @@ inline void sep_masks(const char* blk, uint64_t& tabs, uint64_t& nls) {
 void parse_blast_chunk(Chunk& ck) {
   if (!all_plain(ck.b, ck.e)) { ck.err = "BLAST file has a lone CR, NUL or non-ASCII bytes"; return; }
   ck.rows.reserve((size_t)((ck.e - ck.b) / 30) + 2);   // (a row is >= 30 bytes)
-  ck.ann.reserve((size_t)((ck.e - ck.b) / 4) + 2);     // (an annotation is >= 4 bytes: "|s=v")
+  ck.ann.reserve((size_t)((ck.e - ck.b) / 2) + 2);     // (an annotation is >= 2 bytes: "|=", utils.py:239-241)
   sv f[15];
   int nf = 0;                                       // fields closed in the current row
   const char* fs = ck.b;                            // start of the current field

@@ -18,7 +18,7 @@ MODE_WAVES = 3
 OPT_SPARSE_BIG, OPT_ATT_LIMIT, OPT_WAVE_TWO, OPT_DUMP_CAP = 1, 2, 3, 4   # wf_set_option
 PHASES = ("waves", "attach", "segments", "decide", "big", "handover", "rollup")   # wf_phase 0..6
 N_PHASES = 8
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _P = C.c_void_p
 
