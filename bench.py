@@ -83,9 +83,9 @@ def parse_args():
     ap.add_argument("--weak", type=int, default=1,
                     help="N > 1: also time the weak-scaling workload (every rank its own n contigs)")
     ap.add_argument("--traffic-json", default=None)
-    ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r04", "cfg4_valu.json"),
+    ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r05", "cfg4_valu.json"),
                     help="PMC VALU counts of the main pass (scripts/pmc_main.py, optional)")
-    ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r04", "k2_pmc.json"),
+    ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r05", "k2_pmc.json"),
                     help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
     return ap.parse_args()
 
@@ -107,6 +107,13 @@ def k2_algorithmic(pair_evals, batch):
     return {"contigs_explain_two": int(sel.sum()), "p_pot_max": int(ppot.max()) if p.size else 0,
             "b_k2_bytes": float((ppot * g * 8.0).sum()), "ops_pair": float((p * g).sum()),
             "pairs": float(p.sum())}
+
+
+def file_sha(path):
+    """sha256 of a file (the library build a PMC summary was taken on), first 16 hex digits."""
+    import hashlib
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
 
 
 def host_cpus():
@@ -356,7 +363,8 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
     if pmc_json and os.path.exists(pmc_json):
         with open(pmc_json) as fh:
             pj = json.load(fh)
-        if pj.get("contigs") == kbatch.n_contigs:
+        from waafle_amd import lib as L
+        if pj.get("contigs") == kbatch.n_contigs and pj.get("lib_sha") == file_sha(L.LIB_PATH):
             insts = pj["valu_insts_per_pass"]
             peak = pj.get("valu_peak_insts_per_s", 2.4576e12)
             out["valu"] = {"insts_per_pass": insts, "achieved_insts_per_s": insts / (k2_max),
@@ -440,7 +448,8 @@ def main():
     for o in args.option:
         name, val = o.split("=")
         chk(so.wf_set_option(h, {"sparse_big": L.OPT_SPARSE_BIG, "att_limit": L.OPT_ATT_LIMIT,
-                                       "wave_two": L.OPT_WAVE_TWO, "dump_cap": L.OPT_DUMP_CAP}[name],
+                                       "wave_two": L.OPT_WAVE_TWO, "dump_cap": L.OPT_DUMP_CAP,
+                                       "triage": L.OPT_TRIAGE}[name],
                              int(val)))
     tstruct = engine.taxonomy_struct(tax)
     chk(so.wf_set_taxonomy(h, C.byref(tstruct)))
@@ -480,39 +489,67 @@ def main():
     value = n_total / (elapsed / args.steps)
     pass_ms = tm.pass_ms / max(1, tm.passes)
     phases = tm.phases()
-    # the dominant kernel: the first wave form's level-0 launch (wf_phase "waves" spans that
-    # launch alone when the wave levels run), every contig's hits and loci read once and
-    # every record written -- the whole algorithmic byte count of the pass
-    dom_ms = phases["waves"][0] / max(1, tm.passes)
+    # The dominant kernel: the level-0 triage launch when it runs (wf_phase "triage" spans that
+    # launch alone), else the first wave form's level-0 launch (wf_phase "waves").  Its
+    # algorithmic bytes: every contig's hits, loci and offsets read once (24 B/hit, 12 B/locus,
+    # 16 B/contig) and the 80 B records of the contigs explain_one decided at level 0 (call
+    # no_lgt after one iteration: an upper bound on the ones this launch wrote -- the wave form
+    # decides the few the triage hands on).  `pass`: the whole pass's bytes over its time.
+    tri_ms = phases["triage"][0] / max(1, tm.passes)
+    cap = 224 if batch.max_hits <= 224 else (256 if batch.max_hits <= 256 else 512)
+    if tri_ms > 0.0:
+        dom_kernel, dom_ms = "k_triage", tri_ms
+        dom_label = "k_triage: the level-0 triage launch (HIP events on its stream, wf_phase triage)"
+    else:
+        dom_kernel, dom_ms = "k_wave<{}, false, false>".format(cap), phases["waves"][0] / max(1, tm.passes)
+        dom_label = dom_kernel + ": the first wave form's level-0 launch (HIP events, wf_phase waves)"
+    n_rec = int(((calls == 1) & (iters == 1)).sum())
+    b_dom = 24 * batch.n_hits + 12 * batch.n_loci + 16 * (N + 1) + 80 * n_rec
     b_alg = algorithmic_bytes(batch)
-    achieved = b_alg / (dom_ms * 1e-3) / 1e9
+    achieved = b_dom / (dom_ms * 1e-3) / 1e9
     achieved_pass = b_alg / (pass_ms * 1e-3) / 1e9
+    lib_sha = file_sha(L.LIB_PATH)
+
+    def pmc_file(path, kind):
+        """A PMC summary of this config, contig count, dominant kernel and library build, or
+        (None, why not)."""
+        if not path or not os.path.exists(path):
+            return None, "no {} file".format(kind)
+        with open(path) as fh:
+            j = json.load(fh)
+        if j.get("config") != args.config or j.get("contigs") != N:
+            return None, "{} file of another workload".format(kind)
+        if j.get("dominant_kernel") != dom_kernel:
+            return None, "{} file of another dominant kernel ({})".format(kind, j.get("dominant_kernel"))
+        if j.get("lib_sha") != lib_sha:
+            return None, "{} file of another libwaafle_hip.so build".format(kind)
+        return j, None
     traffic, tsrc = None, None
-    tpath = args.traffic_json or os.path.join(PROFILES, "r04", "traffic_{}.json".format(args.config))
-    if os.path.exists(tpath):
-        with open(tpath) as fh:
-            tj = json.load(fh)
-        if tj.get("config") == args.config and tj.get("contigs") == N:
-            traffic = tj.get("dominant_hbm_bytes_raw")
-            tsrc = {k: tj.get(k) for k in ("dominant_kernel", "dominant_fetch_bytes_raw",
-                                           "dominant_write_bytes", "fetch_bytes_raw",
-                                           "fetch_bytes_x2", "write_bytes", "hbm_bytes_raw",
-                                           "hbm_bytes_x2", "dispatches_per_pass", "source")}
+    tj, why_t = pmc_file(args.traffic_json or os.path.join(PROFILES, "r05", "traffic_{}.json".format(args.config)),
+                         "traffic")
+    if tj:
+        traffic = tj.get("dominant_hbm_bytes_raw")
+        tsrc = {k: tj.get(k) for k in ("dominant_kernel", "dominant_fetch_bytes_raw",
+                                       "dominant_write_bytes", "fetch_bytes_raw",
+                                       "fetch_bytes_x2", "write_bytes", "hbm_bytes_raw",
+                                       "hbm_bytes_x2", "dispatches_per_pass", "source")}
+    else:
+        tsrc = {"skipped": why_t}
     valu = None
-    if args.valu_pmc_json and os.path.exists(args.valu_pmc_json):
-        with open(args.valu_pmc_json) as fh:
-            vj = json.load(fh)
-        if vj.get("config") == args.config and vj.get("contigs") == N:
-            peak = vj.get("valu_peak_insts_per_s", 1.2288e12)
-            vi, vd = vj["valu_insts_per_pass"], vj["dominant_valu_insts_per_pass"]
-            valu = {"unit": "wave-instructions/s", "peak": peak,
-                    "pass": {"insts": vi, "achieved": vi / (pass_ms * 1e-3),
-                             "frac": vi / (pass_ms * 1e-3) / peak},
-                    "dominant": {"kernel": vj.get("dominant_kernel"), "insts": vd,
-                                 "achieved": vd / (dom_ms * 1e-3),
-                                 "frac": vd / (dom_ms * 1e-3) / peak,
-                                 "wait_frac": vj.get("dominant_wait_frac")},
-                    "source": vj.get("source")}
+    vj, why_v = pmc_file(args.valu_pmc_json, "VALU")
+    if vj:
+        peak = vj.get("valu_peak_insts_per_s", 1.2288e12)
+        vi, vd = vj["valu_insts_per_pass"], vj["dominant_valu_insts_per_pass"]
+        valu = {"unit": "wave-instructions/s", "peak": peak,
+                "pass": {"insts": vi, "achieved": vi / (pass_ms * 1e-3),
+                         "frac": vi / (pass_ms * 1e-3) / peak},
+                "dominant": {"kernel": vj.get("dominant_kernel"), "insts": vd,
+                             "achieved": vd / (dom_ms * 1e-3),
+                             "frac": vd / (dom_ms * 1e-3) / peak,
+                             "wait_frac": vj.get("dominant_wait_frac")},
+                "source": vj.get("source")}
+    else:
+        valu = {"skipped": why_v}
     spec = synth.CONFIGS[args.config]
     result = {
         "metric": "contigs scored/sec + k2 clade-pair evals/sec at 1/2/4/8 MI355X vs CPU ref",
@@ -542,12 +579,14 @@ def main():
                              for k, v in tm.phases().items()}),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_wave<224, false, false>: the first wave form's level-0 launch "
-                               "(HIP events on its stream, wf_phase waves)",
+                     "kernel": dom_label,
                      "kernel_ms": dom_ms,
-                     "algorithmic_bytes_per_launch": b_alg,
-                     "algorithmic_bytes_rule": "24 B/hit + 12 B/locus + 96 B/contig",
-                     "pass": {"ms": pass_ms, "achieved": achieved_pass,
+                     "algorithmic_bytes_per_launch": b_dom,
+                     "algorithmic_bytes_rule": "24 B/hit + 12 B/locus + 16 B/contig + 80 B per "
+                                               "record of a contig explain_one decided at level 0 "
+                                               "({} of {})".format(n_rec, N),
+                     "pass": {"ms": pass_ms, "achieved": achieved_pass, "bytes": b_alg,
+                              "bytes_rule": "24 B/hit + 12 B/locus + 96 B/contig",
                               "frac": achieved_pass / HBM_PEAK_GBS,
                               "note": "every kernel of one wf_score pass (level 0, hand-over, "
                                       "roll-up levels, staged remainder)"},

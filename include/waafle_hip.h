@@ -24,7 +24,8 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 4   /* 4: WF_OPT_SPARSE_BIG 0/1 retired, WF_PHASE_ROLLUP, WF_OPT_WAVE_TWO / _DUMP_CAP */
+#define WF_ABI_VERSION 5   /* 4: WF_OPT_SPARSE_BIG 0/1 retired, WF_PHASE_ROLLUP, WF_OPT_WAVE_TWO / _DUMP_CAP;
+                                 5: WF_OPT_TRIAGE, WF_PHASE_TRIAGE */
 
 enum wf_status {
   WF_OK = 0,
@@ -73,8 +74,14 @@ enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
  *   over the contigs still open; the rest goes to the segment-table decision (k_dump_sparse);
  *   0: every explain_two contig goes there and the roll-up levels run in the staged kernels.
  * WF_OPT_DUMP_CAP: segment-table entries of the wave form's hand-over buffer (default
- *   max(32 * contigs, 65536)); contigs past it go to the staged kernels (a test setting). */
-enum wf_option { WF_OPT_SPARSE_BIG = 1, WF_OPT_ATT_LIMIT = 2, WF_OPT_WAVE_TWO = 3, WF_OPT_DUMP_CAP = 4 };
+ *   max(32 * contigs, 65536)); contigs past it go to the staged kernels (a test setting).
+ * WF_OPT_TRIAGE (WF_MODE_LEVEL0 / _WAVES): 1 (default) a level-0 triage kernel first decides
+ *   the contigs explain_one settles from the clades present on every locus (one-run gene
+ *   scores), without the wave form's sort and segment table; the wave form runs the rest.
+ *   0: the wave form runs every contig (a test setting: it exercises that path on every
+ *   input). */
+enum wf_option { WF_OPT_SPARSE_BIG = 1, WF_OPT_ATT_LIMIT = 2, WF_OPT_WAVE_TWO = 3, WF_OPT_DUMP_CAP = 4,
+                 WF_OPT_TRIAGE = 5 };
 
 typedef struct wf_ctx wf_ctx;
 
@@ -174,6 +181,9 @@ enum wf_phase {
                                  their segment tables (k_dump_sparse) */
   WF_PHASE_ROLLUP = 6,        /* roll-up levels 1, 2, ... in the first wave form (with their
                                  hand-overs), WF_OPT_WAVE_TWO 1 */
+  WF_PHASE_TRIAGE = 7,        /* the level-0 triage kernel and the list of contigs it hands
+                                 on (WF_OPT_TRIAGE 1); WF_PHASE_WAVES is then the first wave
+                                 form's launch over that list */
   WF_N_PHASES = 8
 };
 typedef struct wf_timing {

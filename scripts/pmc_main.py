@@ -3,23 +3,28 @@ the pass and for the dominant kernel (the first wave form's level-0 launch), fro
 rocprofv3 --pmc SQ_* run of bench.py (scripts/pmc_r4.sh).  bench.py reads the output as
 --valu-pmc-json and divides by the pass / kernel times it measures itself.
 
-    pmc_main.py PMC_DIR PASSES CONFIG CONTIGS OUT.json
+    pmc_main.py PMC_DIR PASSES CONFIG CONTIGS OUT.json [DOMINANT]
 """
 import collections
 import csv
 import glob
 import json
+import os
 import re
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from traffic import lib_sha  # noqa: E402
 
 # wave64 VALU issue: each SIMD-32 takes 2 cycles per wave-instruction (MI355X_MICROARCH.md):
 # 256 CUs x 4 SIMDs x 2.4 GHz / 2
 VALU_PEAK = 256 * 4 * 2.4e9 / 2
-DOMINANT = "k_wave<224, false, false>"
+DOMINANT = "k_triage"
 
 
 def main():
     d, passes, config, contigs, out = sys.argv[1], int(sys.argv[2]), sys.argv[3], int(sys.argv[4]), sys.argv[5]
+    dominant = sys.argv[6] if len(sys.argv) > 6 else DOMINANT
     f = glob.glob(d + "/**/*counter_collection.csv", recursive=True)[0]
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(f)):
@@ -27,11 +32,11 @@ def main():
         acc[m.group(1) if m else r["Kernel_Name"][:40]][r["Counter_Name"]] += float(r["Counter_Value"])
     per = {k: {c: x / passes for c, x in v.items()} for k, v in acc.items()}
     total = sum(v.get("SQ_INSTS_VALU", 0.0) for v in per.values())
-    dom = per.get(DOMINANT, {})
+    dom = per.get(dominant, {})
     res = {"config": config, "contigs": contigs, "passes": passes,
            "valu_insts_per_pass": total,
            "salu_insts_per_pass": sum(v.get("SQ_INSTS_SALU", 0.0) for v in per.values()),
-           "dominant_kernel": DOMINANT,
+           "dominant_kernel": dominant, "lib_sha": lib_sha(),
            "dominant_valu_insts_per_pass": dom.get("SQ_INSTS_VALU", 0.0),
            "dominant_wait_frac": (dom.get("SQ_WAIT_ANY", 0.0) / dom["SQ_WAVE_CYCLES"])
            if dom.get("SQ_WAVE_CYCLES") else None,

@@ -34,7 +34,7 @@ def test_struct_layouts_match_header():
 
 def test_abi_version_and_no_device_is_an_error_not_a_crash():
     so = lib.load()
-    assert so.wf_abi_version() == lib.ABI_VERSION == 4
+    assert so.wf_abi_version() == lib.ABI_VERSION == 5
     n = ctypes.c_int(-1)
     rc = so.wf_device_count(ctypes.byref(n))
     assert (rc == 0 and n.value >= 0) or (rc != 0 and n.value == 0)

@@ -28,6 +28,8 @@ FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n
 FORMS = {
     # (default) explain_two and the roll-up levels in the first wave form's hand-over
     "level0": dict(mode="level0"),
+    # the same without the level-0 triage (wf_triage.hip): the wave form runs every contig
+    "notriage": dict(mode="level0", options={lib.OPT_TRIAGE: 0}),
     # round-3 flow: every explain_two contig handed over whole, roll-up in the staged kernels
     "handover": dict(mode="level0", options={lib.OPT_WAVE_TWO: 0}),
     # a hand-over buffer of 96 entries: the contigs past it take the staged kernels

@@ -166,7 +166,8 @@ def test_attachment_limit_default_mode_oversized_contigs():
 def test_option_validation():
     s = engine.GpuScorer(0)
     for opt, val in ((lib.OPT_ATT_LIMIT, 0), (lib.OPT_ATT_LIMIT, 1 << 31), (lib.OPT_SPARSE_BIG, 4),
-                     (lib.OPT_SPARSE_BIG, 0), (lib.OPT_SPARSE_BIG, 1), (99, 1)):   # (0, 1: retired)
+                     (lib.OPT_SPARSE_BIG, 0), (lib.OPT_SPARSE_BIG, 1), (lib.OPT_TRIAGE, 2),
+                     (99, 1)):   # (SPARSE_BIG 0, 1: retired)
         assert s.lib.wf_set_option(s.h, opt, val) == lib.WF_E_BADINPUT
     s.close()
 
@@ -196,7 +197,7 @@ def test_cfg4_full_size(cfg4_full):
     s.close()
     assert_same(engine.Results.concat(parts, [int(batch.hit_off[x]) for x, _ in bounds]), a, batch)
     for kw in (dict(lds_bytes=16384), dict(options={lib.OPT_SPARSE_BIG: 2}),
-               dict(options={lib.OPT_WAVE_TWO: 0})):
+               dict(options={lib.OPT_WAVE_TWO: 0}), dict(options={lib.OPT_TRIAGE: 0})):
         c = score(batch, tax, **kw)
         assert not c.status.any(), kw
         assert_same(c, a, batch)

@@ -290,3 +290,12 @@ def test_pairwise_model_is_numpy():
     for n in list(range(1, 300)) + [1000, 1031, 4103, 8191]:
         v = float(rng.uniform(0.1, 1.0))
         assert float(np.add.reduce(np.full(n, v))) == 0.0 + pairwise(n, v), n
+
+
+def test_pw_run_sum_whole_run_equals_pw_const_sum():
+    """The level-0 triage (wf_triage.hip) evaluates every one-run segment by pw_run_sum, whole
+    runs included: over [0, n) it must equal pw_const_sum bit for bit at every buffer length."""
+    rng = random.Random(5)
+    for v in [rng.uniform(0.05, 1.0) for _ in range(2)] + [0.987654321]:
+        for n in range(1, 8192):
+            assert pw_run_sum(n, 0, n, v) == pw_const_sum(n, v), (n, v)

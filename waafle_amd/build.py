@@ -12,7 +12,8 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libwaafle_hip.so")
 SOURCES = [os.path.join(CSRC, "wf_staged.hip"), os.path.join(CSRC, "wf_fast.hip"),
-           os.path.join(CSRC, "wf_genecall.hip"), os.path.join(CSRC, "wf_junctions.hip"),
+           os.path.join(CSRC, "wf_triage.hip"), os.path.join(CSRC, "wf_genecall.hip"),
+           os.path.join(CSRC, "wf_junctions.hip"),
            os.path.join(CSRC, "wf_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "wf_internal.h"), os.path.join(CSRC, "wf_device.h"),
                   os.path.join(CSRC, "wf_sparse.h"), os.path.join(CSRC, "wf_lanes.h"),

@@ -50,6 +50,7 @@ struct wf_ctx {
   int64_t att_limit = (int64_t(1) << 31) - 1;   // wf_set_option(WF_OPT_ATT_LIMIT)
   int wave_two = 1;                // wf_set_option(WF_OPT_WAVE_TWO)
   int64_t dump_cap = 0;            // wf_set_option(WF_OPT_DUMP_CAP), 0: the default size
+  int triage = 1;                  // wf_set_option(WF_OPT_TRIAGE)
   wf::StagedState* staged = nullptr;
   // --write-details
   bool details_on = false;
@@ -277,6 +278,10 @@ int wf_set_option(wf_ctx* ctx, int option, int64_t value) {
         return fail(ctx, WF_E_BADINPUT, "WF_OPT_DUMP_CAP %lld out of [0, 2^31 - 4096]", (long long)value);
       ctx->dump_cap = value;
       return WF_OK;
+    case WF_OPT_TRIAGE:
+      if (value < 0 || value > 1) return fail(ctx, WF_E_BADINPUT, "WF_OPT_TRIAGE is 0 or 1");
+      ctx->triage = (int)value;
+      return WF_OK;
     default:
       return fail(ctx, WF_E_BADINPUT, "unknown option %d", option);
   }
@@ -380,7 +385,8 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
   if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
   wf::staged_set_level0(ctx->staged, ctx->mode != WF_MODE_STAGED, ctx->mode == WF_MODE_WAVES);
-  wf::staged_set_options(ctx->staged, ctx->sparse_big, ctx->att_limit, ctx->wave_two, ctx->dump_cap);
+  wf::staged_set_options(ctx->staged, ctx->sparse_big, ctx->att_limit, ctx->wave_two, ctx->dump_cap,
+                         ctx->triage);
   std::pair<int, int> el{-1, -1};
   if (ctx->timing) {
     if (take_event_pair(ctx, ctx->ev_lds) < 0) return fail(ctx, WF_E_HIP, "hipEventCreate failed");

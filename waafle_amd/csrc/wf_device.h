@@ -95,6 +95,19 @@ struct Arena {
 
 __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
 
+// The kernel's first argument (at kernarg offset 0), through a pointer the compiler cannot
+// see through: loads of its fields are not hoisted out of the loop that calls this.
+template <class T>
+__device__ __forceinline__ const T& kernarg_fresh(const T& arg) {
+#ifdef __HIP_DEVICE_COMPILE__
+  uint64_t a = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(a));
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(a);
+#else
+  return arg;                                        // (host pass: never executed)
+#endif
+}
+
 // --------------------------------------------------------------------------
 // block-wide primitives
 // --------------------------------------------------------------------------

@@ -176,19 +176,6 @@ __device__ __forceinline__ int leaves_for(const SArgs& S, int len) {
          (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
 }
 
-// The kernel's first argument (at kernarg offset 0), through a pointer the compiler cannot
-// see through: loads of its fields are not hoisted out of the loop that calls this.
-template <class T>
-__device__ __forceinline__ const T& kernarg_fresh(const T& arg) {
-#ifdef __HIP_DEVICE_COMPILE__
-  uint64_t a = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
-  asm volatile("" : "+s"(a));
-  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(a);
-#else
-  return arg;                                        // (host pass: never executed)
-#endif
-}
-
 __device__ __forceinline__ uint64_t lanes_below() { return (1ull << lane_id()) - 1ull; }
 
 // (every lane active: wf_lanes.h)
@@ -1772,6 +1759,16 @@ hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t
 #endif
   return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s)
                          : launch_cap<512, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s);
+}
+
+hipError_t launch_fast_list(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
+                            const int64_t* n_dev, int max_hits, int cus, hipStream_t s) {
+  const int N = sa.k.n_contigs;
+#ifndef WF_NO_CAP224
+  if (max_hits <= 224) return launch_cap<224, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s);
+#endif
+  return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s)
+                         : launch_cap<512, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s);
 }
 
 hipError_t launch_level(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,

@@ -172,6 +172,13 @@ struct DetailsSink {
 };
 
 struct StagedState;
+// Level-0 triage (wf_triage.hip): pend[c] = 0 for the contigs it finished (explain_one from
+// the full clades), kPendTriage for the rest, which the first wave form then runs (list).
+constexpr int kPendTriage = 9;
+hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int cus, hipStream_t s);
+// the first wave form over `list` (length *n_dev, on the device) at level 0
+hipError_t launch_fast_list(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
+                            const int64_t* n_dev, int max_hits, int cus, hipStream_t s);
 // Per-contig wave kernels (wf_fast.hip): pend[c] = 0 finished there, 1 handed to the
 // staged path with its attachment and leaf counts in ccnt / cleaves.  launch_fast: every
 // contig, explain_one at level 0; launch_full: the contigs of `list` (length *n_dev, on
@@ -189,7 +196,8 @@ void staged_set_lds(StagedState* st, int64_t bytes);
 // context options (include/waafle_hip.h wf_option): the segment-table decision for contigs
 // that outgrow the LDS arena, the attachments one call accepts (more: WF_E_TOOBIG), explain_two
 // and the roll-up levels in the first wave form, the hand-over buffer's size (0: default)
-void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap);
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap,
+                        int triage);
 // per-phase timing (wf_phase): HIP events around each phase of each level, read back at the
 // end of every staged_score call into the accumulators (reset by staged_timing(st, on))
 void staged_timing(StagedState* st, bool on);

@@ -1274,6 +1274,8 @@ struct StagedState {
   int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
   int wave_two = 1;                  // WF_OPT_WAVE_TWO: explain_two + roll-up levels in the wave form
   int64_t dump_cap = 0;              // WF_OPT_DUMP_CAP (0: max(32 N, 65536))
+  int triage = 1;                    // WF_OPT_TRIAGE: level-0 triage before the first wave form
+  Buf tri_list, tri_cnt;             // the contigs the triage hands on, and their count
   Buf roll0, roll1, roll_cnt, anc;   // wave levels: contig lists, per-level counts, ancestors
   // per-phase timing (wf_phase): event pool, this call's spans (phase, begin, end)
   bool timing = false;
@@ -1339,7 +1341,9 @@ void staged_set_lds(StagedState* st, int64_t bytes) {
   st->dec_lds_fixed = true;
 }
 
-void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap) {
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap,
+                        int triage) {
+  st->triage = triage;
   st->sparse_big = sparse_big;
   st->att_limit = att_limit;
   st->wave_two = wave_two;
@@ -1713,8 +1717,26 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         da.fail_ctr = rcnt + kMaxIter + 2;
       }
     }
-    ST_TRY(launch_fast(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
-                       st->cus, s));
+    if (st->triage && max_hits <= 256) {
+      // the triage (wf_triage.hip) decides the contigs explain_one settles from their full
+      // clades; the first wave form runs the rest from its list (count on the device)
+      ST_TRY(st->tri_list.ensure(s, (size_t)N * 4));
+      ST_TRY(st->tri_cnt.ensure(s, 8));
+      const int t_tri0 = t_mark(st, s);                 // (the triage span: its launch alone)
+      ST_TRY(launch_triage(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), st->cus, s));
+      const int t_tri = t_mark(st, s);
+      t_span(st, WF_PHASE_WAVES, t_waves, t_tri0);
+      t_span(st, WF_PHASE_TRIAGE, t_tri0, t_tri);
+      t_waves = t_tri;
+      using PendItT = hipcub::TransformInputIterator<bool, PendIs, const int32_t*>;
+      ST_TRY(select_list(st, s, PendItT(st->pend.as<int32_t>(), PendIs{kPendTriage}), st->tri_list.as<int32_t>(),
+                         st->tri_cnt.as<int64_t>(), N));
+      ST_TRY(launch_fast_list(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
+                              st->tri_list.as<int32_t>(), st->tri_cnt.as<int64_t>(), max_hits, st->cus, s));
+    } else {
+      ST_TRY(launch_fast(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
+                         st->cus, s));
+    }
     if (dump) {
       const int t_h0 = t_mark(st, s);
       t_span(st, WF_PHASE_WAVES, t_waves, t_h0);

@@ -1,0 +1,424 @@
+// Level-0 triage of the contig-scoring path (gfx950 / MI355X): the contigs explain_one
+// settles from the clades present on every locus, decided without a sort.
+//
+// One wave64 per contig, alone in its workgroup (no barriers), persistent over the batch in
+// the XCD-aware order of the wave kernels (wf_fast.hip).  Per contig (orgscorer.py:359-429,
+// 447-461, 585-597, 621-631):
+//   hits -> attachments     lane per hit, up to 4 batches of 64 held in registers; the loci
+//                           (ascending, disjoint) in LDS, each hit's first candidate locus by
+//                           binary search (orgscorer.py:359-369, calc_overlap utils.py:487-500)
+//   full clades             the clades attached to locus 0 go into a small LDS hash table;
+//                           every attachment ORs its locus into its clade's mask there; a clade
+//                           whose mask holds every locus is "full".  An explain_one option has
+//                           crit >= k1 > 0, so a nonzero gene score on every unmasked locus: with
+//                           every locus unmasked, the options are full clades
+//   their gene scores       lane per locus: the segment's envelope is one run (one attachment,
+//                           or a whole-locus one dominating the rest), whose exact numpy mean has
+//                           a closed form (pw_const_sum / pw_run_sum, wf_device.h)
+//   weak-locus mask         every locus is unmasked when a full known clade's mean reaches kmin
+//                           on it (orgscorer.py:420-427; --weak-loci penalize masks nothing)
+//   explain_one + meld_one  crit = min, rank = numpy-order mean; best by (rank, clade) as the
+//                           wave kernels; options within --range melded to their LCA
+//   annotations             the last hit at the best score per (locus, system), :383-392
+// Everything else -- no full clade (explain_two), a locus the full clades leave unsettled, a
+// segment of several envelope runs, no option, more than 256 hits or 64 loci, overlapping or
+// unordered loci, --min-overlap 0, --weak-loci assign-unknown -- is handed on untouched
+// (pend = kPendTriage): the first wave form (k_wave<CAP, false>) runs exactly those contigs,
+// from their hits, as it runs every contig without the triage.  Same arithmetic, so the same
+// bits: the triage only skips the sort, the segment table and the pruning passes the wave
+// form spends on the contigs explain_one settles at level 0 (~90% at cfg4).
+#include "wf_device.h"
+#include "wf_lanes.h"
+
+#ifndef WF_TRIAGE_WAVES
+#define WF_TRIAGE_WAVES 6              // resident waves per SIMD (75 VGPRs unspilled, a 4.8 KB slice)
+#endif
+
+namespace wf {
+
+namespace {
+
+constexpr int kTrHB = 4;               // hit batches of 64: contigs of up to 256 hits
+constexpr int kTrLoc = 64;             // loci (64-bit locus masks)
+constexpr int kTrTab = 128;            // candidate table: clades attached to locus 0
+constexpr int kTrSeg = 64;             // full clades x loci evaluated (one lane each)
+constexpr int kTrSpan = 26;            // loci one hit may attach to, from its first candidate
+constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
+constexpr int kTrXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
+
+struct TriSmem {
+  int lo[kTrLoc], hi[kTrLoc];          // locus site ranges (min, max of start/end)
+  uint32_t tkey[kTrTab];               // candidate clade (kTrEmpty: free slot)
+  uint64_t tmask[kTrTab];              // loci it is attached to
+  uint64_t abest[kTrLoc];              // (locus, system): best annotation score bits
+  int ahit[kTrLoc];                    // ... and the last hit at that score
+  // the full clades' segments, slot i * G + g (full clade i, locus g): attachments (bit 16:
+  // one not dominated by a whole-locus attachment), the last attachment's site range and
+  // score, the best score of its whole-locus attachments
+  int scnt[kTrSeg];
+  uint32_t slohi[kTrSeg];
+  double ssc[kTrSeg];
+  uint64_t sfw[kTrSeg];
+  int fcl[kTrSeg];                     // full clade i: its id
+  int8_t tfull[kTrTab];                // table slot -> full clade index (-1: not full)
+  int8_t st[kTrLoc];
+};
+static_assert(sizeof(TriSmem) <= 160 * 1024 / (4 * WF_TRIAGE_WAVES), "triage slice: WF_TRIAGE_WAVES per SIMD");
+
+__device__ __forceinline__ uint32_t tr_hash(uint32_t clade) { return (clade * 0x9E3779B1u) >> 25; }   // 7 bits
+
+// Site range [start, stop) of a hit on a locus (orgscorer.py:371-382, python slice rules),
+// packed lo | hi << 16 (loci < 8192 sites here).
+__device__ __forceinline__ uint32_t tr_lohi(int qlo, int qhi, int llo, int len) {
+  const int h1s = max(0, qlo - llo);
+  const int h2s = min(len - 1, qhi - llo);
+  const int start = min(h1s, len);
+  int stop = h2s + 1;
+  if (stop < 0) { stop += len; if (stop < 0) stop = 0; }
+  return (uint32_t)start | ((uint32_t)stop << 16);
+}
+
+__global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves,
+                                                               int32_t* pend) {
+  __shared__ TriSmem F;
+  const int lane = threadIdx.x;
+  const int N = S_arg.k.n_contigs;
+  // XCD-aware order (k_wave): XCD x's j-th workgroup takes contig (8 k + x) * B + j at step k
+  const bool xmap = gridDim.x % kTrXcds == 0;
+  const int xb = (int)gridDim.x / kTrXcds, xj = (int)blockIdx.x / kTrXcds, xx = (int)blockIdx.x % kTrXcds;
+  for (int it = 0;; ++it) {
+    const int c = xmap ? (it * kTrXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
+    if (c >= N) break;
+    const SArgs& S = kernarg_fresh<SArgs>(S_arg);
+    const KArgs& K = S.k;
+    const DevParams& P = K.p;
+    const int nsys = K.n_sys;
+    const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
+    const int64_t nh = h1 - h0;
+    const int64_t hend = min(h1, h0 + 64 * kTrHB);
+    // every field of the contig's hits, issued before the loci
+    int r_qlo[kTrHB], r_qhi[kTrHB], r_cl[kTrHB], r_hs[kTrHB];
+    double r_sc[kTrHB], r_scv[kTrHB];
+    uint32_t r_m[kTrHB];
+#pragma unroll
+    for (int b = 0; b < kTrHB; ++b) {
+      const int64_t h = h0 + 64 * b + lane;
+      r_qlo[b] = 0; r_qhi[b] = 0; r_cl[b] = 0; r_hs[b] = 0; r_sc[b] = 0.0; r_scv[b] = 0.0; r_m[b] = 0u;
+      if (h < hend) {
+        r_scv[b] = K.scov[h];
+        r_qlo[b] = K.qlo[h];
+        r_qhi[b] = K.qhi[h];
+        r_hs[b] = K.hstrand[h];
+        r_cl[b] = K.taxon[h];
+        r_sc[b] = K.score[h];
+        if (nsys > 0) r_m[b] = K.sysmask[h];
+      }
+    }
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    int my_lo = 0, my_hi = -1, my_st = 0;
+    if (lane < G && G <= kTrLoc) {
+      const int a = K.lstart[l0 + lane], e = K.lend[l0 + lane];
+      my_lo = min(a, e);
+      my_hi = max(a, e);
+      my_st = K.lstrand[l0 + lane];
+    }
+    const int prev_hi = __shfl_up(my_hi, 1, 64);
+    // what the triage takes (else the wave form): loci ascending and disjoint (each hit's
+    // loci found by binary search), every locus one numpy buffer, options only on full
+    // clades (k1 > 0), the weak-locus mask from the full clades' means
+    const bool take =
+        nh > 0 && nh <= 64 * kTrHB && G > 0 && G <= kTrLoc && G * nsys <= kTrLoc && P.min_overlap > 0.0 &&
+        P.k1 > 0.0 && P.weak != 2 &&
+        __ballot(lane < G && ((lane >= 1 && my_lo <= prev_hi) || my_hi - my_lo + 1 >= kNpyBuf)) == 0ull;
+    if (!take) {
+      if (lane == 0) pend[c] = kPendTriage;
+      continue;
+    }
+    const uint64_t allG = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+    const int nann = G * nsys;
+    const bool ann_on = nsys > 0;
+    if (lane < G) { F.lo[lane] = my_lo; F.hi[lane] = my_hi; F.st[lane] = (int8_t)my_st; }
+    F.tkey[lane] = kTrEmpty; F.tkey[lane + 64] = kTrEmpty;
+    F.tmask[lane] = 0ull; F.tmask[lane + 64] = 0ull;
+    F.abest[lane] = 0ull; F.ahit[lane] = -1;
+    F.scnt[lane] = 0; F.sfw[lane] = 0ull;
+    wave_sync();
+    // ---- hits -> attachments (orgscorer.py:359-369): per batch, the first locus ending at or
+    // after qlo, then the loci up to the one starting past qhi; attached loci relative to the
+    // first: g0 | mask << 6 (0: none) ----
+    uint32_t r_am[kTrHB];
+    bool bad = false;
+#pragma unroll
+    for (int b = 0; b < kTrHB; ++b) {
+      uint32_t am = 0u;
+      if (h0 + 64 * b + lane < hend && r_scv[b] >= P.min_scov) {
+        const int qlo = r_qlo[b], qhi = r_qhi[b];
+        int g = 0;
+#pragma unroll
+        for (int k = 32; k > 0; k >>= 1)
+          if (g + k <= G && F.hi[g + k - 1] < qlo) g += k;
+        const int g0 = g;
+        uint32_t rel = 0u;
+        for (; g < G; ++g) {
+          const int lo = F.lo[g];
+          if (lo > qhi) break;
+          if (attaches(P, qlo, qhi, r_hs[b], lo, F.hi[g] - lo + 1, F.st[g])) {
+            if (g - g0 < kTrSpan) rel |= 1u << (g - g0);
+            else bad = true;
+          }
+        }
+        if (rel) {
+          am = (uint32_t)g0 | (rel << 6);
+          for (int j = 0; j < P.jump; ++j) r_cl[b] = K.parent[r_cl[b]];   // orgscorer.py:955-957
+        }
+      }
+      r_am[b] = am;
+    }
+    // ---- the candidates: clades attached to locus 0 ----
+#pragma unroll
+    for (int b = 0; b < kTrHB; ++b) {
+      if ((r_am[b] & 0x7Fu) == 0x40u) {               // g0 == 0 and locus 0 attached
+        const uint32_t cl = (uint32_t)r_cl[b];
+        uint32_t slot = tr_hash(cl);
+        for (int probes = 0;; ++probes) {
+          if (probes == kTrTab) { bad = true; break; }
+          const uint32_t old = atomicCAS(&F.tkey[slot], kTrEmpty, cl);
+          if (old == kTrEmpty || old == cl) break;
+          slot = (slot + 1) & (kTrTab - 1);
+        }
+      }
+    }
+    if (__ballot(bad) != 0ull) {
+      if (lane == 0) pend[c] = kPendTriage;
+      wave_sync();
+      continue;
+    }
+    wave_sync();
+    // ---- every attachment ORs its loci into its clade's mask (r_cl becomes the clade's table
+    // slot, -1 outside the table); annotation pass 1 (:383-392) ----
+#pragma unroll
+    for (int b = 0; b < kTrHB; ++b) {
+      const uint32_t am = r_am[b];
+      int found = -1;
+      if (am != 0u) {
+        const int g0 = (int)(am & 63u);
+        const uint64_t lm = (uint64_t)(am >> 6) << g0;
+        const uint32_t cl = (uint32_t)r_cl[b];
+        uint32_t slot = tr_hash(cl);
+        for (int probes = 0; probes < kTrTab; ++probes) {
+          const uint32_t k = F.tkey[slot];
+          if (k == cl) { atomicOr(&F.tmask[slot], lm); found = (int)slot; break; }
+          if (k == kTrEmpty) break;
+          slot = (slot + 1) & (kTrTab - 1);
+        }
+        if (ann_on && r_m[b] != 0u && r_sc[b] >= P.annot_ref)
+          for (uint64_t bits = lm; bits; bits &= bits - 1) {
+            const int g = __builtin_ctzll(bits);
+            for (int s = 0; s < nsys; ++s)
+              if ((r_m[b] >> s) & 1u) atomicMax(&F.abest[g * nsys + s], dbits(r_sc[b]));
+          }
+      }
+      r_cl[b] = found;
+    }
+    wave_sync();
+    // full clades (every locus in the mask), numbered in table order (lane i: slots i, i + 64)
+    int nfull = 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int e = lane + 64 * half;
+      const bool full = F.tkey[e] != kTrEmpty && F.tmask[e] == allG;
+      const uint64_t fm = __ballot(full);
+      const int fi = nfull + __popcll(fm & ((1ull << lane) - 1ull));
+      F.tfull[e] = (int8_t)(full && fi * G < kTrSeg ? fi : -1);
+      if (full && fi * G < kTrSeg) F.fcl[fi] = (int)F.tkey[e];
+      nfull += __popcll(fm);
+    }
+    if (nfull == 0 || nfull * G > kTrSeg) {            // explain_two (no full clade), or the wave form
+      if (lane == 0) pend[c] = kPendTriage;
+      wave_sync();
+      continue;
+    }
+    wave_sync();
+    // ---- the full clades' attachments per segment; annotation pass 2: the last hit (largest
+    // index) at the best score ----
+#pragma unroll
+    for (int b = 0; b < kTrHB; ++b) {
+      const uint32_t am = r_am[b];
+      int fi = -1;
+      if (am != 0u) {
+        const int g0 = (int)(am & 63u);
+        fi = r_cl[b] >= 0 ? (int)F.tfull[r_cl[b]] : -1;
+        if (fi >= 0)
+          for (uint32_t rel = am >> 6; rel; rel &= rel - 1) {
+            const int g = g0 + __builtin_ctz(rel);
+            const int q = fi * G + g;
+            const int llo = F.lo[g], len = F.hi[g] - llo + 1;
+            const uint32_t lh = tr_lohi(r_qlo[b], r_qhi[b], llo, len);
+            atomicAdd(&F.scnt[q], 1);
+            F.slohi[q] = lh;
+            F.ssc[q] = r_sc[b];
+            // (k_wave's Fw: the best whole-locus score above 0.0)
+            if ((int)(lh & 0xFFFFu) <= 0 && (int)(lh >> 16) >= len && r_sc[b] > 0.0) atomicMax(&F.sfw[q], dbits(r_sc[b]));
+          }
+        if (ann_on && r_m[b] != 0u && r_sc[b] >= P.annot_ref) {
+          const int h = (int)(h0 + 64 * b + lane);
+          for (uint64_t bits = (uint64_t)(am >> 6) << g0; bits; bits &= bits - 1) {
+            const int g = __builtin_ctzll(bits);
+            for (int s = 0; s < nsys; ++s)
+              if (((r_m[b] >> s) & 1u) && F.abest[g * nsys + s] == dbits(r_sc[b])) atomicMax(&F.ahit[g * nsys + s], h);
+          }
+        }
+      }
+      r_cl[b] = fi;
+    }
+    wave_sync();
+    // an attachment the best whole-locus one does not cover (k_wave's "kept")
+#pragma unroll
+    for (int b = 0; b < kTrHB; ++b) {
+      const uint32_t am = r_am[b];
+      const int fi = r_cl[b];
+      if (am == 0u || fi < 0) continue;
+      const int g0 = (int)(am & 63u);
+      for (uint32_t rel = am >> 6; rel; rel &= rel - 1) {
+        const int g = g0 + __builtin_ctz(rel);
+        const int q = fi * G + g;
+        const int llo = F.lo[g], len = F.hi[g] - llo + 1;
+        const uint32_t lh = tr_lohi(r_qlo[b], r_qhi[b], llo, len);
+        if ((int)(lh & 0xFFFFu) < (int)(lh >> 16) && r_sc[b] > __longlong_as_double((long long)F.sfw[q]))
+          atomicOr(&F.scnt[q], 1 << 16);
+      }
+    }
+    wave_sync();
+    // ---- gene scores (:399-406), lane per segment: one envelope run, exact numpy mean ----
+    const int nseg = nfull * G;
+    const int my_g = lane % G, my_f = lane / G;
+    double mean = 0.0;
+    bool fail = false;
+    if (lane < nseg) {
+      const int n = F.scnt[lane];
+      const int len = F.hi[my_g] - F.lo[my_g] + 1;
+      int lo = 0, hi = len;
+      double v = 0.0;
+      if ((n & 0xFFFF) == 1) {
+        const uint32_t lh = F.slohi[lane];
+        lo = (int)(lh & 0xFFFFu); hi = (int)(lh >> 16); v = F.ssc[lane];
+      } else if ((n >> 16) == 0) {
+        v = __longlong_as_double((long long)F.sfw[lane]);   // dominated by a whole-locus run
+      } else {
+        fail = true;                                   // several envelope runs: the wave form
+      }
+      hi = max(hi, lo);
+      mean = (0.0 + pw_run_sum(len, lo, hi, v)) / (double)len;   // (= pw_const_sum on [0, len))
+    }
+    // every locus unmasked (:420-427): a full known clade's mean >= kmin on it (penalize and
+    // kmin <= 0 mask nothing)
+    const bool sure_l = lane < nseg && F.fcl[my_f] != K.unknown && mean >= P.kmin;
+    const uint64_t sure = wave_or_dpp(sure_l ? 1ull << my_g : 0ull);
+    const bool um_all = P.weak != 0 || P.kmin <= 0.0;
+    if (__ballot(fail) != 0ull || (!um_all && sure != allG)) {
+      if (lane == 0) pend[c] = kPendTriage;
+      wave_sync();
+      continue;
+    }
+    // crit = min, rank = numpy's mean over the G loci (np_sum_seq order), full clade i on lane i
+    double my_r = -__builtin_inf(), my_c = 0.0;
+    for (int i = 0; i < nfull; ++i) {
+      const int base = i * G;
+      const int m8 = G < 8 ? 0 : G - (G & 7);
+      double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
+      double mn = __builtin_inf();
+      for (int u = 0; u < m8; ++u) {
+        const double x = lane_bcast(mean, base + u);
+        mn = x < mn ? x : mn;
+        switch (u & 7) {
+          case 0: r0 += x; break;
+          case 1: r1 += x; break;
+          case 2: r2 += x; break;
+          case 3: r3 += x; break;
+          case 4: r4 += x; break;
+          case 5: r5 += x; break;
+          case 6: r6 += x; break;
+          default: r7 += x; break;
+        }
+      }
+      double res = m8 > 0 ? leaf_tree(r0, r1, r2, r3, r4, r5, r6, r7) : 0.0;
+      for (int u = m8; u < G; ++u) {
+        const double x = lane_bcast(mean, base + u);
+        mn = x < mn ? x : mn;
+        res += x;
+      }
+      if (lane == i) { my_r = (0.0 + res) / (double)G; my_c = mn; }
+    }
+    // ---- explain_one (:585-597): options = full clades with crit >= k1; best by (rank, clade) ----
+    const bool mine = lane < nfull;
+    const int my_cl = mine ? F.fcl[lane] : -1;
+    const bool opt = mine && my_c >= P.k1;
+    double br = opt ? my_r : -__builtin_inf(), bcrit = opt ? my_c : 0.0;
+    long long bk = opt ? my_cl : -1;
+    each_stride([&](auto J) {
+      const double r2 = xor_lanes<decltype(J)::value>(br), c2 = xor_lanes<decltype(J)::value>(bcrit);
+      const long long k2 = xor_lanes<decltype(J)::value>(bk);
+      if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
+    });
+    if (bk < 0) {                                      // no option: explain_two (the wave form)
+      if (lane == 0) pend[c] = kPendTriage;
+      wave_sync();
+      continue;
+    }
+    // meld_one (:621-631): options within --range of the best, LCA of their clades
+    int nm = 0, lca = (int)bk;
+    const bool in = P.dis1 == 1 && opt && (br - my_r) <= P.range;
+    const uint64_t inm = __ballot(in);
+    if (P.dis1 == 1) {
+      nm = __popcll(inm);
+      if (nm == 0) {                                   // negative --range: the wave form's status
+        if (lane == 0) pend[c] = kPendTriage;
+        wave_sync();
+        continue;
+      }
+      int acc = in ? my_cl : -1;
+      each_stride([&](auto J) { acc = lca2(K, acc, xor_lanes<decltype(J)::value>(acc)); });
+      lca = acc;
+      // melded clades in ascending id order (the wave form's segment order)
+      int pos = 0;
+      for (uint64_t rest = inm; rest; rest &= rest - 1) pos += lane_bcast(my_cl, __builtin_ctzll(rest)) < my_cl ? 1 : 0;
+      if (in) K.meld[2 * h0 + 2 * (int64_t)c + pos] = my_cl;
+    }
+    // ---- the record (set_synteny_one: every locus 'A') ----
+    if (lane < G) K.syn[l0 + lane] = 'A';
+    if (ann_on && lane < nann) K.annot[l0 * nsys + lane] = F.ahit[lane];
+    if (lane == 0) {
+      K.call[c] = WF_CALL_NO_LGT;
+      K.crit[c] = bcrit;
+      K.rank[c] = br;
+      K.c1[c] = lca;
+      K.c2[c] = -1;
+      K.nm1[c] = nm;
+      K.iters[c] = 1;
+      K.pair_evals[c] = 0;
+      ccnt[c] = 0;
+      cleaves[c] = 0;
+      pend[c] = 0;
+    }
+    wave_sync();                                       // the slice is reused by the next contig
+  }
+}
+
+}  // namespace
+
+hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int cus, hipStream_t s) {
+  static const int per_cu = [] {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_triage), 64, 0) !=
+            hipSuccess || b < 1)
+      b = 1;
+    return b;
+  }();
+  const int N = sa.k.n_contigs;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * per_cu));
+  hipLaunchKernelGGL(k_triage, dim3(grid), dim3(64), 0, s, sa, ccnt, cleaves, pend);
+  return hipGetLastError();
+}
+
+}  // namespace wf

@@ -15,10 +15,10 @@ CALL_UNCLASSIFIED, CALL_NO_LGT, CALL_LGT = 0, 1, 2
 MODE_STAGED = 0
 MODE_LEVEL0 = 2
 MODE_WAVES = 3
-OPT_SPARSE_BIG, OPT_ATT_LIMIT, OPT_WAVE_TWO, OPT_DUMP_CAP = 1, 2, 3, 4   # wf_set_option
-PHASES = ("waves", "attach", "segments", "decide", "big", "handover", "rollup")   # wf_phase 0..6
+OPT_SPARSE_BIG, OPT_ATT_LIMIT, OPT_WAVE_TWO, OPT_DUMP_CAP, OPT_TRIAGE = 1, 2, 3, 4, 5   # wf_set_option
+PHASES = ("waves", "attach", "segments", "decide", "big", "handover", "rollup", "triage")   # wf_phase 0..7
 N_PHASES = 8
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _P = C.c_void_p
 
