@@ -572,7 +572,10 @@ def main():
                               "on the cfg5 stress leg (`k2`); the mask-class search "
                               "evaluates far fewer pairs",
         "calls": {"lgt": int(n_lgt), "no_lgt": int(n_no), "unclassified": int(n_un),
-                  "rolled_up": int(n_up)},
+                  "rolled_up": int(n_up),
+                  "iterations_rank0": {int(k): int(v) for k, v in
+                                       enumerate(np.bincount(iters[calls != 0].astype(np.int64)))
+                                       if v}},
         "main_k2_counts": dict(k2_counts, pair_evals_per_sec=pairs / (elapsed / args.steps)),
         "kernel_ms": dict({"wf_score_pass": pass_ms},
                           **{"phase_" + k: v[0] / max(1, tm.passes)

@@ -20,6 +20,10 @@ PHASES = ["loci+lut", "hits/attach", "annotations", "sort", "segments", "prune s
           "pass select", "one-run means p0", "post-pass", "dump/level end", "record/end",
           "one-run means p6", "multi means p0", "multi means p1/7/6/2/4/5", "one-run means p1/7/2/4/5",
           "means prep (all passes)"]
+# k_triage laps (wf_triage.hip TLAP), per contig it decided
+TRIAGE_PHASES = ["offsets, hits, loci, set-up", "attachments", "candidate inserts",
+                 "masks, annotation pass 1", "full-clade scan", "segments, annotation pass 2",
+                 "gene scores", "mask, crit, rank", "explain_one, meld_one, record"]
 STATS = {16: "contigs", 17: "attachments", 18: "segments", 19: "pass iterations",
          20: "segments listed", 21: "dumps", 22: "handed on", 23: "hits"}
 
@@ -53,6 +57,7 @@ def main():
             torch.cuda.synchronize()
             so.wf_stamps_reset_fast()
             so.wf_stamps_reset_sparse()
+            so.wf_stamps_reset_triage()
         assert so.wf_score(h, C.byref(db.bs), C.byref(params), C.byref(db.rs)) == 0
     torch.cuda.synchronize()
     st = (C.c_ulonglong * 48)()
@@ -80,6 +85,13 @@ def main():
                            "candidate pairs", "pass 1 ranks", "pass 2, eval_two, meld, record"])},
                       "per_contig": {"segments": w[9] / max(1, w[8]), "potential clades": w[10] / max(1, w[8]),
                                      "candidate pairs": w[11] / max(1, w[8])}}}
+    tr = (C.c_ulonglong * 16)()
+    so.wf_stamps_read_triage.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    so.wf_stamps_read_triage(tr, 16)
+    t = [int(x) for x in tr]
+    nt = max(1, t[15])
+    out["triage"] = {"decided_sampled": t[15], "cycles_per_contig": sum(t[:9]) / nt,
+                     "phases": {k: t[i] / nt for i, k in enumerate(TRIAGE_PHASES)}}
     print(json.dumps(out))
     for p, d in out["phases"].items():
         print("{:24s} {:10.0f} cyc  {:5.1f}%".format(p, d["cycles_per_contig"], 100 * d["frac"]),

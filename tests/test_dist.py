@@ -44,14 +44,18 @@ def _worker(rank, port, outdir, fail_rank):
         batch, tax = synth.to_batch(data, with_codes=False)
         inner = _oracle_scorer(data, tax)
 
-        def score(sub):
+        def score(sub, stax, a, b):
+            assert sub.n_contigs == b - a and np.array_equal(sub.hit_qlo, batch.slice(a, b).hit_qlo)
+            assert list(stax.parent) == list(tax.parent)
+            sub = batch.slice(a, b)                   # (the oracle reads names and annotations)
             if rank == fail_rank:
                 err = L.WaafleHipError(L.WF_E_RUNAWAY, "runaway")
                 err.contigs = np.array([1])
                 raise err
             return inner(sub)
         try:
-            res = wdist.score_ranked(batch, tax, None, score, dist)
+            res = wdist.score_ranked(batch if rank == 0 else None, tax if rank == 0 else None,
+                                     None, score, dist)
             outcome = "ok"
         except L.WaafleHipError as exc:
             res, outcome = None, "err:{}:{}".format(exc.code, list(exc.contigs))

@@ -41,7 +41,8 @@ def _rank_main(rank, port, outdir):
         scorer = engine.GpuScorer(0)          # the device override: every rank on device 0
         try:
             scorer.set_taxonomy(tax)
-            got = wdist.score_ranked(batch, tax, params, lambda sub: scorer.score(sub, params), dist)
+            got = wdist.score_ranked(batch if rank == 0 else None, tax if rank == 0 else None, params,
+                                     lambda sub, stax, a, b: scorer.score(sub, params), dist)
             if rank == 0:
                 want = scorer.score(batch, params)
                 np.savez(os.path.join(outdir, "ranked.npz"),
@@ -112,3 +113,40 @@ def test_bench_two_ranks_on_one_device(tmp_path):
     if os.environ.get("WAAFLE_KEEP_BENCH2"):
         with open(os.environ["WAAFLE_KEEP_BENCH2"], "w") as fh:
             fh.write(lines[0] + "\n")
+
+
+def test_cli_two_ranks_one_device_match_one_rank(tmp_path):
+    """The drop-in CLI under torch.distributed.run as 2 ranks on device 0 (WAAFLE_DEVICE_MAP):
+    the inputs are parsed once, on rank 0, which sends rank 1 its cost-balanced contig range
+    as typed arrays; each rank scores exactly its shard's hits; the TSVs are byte-identical
+    to a one-rank run."""
+    import re
+    from waafle_amd import cli, dist as wdist, engine, inputs, synth
+    data = synth.generate(n=600, genes=8, clades=200, seed=63, lgt_frac=0.2)
+    paths = synth.write_text(data, str(tmp_path / "in"))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", WAAFLE_DEVICE_MAP="0,0")
+    one, two = tmp_path / "one", tmp_path / "two"
+    one.mkdir()
+    two.mkdir()
+    r1 = subprocess.run([sys.executable, "-m", "waafle_amd.orgscorer"] + paths + ["--outdir", str(one)],
+                        capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m",
+           "waafle_amd.orgscorer"] + paths + ["--outdir", str(two)]
+    r2 = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    for kind in ("lgt", "no_lgt", "unclassified"):
+        a = (one / "synth.{}.tsv".format(kind)).read_bytes()
+        b = (two / "synth.{}.tsv".format(kind)).read_bytes()
+        assert a == b, kind
+    # each rank scored exactly its shard's hits (rank 0 parsed; rank 1 received its range)
+    batch, _ = inputs.load_inputs(*paths, 200.0, warn=None)
+    params = cli.param_dict(cli.parse_flags([]))
+    bounds = wdist.rank_bounds(engine.contig_cost(batch, params["two_clade_threshold"]), 2)
+    seen = {int(m.group(1)): (int(m.group(2)), int(m.group(3)), int(m.group(4).replace(",", "")))
+            for m in re.finditer(r"rank (\d+): contigs (\d+)\.\.(\d+) \(([\d,]+) hits\)", r2.stderr)}
+    assert sorted(seen) == [0, 1]
+    for r, (a, b) in enumerate(bounds):
+        assert seen[r] == (a, b, int(batch.hit_off[b] - batch.hit_off[a]))
+    assert 0 < bounds[0][1] < batch.n_contigs

@@ -1124,15 +1124,26 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         b = wave_or_dpp(b);
         return b;
       };
-      // Upper bound of segment t's mean.  The roll-up launches, which run several pruned
-      // passes over segments of several attachments each, compute it once per segment in
-      // the prune setup and keep it in the not-evaluated marker, v[t] = -1 - ub (any v < 0
-      // is "not evaluated"; -1 - (-1 - ub) may lose ub's bits below 2^-52, far inside the
-      // bounds' 1e-12 slack); level 0 scans the attachments when asked (most of its
-      // contigs never ask).
+      // Upper bound of segment t's mean, computed once per segment in the prune setup and
+      // kept in the not-evaluated marker, v[t] = -1 - ub (any v < 0 is "not evaluated";
+      // -1 - (-1 - ub) may lose ub's bits below 2^-52, far inside the bounds' 1e-12 slack).
+      // The best attachment score bounds any envelope's mean; a one-attachment segment's
+      // mean is its score times its run's share of the locus up to numpy's rounding (a
+      // pairwise sum of <= 8191 equal terms: relative error < 1e-14), so score x share x
+      // (1 + 2e-12) bounds it too and rules out the partial decoy hits the explain_two
+      // passes (4, 5) would otherwise evaluate.  (With the triage, the first form's level-0
+      // contigs are the explain_two ones: every one of them asks.)
       auto scan_best = [&](int t) -> double {
         const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
         double ub = 0.0;
+        if (ke - kb == 1) {
+          const int slot = slot_at(kb);
+          const uint32_t x = F.lohi[slot];
+          const double sc = F.sc[slot];
+          const int len = F.len[cg_of(F, t).y];
+          const int run = max(0, hi16(x) - lo16(x));
+          return fmin(sc, sc * ((double)run / (double)len) * (1.0 + 2e-12));
+        }
         if (kDescOrder) {                            // best first: past its top bits, nothing higher
           const long long tb0 = desc_tb(F.sc[slot_at(kb)]);
           for (int q = kb; q < ke; ++q) {
@@ -1146,7 +1157,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         return ub;
       };
       auto best_score = [&](int t) -> double {       // (callers: v[t] < 0)
-        return ROLL ? -1.0 - v[t] : scan_best(t);
+        return FULL ? scan_best(t) : -1.0 - v[t];
       };
       int n_pass0 = -1;                                // pass 0's list, built with the run sizes
       if (prune) {
@@ -1178,7 +1189,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           carry = hd[i] ? 64 * i + __ffsll((unsigned long long)hd[i]) - 1 : carry;
           rsz[i] = re - rs[i];
           if (t < ns) {
-            v[t] = ROLL ? -1.0 - scan_best(t) : -1.0;  // not evaluated
+            v[t] = FULL ? -1.0 : -1.0 - scan_best(t);  // not evaluated (first form: its bound)
             rc[t] = (uint8_t)rsz[i];
           }
         }

@@ -175,7 +175,8 @@ struct StagedState;
 // Level-0 triage (wf_triage.hip): pend[c] = 0 for the contigs it finished (explain_one from
 // the full clades), kPendTriage for the rest, which the first wave form then runs (list).
 constexpr int kPendTriage = 9;
-hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int cus, hipStream_t s);
+hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
+                         hipStream_t s);
 // the first wave form over `list` (length *n_dev, on the device) at level 0
 hipError_t launch_fast_list(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
                             const int64_t* n_dev, int max_hits, int cus, hipStream_t s);

@@ -49,6 +49,11 @@ struct SpMember {                // 32 B
 struct SpParent {                // 32 B: parent id (~0: empty), clades >= threshold at a
   unsigned long long key, c1, c2, c3;   // locus: >= 1, >= 2, >= 3 (bit per locus)
 };
+// parent-table slots held in LDS (up to 32 members: at cfg5 a contig has 2); more go to the
+// wave's HBM scratch.  Pass 4 probes the table once per clade run of the contig (~5,000 at
+// the stress shape): in HBM each probe was a dependent global load.
+constexpr int kSpLPar = 64;
+static_assert(kSpLPar * 32 == kSpCls * (8 + 4 + 4), "lpar overlays the class table");
 // per-wave scratch: members (in the order found) | their positions grouped by class | parents
 // | the members' dense rows
 constexpr int64_t kSpOffGidx = (int64_t)kSpMemG * sizeof(SpMember);
@@ -60,10 +65,15 @@ struct SpShared {
   int2 wcg[kSpWin + 64];                     // staged segments: (clade, locus) ...
   double wv[kSpWin + 64];                    // ... and gene score
   unsigned long long mx[64];                 // per-locus max score bits (known clades)
-  unsigned long long ckey[kSpCls];           // class mask (~0: empty)
-  int cmany[kSpCls];                         // the class has at least 2 potential clades
+  union {
+    struct {                                 // the class table (passes 2, 3) ...
+      unsigned long long ckey[kSpCls];       // class mask (~0: empty)
+      int cmany[kSpCls];                     // the class has at least 2 potential clades
+      int cint[kSpCls];                      // class is in a passing pair
+    };
+    SpParent lpar[kSpLPar];                  // ... then (pass 4 on) the parent table, when it fits
+  };
   int ccnt[kSpCls];                          // members of a passing class (pass 3)
-  int cint[kSpCls];                          // class is in a passing pair
   int cls[kSpCls];                           // occupied slots, compacted
   int coff[kSpCls], cfill[kSpCls];           // members of the class: first, filled
   int pair[kSpPairs];                        // passing class pairs: a | b << 16 (a <= b)
@@ -684,6 +694,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     // ---- pass 4: per parent of a member, clades listed under it scoring >= threshold ----
     int pcap = 64;
     while (pcap < 2 * M) pcap <<= 1;
+    if (pcap <= kSpLPar) par = sh.lpar;              // (the class table is done with)
     if (P.sister_on) {
       for (int h = lane; h < pcap; h += 64) par[h].key = ~0ull;
       __threadfence_block();

@@ -147,6 +147,33 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* c
       const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
       return LocView{min(a, b), max(a, b) - min(a, b) + 1, K.lstrand[l0 + g]};
     };
+    // loci ascending and disjoint (the usual GFF) with min_overlap > 0: a hit attaches only to
+    // loci it overlaps, a run found by binary search (the wave kernels' rule) instead of a
+    // test against every locus -- O(H log G) rather than O(H G) for the cfg5 stress contigs
+    bool ordered = lds_loc && P.min_overlap > 0.0;
+    if (ordered) {
+      bool bad = false;
+      for (int g = 1 + tid; g < G; g += kAttNT) bad = bad || s_lo[g] <= s_lo[g - 1] + s_len[g - 1] - 1;
+      ordered = !__syncthreads_or(bad);
+    }
+    // the loci hit h attaches to, in GFF order: f(g, L) for each
+    auto each_locus = [&](int qlo, int qhi, int hs, auto f) {
+      if (ordered) {
+        int g = 0;                                   // first locus ending at or after qlo
+        for (int k = 64; k > 0; k >>= 1)
+          if (g + k <= G && s_lo[g + k - 1] + s_len[g + k - 1] - 1 < qlo) g += k;
+        for (; g < G; ++g) {
+          const LocView L{s_lo[g], s_len[g], s_st[g]};
+          if (L.lo > qhi) break;
+          if (attaches(P, qlo, qhi, hs, L.lo, L.len, L.st)) f(g, L);
+        }
+        return;
+      }
+      for (int g = 0; g < G; ++g) {
+        const LocView L = locus(g);
+        if (attaches(P, qlo, qhi, hs, L.lo, L.len, L.st)) f(g, L);
+      }
+    };
     long long n_tot = 0, nl_tot = 0;
     int64_t base = PASS == 1 ? S.catt_off[c] : 0;
     for (int64_t hb = h0; hb < h1; hb += kAttNT) {
@@ -157,16 +184,13 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* c
       const bool live = h < h1 && K.scov[h] >= P.min_scov;
       if (live) {
         qlo = K.qlo[h]; qhi = K.qhi[h]; hs = K.hstrand[h];
-        for (int g = 0; g < G; ++g) {
-          const LocView L = locus(g);
-          if (attaches(P, qlo, qhi, hs, L.lo, L.len, L.st)) {
-            ++n;
-            if (PASS == 0)
-              nl += lds_loc ? s_nl[g]
-                            : (L.len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
-                                  (S.lut_off[L.len % kNpyBuf + 1] - S.lut_off[L.len % kNpyBuf]);
-          }
-        }
+        each_locus(qlo, qhi, hs, [&](int g, const LocView& L) {
+          ++n;
+          if (PASS == 0)
+            nl += lds_loc ? s_nl[g]
+                          : (L.len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+                                (S.lut_off[L.len % kNpyBuf + 1] - S.lut_off[L.len % kNpyBuf]);
+        });
       }
       if (PASS == 0) {
         n_tot += n;
@@ -197,9 +221,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* c
       const double sc = K.score[h];
       const uint32_t m = ns > 0 ? K.sysmask[h] : 0u;
       const bool ann = m != 0 && sc >= P.annot_ref;
-      for (int g = 0; g < G; ++g) {
-        const LocView L = locus(g);
-        if (!attaches(P, qlo, qhi, hs, L.lo, L.len, L.st)) continue;
+      each_locus(qlo, qhi, hs, [&](int g, const LocView& L) {
         const int h1s = max(0, qlo - L.lo);
         const int h2s = min(L.len - 1, qhi - L.lo);
         const int start = min(h1s, L.len);
@@ -219,7 +241,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* c
             else atomicMax(reinterpret_cast<unsigned long long*>(&S.annot_best[(l0 + g) * ns + b]), dbits(sc));
           }
         }
-      }
+      });
     }
     if (PASS == 0) {
       long long a = n_tot, b = nl_tot;
@@ -355,6 +377,138 @@ __global__ __launch_bounds__(NT) void k_sort_contig(const SArgs S, int n_act,
         for (int w = 1; w < NT / 64; ++w) ns += s_red[w];
     }
     if (tid == 0) S.seg_cnt[cr] = ns;
+    __syncthreads();
+  }
+  if (blockIdx.x == 0 && tid == 0) S.seg_cnt[n_act] = 0;   // exclusive scan -> crank_first
+}
+
+// Contigs of more than kSortMax attachments (up to kRadixMax: the cfg5 stress contigs, ~5,000
+// each), one 512-thread workgroup per contig, LDS radix sort: the contig's 32-bit keys (clade
+// << lb | locus; rank bits added on the way out) and 16-bit attachment indices, ping-pong in
+// LDS, sorted by stable counting passes of 8 bits (3 for the usual 20-bit key).  Per pass
+// each wave owns a contiguous slice of the elements: per-wave digit counts (the lanes of a
+// 64-element chunk that share a digit found by 8 ballots, one LDS add per digit group), a
+// digit-major / wave-minor prefix, then each wave scatters its chunks in order (rank =
+// lanes below with the same digit).  Same order as the bitonic sort of the (key, index)
+// words, so k_seg_build follows unchanged.  (The round-4 bitonic 8,192 sort took 91
+// barrier-separated stages per contig and measured slower than the device radix sort.)
+constexpr int kRadixMax = 8192;
+constexpr int kRadixNT = 512;
+constexpr int kRadixBits = 8;
+constexpr int kRadixBins = 1 << kRadixBits;
+constexpr size_t kRadixLds = (size_t)kRadixMax * 2 * (4 + 2) + (size_t)(kRadixNT / 64) * kRadixBins * 4 + 64;
+
+__global__ __launch_bounds__(kRadixNT) void k_sort_radix(const SArgs S, int n_act, int level, uint64_t* keys,
+                                                       int32_t* vals) {
+  int64_t n_keys_ = 0;
+  lvl_counts(S, n_act, n_keys_);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* const kb0 = reinterpret_cast<uint32_t*>(smem);
+  uint16_t* const ib0 = reinterpret_cast<uint16_t*>(smem + 8 * kRadixMax);
+  // buffer x of the ping-pong pair (keys, indices)
+  auto kb = [&](int x) { return kb0 + x * kRadixMax; };
+  auto ib = [&](int x) { return ib0 + x * kRadixMax; };
+  int* cnt = reinterpret_cast<int*>(smem + 12 * kRadixMax);      // [wave][bin]
+  __shared__ int s_red[kRadixNT / 64];
+  constexpr int kW = kRadixNT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int kbits = S.key_tb + S.key_lb;              // (<= 32: checked on the host)
+  const uint64_t rank_shift = (uint64_t)kbits;
+  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const int c = S.act ? S.act[cr] : cr;
+    const int64_t a0 = S.catt_off[c], a1 = S.catt_off[c + 1];
+    const int n = (int)(a1 - a0);
+    const int64_t base = S.act_base ? S.act_base[cr] : a0;   // level 0: own offsets
+    if (n == 0) {
+      if (tid == 0) S.seg_cnt[cr] = 0;
+      continue;
+    }
+    for (int i = tid; i < n; i += kRadixNT) {
+      kb(0)[i] = (uint32_t)make_key(S, 0, (int)(a0 + i));
+      ib(0)[i] = (uint16_t)i;
+    }
+    // wave w's slice [lo, hi) of the elements
+    const int per = (n + kW - 1) / kW;
+    const int lo = min(n, w * per), hi = min(n, lo + per);
+    int cur = 0;
+    for (int shift = 0; shift < kbits; shift += kRadixBits) {
+      for (int i = tid; i < kW * kRadixBins; i += kRadixNT) cnt[i] = 0;
+      __syncthreads();
+      // the lanes of this chunk with the same digit (d), from 8 ballots
+      auto group = [&](int i, int& d) -> uint64_t {
+        const bool live = i < hi;
+        d = live ? (int)((kb(cur)[i] >> shift) & (kRadixBins - 1)) : 0;
+        uint64_t m = __ballot(live);
+#pragma unroll
+        for (int b = 0; b < kRadixBits; ++b) {
+          const uint64_t bal = __ballot((d >> b) & 1);
+          m &= ((d >> b) & 1) ? bal : ~bal;
+        }
+        return live ? m : 0ull;
+      };
+      for (int i0 = lo; i0 < hi; i0 += 64) {           // per-wave digit counts
+        int d;
+        const uint64_t m = group(i0 + lane, d);
+        if (m && (m & below) == 0ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's first lane)
+      }
+      __syncthreads();
+      // offsets: digit-major, wave-minor (thread d walks the waves of digit d, then a scan of
+      // the digit totals across the block)
+      int tot = 0;
+      if (tid < kRadixBins)
+        for (int x = 0; x < kW; ++x) {
+          const int v = cnt[x * kRadixBins + tid];
+          cnt[x * kRadixBins + tid] = tot;
+          tot += v;
+        }
+      // exclusive scan of the 256 digit totals (threads 0..255 = waves 0..3)
+      int incl = tot;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (lane == 63) s_red[w] = incl;
+      __syncthreads();
+      if (tid < kRadixBins) {
+        int pre = incl - tot;
+        for (int x = 0; x < w; ++x) pre += s_red[x];
+        for (int x = 0; x < kW; ++x) cnt[x * kRadixBins + tid] += pre;
+      }
+      __syncthreads();
+      // scatter, each wave its chunks in order (stable)
+      for (int i0 = lo; i0 < hi; i0 += 64) {
+        int d;
+        const uint64_t m = group(i0 + lane, d);
+        if (m) {
+          const int pos = cnt[w * kRadixBins + d] + __popcll(m & below);
+          kb(cur ^ 1)[pos] = kb(cur)[i0 + lane];
+          ib(cur ^ 1)[pos] = ib(cur)[i0 + lane];
+        }
+        wave_sync();                                   // (reads of the counts before the update)
+        if (m && (m >> lane) == 1ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's last lane)
+        wave_sync();
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+    int ns = 0;                                      // distinct keys = segments
+    const uint64_t crank_bits = (uint64_t)cr << rank_shift;
+    for (int t = tid; t < n; t += kRadixNT) {
+      const uint32_t k = kb(cur)[t];
+      keys[base + t] = crank_bits | (uint64_t)k;
+      vals[base + t] = (int)(a0 + (int64_t)ib(cur)[t]);
+      ns += (t == 0 || k != kb(cur)[t - 1]) ? 1 : 0;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off, 64);
+    if (lane == 0) s_red[w] = ns;
+    __syncthreads();
+    if (tid == 0) {
+      for (int x = 1; x < kW; ++x) ns += s_red[x];
+      S.seg_cnt[cr] = ns;
+    }
     __syncthreads();
   }
   if (blockIdx.x == 0 && tid == 0) S.seg_cnt[n_act] = 0;   // exclusive scan -> crank_first
@@ -1257,6 +1411,12 @@ struct Buf {
 }  // namespace
 
 
+// levels whose largest contig has 4,097..8,192 attachments: the per-contig LDS radix sort
+// (k_sort_radix, 1) or the device radix sort of the whole level (0)
+#ifndef WF_RADIX_LDS
+#define WF_RADIX_LDS 1
+#endif
+
 struct StagedState {
   int device = 0;
   int cus = 256;
@@ -1549,6 +1709,13 @@ struct PendIs {
   int v;
   __host__ __device__ bool operator()(int32_t p) const { return p == v; }
 };
+// pend 1 (staged from level 0) with at most `cap` attachments (the second wave form's slice)
+struct PendFits {
+  const int32_t* pend;
+  const int64_t* cnt;
+  int64_t cap;
+  __host__ __device__ bool operator()(int i) const { return pend[i] == 1 && cnt[i] <= cap; }
+};
 
 // attachments of list[i] (0 at and past the device count *n): the exclusive scan of it gives
 // each listed contig's compact key base, and its element N the list's key total
@@ -1717,13 +1884,14 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         da.fail_ctr = rcnt + kMaxIter + 2;
       }
     }
-    if (st->triage && max_hits <= 256) {
+    if (st->triage) {
       // the triage (wf_triage.hip) decides the contigs explain_one settles from their full
       // clades; the first wave form runs the rest from its list (count on the device)
       ST_TRY(st->tri_list.ensure(s, (size_t)N * 4));
       ST_TRY(st->tri_cnt.ensure(s, 8));
       const int t_tri0 = t_mark(st, s);                 // (the triage span: its launch alone)
-      ST_TRY(launch_triage(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), st->cus, s));
+      ST_TRY(launch_triage(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
+                           st->cus, s));
       const int t_tri = t_mark(st, s);
       t_span(st, WF_PHASE_WAVES, t_waves, t_tri0);
       t_span(st, WF_PHASE_TRIAGE, t_tri0, t_tri);
@@ -1800,9 +1968,12 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     }
     // the other contigs it handed over (pend 1) through the second wave form, its list and
     // count built on the device
-    using PendIt1 = hipcub::TransformInputIterator<bool, PendIs, const int32_t*>;
-    ST_TRY(select_list(st, s, PendIt1(st->pend.as<int32_t>(), PendIs{1}), st->act0.as<int32_t>(),
-                       st->red.as<int64_t>() + 3, N));
+    // (only those whose attachments fit the second form's slice: the others would load every
+    // hit only to be handed on again)
+    using FitIt = hipcub::TransformInputIterator<bool, PendFits, hipcub::CountingInputIterator<int>>;
+    ST_TRY(select_list(st, s, FitIt(hipcub::CountingInputIterator<int>(0),
+                                    PendFits{st->pend.as<int32_t>(), st->cnt.as<int64_t>(), max_hits <= 256 ? 256 : 512}),
+                       st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, N));
 #ifndef WF_NO_FULL
     ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                        st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
@@ -1884,6 +2055,8 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   if (max_att <= kSortMax && sa.key_tb + sa.key_lb + kSortIdxBits <= 64) {
     sa.sort_cap = 2;
     while (sa.sort_cap < max_att) sa.sort_cap <<= 1;
+  } else if (WF_RADIX_LDS && max_att <= kRadixMax && sa.key_tb + sa.key_lb <= 32) {
+    sa.sort_cap = kRadixMax;                        // the LDS radix sort (k_sort_radix)
   }
   if (A >= st->att_limit || TLB >= (int64_t(1) << 31) - 1) {
     *err = "too many hit-locus attachments for one batch (split it)";
@@ -2016,7 +2189,14 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     const int t_seg = t_mark(st, s);
     if (n_keys > 0) {
       size_t need = st->tmp.n;
-      if (sa.sort_cap > 0) {
+      if (sa.sort_cap > kSortMax) {
+        static const hipError_t rattr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_radix),
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                            (int)kRadixLds);
+        ST_TRY(rattr);
+        hipLaunchKernelGGL(k_sort_radix, dim3(std::min(n_act, st->cus)), dim3(kRadixNT), kRadixLds, s, sa, n_act,
+                           level, kbuf.Current(), vbuf.Current());
+      } else if (sa.sort_cap > 0) {
         const size_t lds = (size_t)sa.sort_cap * 8;
         const int per_cu = std::min(32, std::max(1, (int)((160 * 1024) / lds)));
         // level 0: one wave per contig (10^4+ contigs fill the chip); later levels have

@@ -31,12 +31,30 @@
 #include "wf_lanes.h"
 
 #ifndef WF_TRIAGE_WAVES
-#define WF_TRIAGE_WAVES 6              // resident waves per SIMD (75 VGPRs unspilled, a 4.8 KB slice)
+#define WF_TRIAGE_WAVES 8              // resident waves per SIMD (64 VGPRs, ~12 spilled; a 4.8 KB slice).
+                                       // Same box (r5c): 3.66 ms per cfg4 pass against 3.85 at 6
+                                       // waves per SIMD (75 VGPRs, none spilled)
 #endif
 
 namespace wf {
 
 namespace {
+
+// Diagnostic build only (-DWF_STAMPS): per-phase shader-clock laps of every 16th contig the
+// triage takes (scripts/wave_stamps.py prints them).  Never in the product build.
+#ifdef WF_STAMPS
+__device__ unsigned long long g_tstamps[16];
+#define TLAP_MARK() unsigned long long tlap_ = __builtin_amdgcn_s_memtime(); const bool tsamp_ = (c & 15) == 0
+#define TLAP(i)                                                                     \
+  do {                                                                              \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
+    if (tsamp_ && lane == 0) atomicAdd(&g_tstamps[i], n_ - tlap_);                  \
+    tlap_ = n_;                                                                     \
+  } while (0)
+#else
+#define TLAP_MARK() do {} while (0)
+#define TLAP(i) do {} while (0)
+#endif
 
 constexpr int kTrHB = 4;               // hit batches of 64: contigs of up to 256 hits
 constexpr int kTrLoc = 64;             // loci (64-bit locus masks)
@@ -45,6 +63,7 @@ constexpr int kTrSeg = 64;             // full clades x loci evaluated (one lane
 constexpr int kTrSpan = 26;            // loci one hit may attach to, from its first candidate
 constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
 constexpr int kTrXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
+constexpr int kTrBig = 512;            // more hits than any wave slice: k_count
 
 struct TriSmem {
   int lo[kTrLoc], hi[kTrLoc];          // locus site ranges (min, max of start/end)
@@ -89,10 +108,15 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
   for (int it = 0;; ++it) {
     const int c = xmap ? (it * kTrXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
     if (c >= N) break;
+    TLAP_MARK();
     const SArgs& S = kernarg_fresh<SArgs>(S_arg);
     const KArgs& K = S.k;
     const DevParams& P = K.p;
     const int nsys = K.n_sys;
+    // a contig the triage does not decide goes on to the wave form
+    auto hand_on = [&]() {
+      if (lane == 0) pend[c] = kPendTriage;
+    };
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     const int64_t nh = h1 - h0;
     const int64_t hend = min(h1, h0 + 64 * kTrHB);
@@ -132,7 +156,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
         P.k1 > 0.0 && P.weak != 2 &&
         __ballot(lane < G && ((lane >= 1 && my_lo <= prev_hi) || my_hi - my_lo + 1 >= kNpyBuf)) == 0ull;
     if (!take) {
-      if (lane == 0) pend[c] = kPendTriage;
+      hand_on();
       continue;
     }
     const uint64_t allG = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
@@ -144,6 +168,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
     F.abest[lane] = 0ull; F.ahit[lane] = -1;
     F.scnt[lane] = 0; F.sfw[lane] = 0ull;
     wave_sync();
+    TLAP(0);                                           // (stamps: offsets, hits, loci, slice set-up)
     // ---- hits -> attachments (orgscorer.py:359-369): per batch, the first locus ending at or
     // after qlo, then the loci up to the one starting past qhi; attached loci relative to the
     // first: g0 | mask << 6 (0: none) ----
@@ -175,6 +200,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       }
       r_am[b] = am;
     }
+    TLAP(1);                                           // (stamps: attachments)
     // ---- the candidates: clades attached to locus 0 ----
 #pragma unroll
     for (int b = 0; b < kTrHB; ++b) {
@@ -190,11 +216,12 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       }
     }
     if (__ballot(bad) != 0ull) {
-      if (lane == 0) pend[c] = kPendTriage;
+      hand_on();
       wave_sync();
       continue;
     }
     wave_sync();
+    TLAP(2);                                           // (stamps: candidate inserts)
     // ---- every attachment ORs its loci into its clade's mask (r_cl becomes the clade's table
     // slot, -1 outside the table); annotation pass 1 (:383-392) ----
 #pragma unroll
@@ -222,6 +249,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       r_cl[b] = found;
     }
     wave_sync();
+    TLAP(3);                                           // (stamps: masks, annotation pass 1)
     // full clades (every locus in the mask), numbered in table order (lane i: slots i, i + 64)
     int nfull = 0;
 #pragma unroll
@@ -235,11 +263,12 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       nfull += __popcll(fm);
     }
     if (nfull == 0 || nfull * G > kTrSeg) {            // explain_two (no full clade), or the wave form
-      if (lane == 0) pend[c] = kPendTriage;
+      hand_on();
       wave_sync();
       continue;
     }
     wave_sync();
+    TLAP(4);                                           // (stamps: full-clade scan)
     // ---- the full clades' attachments per segment; annotation pass 2: the last hit (largest
     // index) at the best score ----
 #pragma unroll
@@ -290,6 +319,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       }
     }
     wave_sync();
+    TLAP(5);                                           // (stamps: segments, annotation pass 2)
     // ---- gene scores (:399-406), lane per segment: one envelope run, exact numpy mean ----
     const int nseg = nfull * G;
     const int my_g = lane % G, my_f = lane / G;
@@ -309,15 +339,19 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
         fail = true;                                   // several envelope runs: the wave form
       }
       hi = max(hi, lo);
-      mean = (0.0 + pw_run_sum(len, lo, hi, v)) / (double)len;   // (= pw_const_sum on [0, len))
+      // (a whole-locus run -- the usual owner hit -- by the shorter closed form; pw_run_sum
+      // gives the same bits there, tests/test_pw_const.py)
+      const double sum = (lo <= 0 && hi >= len) ? pw_const_sum(len, v) : pw_run_sum(len, lo, hi, v);
+      mean = (0.0 + sum) / (double)len;
     }
+    TLAP(6);                                           // (stamps: gene scores)
     // every locus unmasked (:420-427): a full known clade's mean >= kmin on it (penalize and
     // kmin <= 0 mask nothing)
     const bool sure_l = lane < nseg && F.fcl[my_f] != K.unknown && mean >= P.kmin;
     const uint64_t sure = wave_or_dpp(sure_l ? 1ull << my_g : 0ull);
     const bool um_all = P.weak != 0 || P.kmin <= 0.0;
     if (__ballot(fail) != 0ull || (!um_all && sure != allG)) {
-      if (lane == 0) pend[c] = kPendTriage;
+      hand_on();
       wave_sync();
       continue;
     }
@@ -350,6 +384,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       }
       if (lane == i) { my_r = (0.0 + res) / (double)G; my_c = mn; }
     }
+    TLAP(7);                                           // (stamps: mask, crit and rank)
     // ---- explain_one (:585-597): options = full clades with crit >= k1; best by (rank, clade) ----
     const bool mine = lane < nfull;
     const int my_cl = mine ? F.fcl[lane] : -1;
@@ -362,7 +397,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       if (better(r2, k2, br, bk)) { br = r2; bk = k2; bcrit = c2; }
     });
     if (bk < 0) {                                      // no option: explain_two (the wave form)
-      if (lane == 0) pend[c] = kPendTriage;
+      hand_on();
       wave_sync();
       continue;
     }
@@ -373,7 +408,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
     if (P.dis1 == 1) {
       nm = __popcll(inm);
       if (nm == 0) {                                   // negative --range: the wave form's status
-        if (lane == 0) pend[c] = kPendTriage;
+        hand_on();
         wave_sync();
         continue;
       }
@@ -402,12 +437,88 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       pend[c] = 0;
     }
     wave_sync();                                       // the slice is reused by the next contig
+    TLAP(8);                                           // (stamps: explain_one, meld_one, record)
+#ifdef WF_STAMPS
+    if (tsamp_ && lane == 0) atomicAdd(&g_tstamps[15], 1ull);
+#endif
+  }
+}
+
+// The staged path's counts of the contigs of more hits than any wave slice (the cfg5 stress
+// shape; k_triage hands them on): attachments and numpy leaves (k_wave's ccnt /
+// cleaves, with the ordered-loci binary search), pend 1 -- straight to the staged kernels,
+// where the wave forms would load every hit only to find the contig does not fit.
+// Unordered or overlapping loci, more than 64, --min-overlap 0: left to the wave form
+// (pend kPendTriage).  Launched after k_triage, only when the batch has such contigs.
+__global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend) {
+  __shared__ int s_lo[kTrLoc], s_hi[kTrLoc];
+  __shared__ int8_t s_st[kTrLoc];
+  const KArgs& K = S.k;
+  const DevParams& P = K.p;
+  const int lane = threadIdx.x;
+  for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
+    const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
+    if (h1 - h0 <= kTrBig) continue;                 // (k_triage handed it on: pend kPendTriage)
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    int clo = 0, chi = -1, cst = 0;
+    if (lane < G && G <= kTrLoc) {
+      const int a = K.lstart[l0 + lane], e = K.lend[l0 + lane];
+      clo = min(a, e);
+      chi = max(a, e);
+      cst = K.lstrand[l0 + lane];
+    }
+    const int cprev = __shfl_up(chi, 1, 64);
+    if (!(G > 0 && G <= kTrLoc && P.min_overlap > 0.0 && __ballot(lane < G && lane >= 1 && clo <= cprev) == 0ull))
+      continue;
+    if (lane < G) { s_lo[lane] = clo; s_hi[lane] = chi; s_st[lane] = (int8_t)cst; }
+    wave_sync();
+    long long n_att = 0, nl = 0;
+    for (int64_t hb = h0; hb < h1; hb += 64) {
+      const int64_t h = hb + lane;
+      if (h >= h1 || !(K.scov[h] >= P.min_scov)) continue;
+      const int qlo = K.qlo[h], qhi = K.qhi[h], hs = K.hstrand[h];
+      int g = 0;
+#pragma unroll
+      for (int k = 32; k > 0; k >>= 1)
+        if (g + k <= G && s_hi[g + k - 1] < qlo) g += k;
+      for (; g < G; ++g) {
+        const int lo = s_lo[g];
+        if (lo > qhi) break;
+        const int len = s_hi[g] - lo + 1;
+        if (attaches(P, qlo, qhi, hs, lo, len, s_st[g])) {
+          ++n_att;
+          nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+                (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+        }
+      }
+    }
+    n_att = wave_sum_dpp(n_att);
+    nl = wave_sum_dpp(nl);
+    if (lane == 0) {
+      ccnt[c] = n_att;
+      cleaves[c] = nl;
+      pend[c] = 1;                                   // staged from level 0
+      if (S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);
+    }
+    wave_sync();
   }
 }
 
 }  // namespace
 
-hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int cus, hipStream_t s) {
+#ifdef WF_STAMPS
+extern "C" int wf_stamps_read_triage(unsigned long long* out, int n) {
+  if (n > 16) n = 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
+}
+extern "C" int wf_stamps_reset_triage(void) {
+  unsigned long long z[16] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tstamps), z, sizeof z) == hipSuccess ? 0 : -2;
+}
+#endif
+
+int triage_per_cu() {
   static const int per_cu = [] {
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_triage), 64, 0) !=
@@ -415,9 +526,17 @@ hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32
       b = 1;
     return b;
   }();
+  return per_cu;
+}
+
+hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
+                         hipStream_t s) {
   const int N = sa.k.n_contigs;
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * per_cu));
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * triage_per_cu()));
   hipLaunchKernelGGL(k_triage, dim3(grid), dim3(64), 0, s, sa, ccnt, cleaves, pend);
+  if (max_hits > kTrBig)
+    hipLaunchKernelGGL(k_count, dim3((unsigned)std::min<int64_t>(N, (int64_t)cus * 32)), dim3(64), 0, s, sa, ccnt,
+                       cleaves, pend);
   return hipGetLastError();
 }
 

@@ -21,25 +21,33 @@ def die(*args):
 def main(argv=None):
     args = cli.build_parser().parse_args(argv)
     say = (lambda *a: None) if args.quiet else inputs.say
-    t0 = time.time()
-    say("Loading inputs.")
-    try:
-        batch, tax = inputs.load_inputs(args.contigs, args.blastout, args.gff, args.taxonomy,
-                                        args.min_gene_length, warn=inputs.say)
-    except (inputs.InputError, ValueError) as exc:
-        die(str(exc))
-    if args.basename is None:
-        args.basename = inputs.basename_of(args.contigs)
-    say("Analyzing {:,} contigs ({:,} hits, {:,} loci) on {} GPU(s).".format(
-        batch.n_contigs, batch.n_hits, batch.n_loci, args.gpus))
-    t1 = time.time()
     rank, world, local = wdist.rank_env()
     group = None
-    if world > 1:   # launched by torch.distributed.run: one process per GPU
-        import torch
+    if world > 1:
+        # launched by torch.distributed.run: one process per GPU.  The inputs are parsed once,
+        # on rank 0, which sends every rank its contig range as typed arrays (host to host:
+        # gloo -- there is no device-side exchange); WAAFLE_DEVICE_MAP (e.g. "0,0") places
+        # the ranks on devices other than their local rank (a rehearsal on one GPU)
         import torch.distributed as group
-        torch.cuda.set_device(local)
-        group.init_process_group("nccl", device_id=torch.device("cuda", local))
+        group.init_process_group("gloo")
+    dmap = os.environ.get("WAAFLE_DEVICE_MAP")
+    device = int(dmap.split(",")[local]) if dmap else local
+    t0 = time.time()
+    batch = tax = None
+    if rank == 0:
+        say("Loading inputs.")
+        try:
+            batch, tax = inputs.load_inputs(args.contigs, args.blastout, args.gff, args.taxonomy,
+                                            args.min_gene_length, warn=inputs.say)
+        except (inputs.InputError, ValueError) as exc:
+            if group is not None:
+                group.destroy_process_group()
+            die(str(exc))
+        if args.basename is None:
+            args.basename = inputs.basename_of(args.contigs)
+        say("Analyzing {:,} contigs ({:,} hits, {:,} loci) on {} GPU(s).".format(
+            batch.n_contigs, batch.n_hits, batch.n_loci, world if group is not None else args.gpus))
+    t1 = time.time()
     det = None
     try:
         if args.write_details:
@@ -55,18 +63,24 @@ def main(argv=None):
         elif group is None:
             res = engine.score(batch, tax, cli.param_dict(args), gpus=args.gpus)
         else:
-            scorer = engine.GpuScorer(local)
-            scorer.set_taxonomy(tax)
-            try:
-                res = wdist.score_ranked(batch, tax, cli.param_dict(args),
-                                         lambda sub: scorer.score(sub, cli.param_dict(args)),
-                                         group)
-            finally:
-                scorer.close()
+            def score_shard(sub, stax, a, b):
+                inputs.say("  rank {}: contigs {}..{} ({:,} hits) on device {}".format(
+                    rank, a, b, sub.n_hits, device))
+                scorer = engine.GpuScorer(device)
+                try:
+                    scorer.set_taxonomy(stax)
+                    return scorer.score(sub, cli.param_dict(args))
+                finally:
+                    scorer.close()
+            res = wdist.score_ranked(batch, tax, cli.param_dict(args), score_shard, group)
     except lib.WaafleHipError as exc:
+        if group is not None:
+            group.destroy_process_group()
         if exc.code == lib.WF_E_RUNAWAY and len(getattr(exc, "contigs", ())):
-            die("  Warning: Runaway taxonomic recursion for",
-                batch.contig_names[int(exc.contigs[0])])
+            if rank == 0:
+                die("  Warning: Runaway taxonomic recursion for",
+                    batch.contig_names[int(exc.contigs[0])])
+            sys.exit("EXITING.")
         die(str(exc))
     t2 = time.time()
     if group is not None:
