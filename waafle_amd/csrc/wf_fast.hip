@@ -800,7 +800,17 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
   const bool xmap = WF_XCD_MAP && gridDim.x % kXcds == 0;
   const int xb = (int)gridDim.x / kXcds, xj = (int)blockIdx.x / kXcds, xx = (int)blockIdx.x % kXcds;
   for (int it = 0;; ++it) {
-    const int ci = xmap ? (it * kXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
+    int ci;
+    if (S_arg.wq) {
+      // a work queue: a wave takes the list's next contig when it finishes one (the roll-up
+      // lists are ~20 k contigs of very different cost over ~4 k waves: static striding left
+      // the launches tail-bound)
+      unsigned long long q = 0;
+      if (lane == 0) q = atomicAdd(S_arg.wq, 1ull);
+      ci = __builtin_amdgcn_readfirstlane((int)q);
+    } else {
+      ci = xmap ? (it * kXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
+    }
     if (ci >= n_list) break;
     const int c = list ? list[ci] : ci;
     WLAP_MARK();

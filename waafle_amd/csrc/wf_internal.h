@@ -86,7 +86,8 @@ struct SArgs {
   const int32_t* lut_off;        // [kNpyBuf + 2] numpy leaf table offsets by length
   const int4* lut;               // (start, length, parent adds) per leaf
   int64_t dec_lds_bytes;         // LDS arena of the decision workgroup
-  int sort_cap;                  // per-contig LDS sort capacity (power of 2; 0: device radix sort)
+  int sort_cap;                  // per-contig LDS sort capacity: a power of 2 <= 4,096 (bitonic), a
+                                 // multiple of 512 above (the LDS radix sort), 0: device radix sort
   int force_big;                 // WF_OPT_SPARSE_BIG 2: k_one hands every contig over
   int route_sparse;              // WF_OPT_SPARSE_BIG 2, 3: every k_decide contig to k_big_sparse
   int sparse_on;                 // WF_OPT_SPARSE_BIG != 0: k_big_sparse runs
@@ -116,6 +117,8 @@ struct SArgs {
   unsigned long long* roll_next_n;
   unsigned long long* fail_ctr;
   unsigned long long* dump_ctr_next;   // k_dump_sparse zeroes the next level's table counter
+  unsigned long long* wq;        // k_wave over a list: its contigs handed out one at a time by this
+                                 // counter (zeroed per pass), else in static XCD order (null)
 };
 
 // waafle_genecaller (wf_genecall.hip): one contig group per wave

@@ -158,19 +158,25 @@ __device__ __forceinline__ double sp_rank_w(const SpShared& sh, int w, int cl, u
 // is called by every lane of the wave for each 64-segment chunk (is_start false on lanes
 // that hold no run start; t the segment, w its window index), so f may use wave operations.
 // The window holds kSpWin segments plus 64 ahead (clade -2 past the contig's end).
+// The next window's loads are issued before this one is walked (registers, then LDS at the
+// next step), so each step's global round trip overlaps the previous step's run walks
+// instead of stalling the wave (a stress contig is ~20 windows per pass, four passes).
 template <class F>
 __device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, int se, F f) {
   const int lane = threadIdx.x & 63;
   int carry = -1;
-  for (int base = so; base < se; base += kSpWin) {
-    int2 cg[5];
-    double v[5];
+  int2 cg[5];
+  double v[5];
+  auto fetch = [&](int base) {
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
       const int t = base + 64 * j + lane;
       cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
       v[j] = t < se ? S.seg_mean[t] : 0.0;
     }
+  };
+  if (so < se) fetch(so);
+  for (int base = so; base < se; base += kSpWin) {
     __syncthreads();                                 // the previous window is consumed
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
@@ -178,6 +184,7 @@ __device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, in
       sh.wv[64 * j + lane] = v[j];
     }
     __syncthreads();
+    if (base + kSpWin < se) fetch(base + kSpWin);    // (in flight while this window is walked)
 #pragma unroll 1
     for (int j = 0; j < kSpWin / 64; ++j) {
       const int w = 64 * j + lane;
@@ -404,19 +411,29 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   if (lane == 0) { sh.n_used = 0; sh.n_pairs = 0; sh.cnt = 0; sh.over = 0; }
   __syncthreads();
   bool root = false;
-  for (int base = so; base < se; base += 256) {
+  {
     int2 cg[4];
     double v[4];
+    auto fetch = [&](int base) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int t = base + 64 * j + lane;
-      cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
-      v[j] = t < se ? S.seg_mean[t] : 0.0;
-    }
+      for (int j = 0; j < 4; ++j) {
+        const int t = base + 64 * j + lane;
+        cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
+        v[j] = t < se ? S.seg_mean[t] : 0.0;
+      }
+    };
+    if (so < se) fetch(so);
+    for (int base = so; base < se; base += 256) {
+      int2 c2[4];
+      double v2[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      root |= cg[j].x == K.root;
-      if (cg[j].x >= 0 && cg[j].x != K.unknown && v[j] > 0.0) atomicMax(&sh.mx[cg[j].y], dbits(v[j]));
+      for (int j = 0; j < 4; ++j) { c2[j] = cg[j]; v2[j] = v[j]; }
+      if (base + 256 < se) fetch(base + 256);        // (the next step's loads in flight)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        root |= c2[j].x == K.root;
+        if (c2[j].x >= 0 && c2[j].x != K.unknown && v2[j] > 0.0) atomicMax(&sh.mx[c2[j].y], dbits(v2[j]));
+      }
     }
   }
   const bool root_present = __ballot(root) != 0ull;
@@ -1278,11 +1295,15 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
 // The contigs whose dense decision state outgrew the LDS arena (big_list, counters[2]):
 // one wave each with kSpSlot bytes of HBM scratch (S.sp_ws); the ones sp_level declines go
 // to big2_list (counters[1]) for k_decide_big.
-__global__ __launch_bounds__(64) void k_big_sparse(const SArgs S, int level, int64_t n_keys) {
+// S_arg stays the first parameter: the loop body re-reads the argument block through
+// kernarg_fresh (wf_device.h) per contig -- held across the loop, its fields overflowed the
+// SGPR file (309 SGPRs spilled to VGPR lanes: a v_readlane per use, the kernel's SALU excess).
+__global__ __launch_bounds__(64) void k_big_sparse(const SArgs S_arg, int level, int64_t n_keys) {
   __shared__ SpShared sh;
-  char* ws = S.sp_ws + (int64_t)blockIdx.x * kSpSlot;
-  const int count = (int)S.counters[2];
+  char* ws = S_arg.sp_ws + (int64_t)blockIdx.x * kSpSlot;
+  const int count = (int)S_arg.counters[2];
   for (int i = blockIdx.x; i < count; i += gridDim.x) {
+    const SArgs& S = kernarg_fresh<SArgs>(S_arg);
     const int cr = S.big_list[2 * i], c = S.big_list[2 * i + 1];
     const bool ok = sp_level(S, sh, ws, c, cr, level, n_keys);
     if (!ok && threadIdx.x == 0) {
@@ -1310,25 +1331,28 @@ __global__ __launch_bounds__(64) void k_big_sparse(const SArgs S, int level, int
 // KIND 1 takes the compact slots, KIND 0 the whole tables: two kernels, so that sp_two's
 // smaller register file gives it twice the resident waves of sp_level.  A wave reads the
 // headers of 64 of its slots (stride gridDim.x, as one slot per step would) at once.
+// (S_arg first: the per-contig loop re-reads the argument block through kernarg_fresh, as
+// k_big_sparse)
 template <int KIND>
-__global__ __launch_bounds__(64, KIND ? 4 : 2) void k_dump_sparse(const SArgs S, int64_t* ccnt, int64_t* cleaves,
+__global__ __launch_bounds__(64, KIND ? 4 : 2) void k_dump_sparse(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves,
                                                                   int level) {
   using Sh = typename std::conditional<KIND == 1, E2Shared, SpShared>::type;
   __shared__ Sh sh;
   const int lane = threadIdx.x & 63;
+  const SArgs& S0 = S_arg;
   if (KIND == 1) {
-    if (S.dump_ctr_next && blockIdx.x == 0 && lane == 0) *S.dump_ctr_next = 0ull;
-    if (S.anc) {
-      const int up = level == 0 ? S.k.p.jump + 1 : 1;
-      for (int t = blockIdx.x * 64 + lane; t < S.n_tax; t += gridDim.x * 64) {
-        int x = level == 0 ? t : S.anc[t];
-        for (int j = 0; j < up; ++j) x = S.k.parent[x];
-        S.anc[t] = x;
+    if (S0.dump_ctr_next && blockIdx.x == 0 && lane == 0) *S0.dump_ctr_next = 0ull;
+    if (S0.anc) {
+      const int up = level == 0 ? S0.k.p.jump + 1 : 1;
+      for (int t = blockIdx.x * 64 + lane; t < S0.n_tax; t += gridDim.x * 64) {
+        int x = level == 0 ? t : S0.anc[t];
+        for (int j = 0; j < up; ++j) x = S0.k.parent[x];
+        S0.anc[t] = x;
       }
     }
   }
-  char* ws = KIND ? nullptr : S.sp_ws + (int64_t)blockIdx.x * kSpSlot;
-  const int count = (int)(*S.dump_ctr >> 40);
+  char* ws = KIND ? nullptr : S0.sp_ws + (int64_t)blockIdx.x * kSpSlot;
+  const int count = (int)(*S0.dump_ctr >> 40);
   const int stride = (int)gridDim.x;
   for (int base = blockIdx.x; base < count; base += 64 * stride) {
     const int my = base + lane * stride;
@@ -1336,20 +1360,21 @@ __global__ __launch_bounds__(64, KIND ? 4 : 2) void k_dump_sparse(const SArgs S,
     uint64_t hdr = 0;
     int64_t h0 = 0, l0 = 0;
     if (my < count) {
-      const int2 dl = reinterpret_cast<const int2*>(S.dump_list)[my];
+      const int2 dl = reinterpret_cast<const int2*>(S0.dump_list)[my];
       if (dl.x == KIND && dl.y >= 0) {               // (c < 0: its table did not fit, pend 1 stands)
         mc = dl.y;
         if (KIND == 1) {
-          so = S.dump_first[my];
-          se = S.dump_first[my + 1];
-          hdr = S.dump_um[my];
-          h0 = S.k.hit_off[mc];
-          l0 = S.k.loc_off[mc];
-          G = (int)(S.k.loc_off[mc + 1] - l0);
+          so = S0.dump_first[my];
+          se = S0.dump_first[my + 1];
+          hdr = S0.dump_um[my];
+          h0 = S0.k.hit_off[mc];
+          l0 = S0.k.loc_off[mc];
+          G = (int)(S0.k.loc_off[mc + 1] - l0);
         }
       }
     }
     for (uint64_t m = __ballot(mc >= 0); m; m &= m - 1) {
+      const SArgs& S = kernarg_fresh<SArgs>(S_arg);
       const int src = __builtin_ctzll(m);
       const int c = lane_bcast(mc, src);
       bool ok;

@@ -108,11 +108,10 @@ struct LocView {
 };
 
 template <int PASS>
-__global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* ccnt,
+// (S_arg first: the per-contig loop re-reads the argument block through kernarg_fresh)
+__global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_t* ccnt,
                                                        int64_t* cleaves, unsigned long long* cmax,
                                                        const int32_t* list, int n_list) {
-  const KArgs& K = S.k;
-  const DevParams& P = K.p;
   __shared__ int s_lo[kAttLoc], s_len[kAttLoc], s_nl[kAttLoc];
   __shared__ int8_t s_st[kAttLoc];
   __shared__ unsigned long long s_best[kAnnSlots];
@@ -121,6 +120,9 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S, int64_t* c
   __shared__ long long s_red[2][kAttNT / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int i = blockIdx.x; i < n_list; i += gridDim.x) {
+    const SArgs& S = kernarg_fresh<SArgs>(S_arg);
+    const KArgs& K = S.k;
+    const DevParams& P = K.p;
     const int c = list ? list[i] : i;               // list: the contigs k_fast handed over
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     const int64_t l0 = K.loc_off[c];
@@ -396,19 +398,22 @@ constexpr int kRadixMax = 8192;
 constexpr int kRadixNT = 512;
 constexpr int kRadixBits = 8;
 constexpr int kRadixBins = 1 << kRadixBits;
-constexpr size_t kRadixLds = (size_t)kRadixMax * 2 * (4 + 2) + (size_t)(kRadixNT / 64) * kRadixBins * 4 + 64;
+// dynamic LDS for a capacity of `cap` attachments (a multiple of 512): two key and two index
+// buffers, the per-wave digit counts -- 80 KB at cap 6,144 (two workgroups per CU), 104 KB at 8,192
+inline size_t radix_lds(int cap) { return (size_t)cap * 2 * (4 + 2) + (size_t)(kRadixNT / 64) * kRadixBins * 4 + 64; }
 
 __global__ __launch_bounds__(kRadixNT) void k_sort_radix(const SArgs S, int n_act, int level, uint64_t* keys,
                                                        int32_t* vals) {
   int64_t n_keys_ = 0;
   lvl_counts(S, n_act, n_keys_);
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int cap = S.sort_cap;                          // (the level's largest contig, rounded up)
   uint32_t* const kb0 = reinterpret_cast<uint32_t*>(smem);
-  uint16_t* const ib0 = reinterpret_cast<uint16_t*>(smem + 8 * kRadixMax);
+  uint16_t* const ib0 = reinterpret_cast<uint16_t*>(smem + 8 * (size_t)cap);
   // buffer x of the ping-pong pair (keys, indices)
-  auto kb = [&](int x) { return kb0 + x * kRadixMax; };
-  auto ib = [&](int x) { return ib0 + x * kRadixMax; };
-  int* cnt = reinterpret_cast<int*>(smem + 12 * kRadixMax);      // [wave][bin]
+  auto kb = [&](int x) { return kb0 + x * cap; };
+  auto ib = [&](int x) { return ib0 + x * cap; };
+  int* cnt = reinterpret_cast<int*>(smem + 12 * (size_t)cap);    // [wave][bin]
   __shared__ int s_red[kRadixNT / 64];
   constexpr int kW = kRadixNT / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -568,6 +573,77 @@ __global__ __launch_bounds__(64) void k_seg_build(const SArgs S, int n_act, int 
         S.seg_len[seg] = len;
       }
       sbase += __popcll(hm);
+    }
+  }
+}
+
+// k_seg_build for the contigs of the LDS radix sort (4,097..8,192 attachments: the cfg5 stress
+// contigs), one 512-thread workgroup per contig: the same outputs, a chunk of 512 sorted keys
+// per step (segment heads counted per wave by ballot, then across the waves through LDS)
+// instead of one wave stepping 64 keys at a time through ~5,000.
+__global__ __launch_bounds__(kRadixNT) void k_seg_build_wide(const SArgs S, int n_act, int level, int64_t n_keys) {
+  lvl_counts(S, n_act, n_keys);
+  constexpr int kW = kRadixNT / 64;
+  __shared__ int s_glen[64];
+  __shared__ int s_cnt[kW];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (blockIdx.x == 0 && tid == 0 && n_keys > 0) {
+    const int total = S.crank_first[n_act];
+    S.seg_start[total] = (int)n_keys;
+    S.seg_id[n_keys - 1] = total;                    // seg_count()
+  }
+  const KArgs& K = S.k;
+  const uint64_t lmask = (1ull << S.key_lb) - 1, tmask = (1ull << S.key_tb) - 1;
+  for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const int c = S.act ? S.act[cr] : cr;
+    const int n = (int)(S.catt_off[c + 1] - S.catt_off[c]);
+    const int64_t base = S.act_base ? S.act_base[cr] : S.catt_off[c];
+    int sbase = S.crank_first[cr];
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    if (tid < 64 && tid < G) {                       // locus lengths (G <= 64)
+      const int a = K.lstart[l0 + tid], b = K.lend[l0 + tid];
+      s_glen[tid] = max(a, b) - min(a, b) + 1;
+    }
+    __syncthreads();
+    for (int t0 = 0; t0 < n; t0 += kRadixNT) {
+      const int t = t0 + tid;
+      const bool live = t < n;
+      uint64_t key = 0, prev = 0;
+      if (live) {
+        key = S.keys[base + t];
+        prev = t > 0 ? S.keys[base + t - 1] : ~key;
+        const int a = S.vals[base + t];
+        S.satt_lohi[base + t] = make_int2(S.att_lo[a], S.att_hi[a]);
+        S.satt_sc[base + t] = S.att_sc[a];
+      }
+      const bool head = live && key != prev;
+      const uint64_t hm = __ballot(head);
+      if (lane == 0) s_cnt[w] = __popcll(hm);
+      __syncthreads();
+      int before = 0, total = 0;
+#pragma unroll
+      for (int x = 0; x < kW; ++x) {
+        before += x < w ? s_cnt[x] : 0;
+        total += s_cnt[x];
+      }
+      if (head) {
+        const int g = (int)(key & lmask);
+        int len;
+        if (G <= 64) {
+          len = s_glen[g];
+        } else {
+          const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
+          len = max(a, b) - min(a, b) + 1;
+        }
+        const int seg = sbase + before + __popcll(hm & ((1ull << lane) - 1ull));
+        S.seg_start[seg] = (int)(base + t);
+        S.seg_crank[seg] = cr;
+        S.seg_cg[seg] = make_int2((int)((key >> S.key_lb) & tmask), g);
+        S.seg_len[seg] = len;
+      }
+      sbase += total;
+      __syncthreads();                               // (s_cnt reused by the next chunk)
     }
   }
 }
@@ -937,11 +1013,11 @@ __host__ __device__ int64_t arena_bound(int64_t P, int64_t G) {
 
 constexpr int kOneCap = 384;
 
-__global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
+// (S_arg first: the per-contig loop re-reads the argument block through kernarg_fresh --
+// held across the loop it spilled 64 SGPRs)
+__global__ __launch_bounds__(64) void k_one(const SArgs S_arg, int n_act, int level,
                                             int64_t n_keys) {
-  lvl_counts(S, n_act, n_keys);
-  const KArgs& K = S.k;
-  const DevParams& P = K.p;
+  lvl_counts(S_arg, n_act, n_keys);
   __shared__ int2 s_cg[kOneCap];
   __shared__ double s_v[kOneCap];
   __shared__ double s_rank[kOneCap];     // rank of the option whose clade run starts here, or -1
@@ -951,6 +1027,9 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S, int n_act, int level,
   __shared__ int s_cnt;
   const int lane = threadIdx.x;
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
+    const SArgs& S = kernarg_fresh<SArgs>(S_arg);
+    const KArgs& K = S.k;
+    const DevParams& P = K.p;
     const int c = S.act ? S.act[cr] : cr;
     const int64_t l0 = K.loc_off[c];
     const int G = (int)(K.loc_off[c + 1] - l0);
@@ -1411,6 +1490,11 @@ struct Buf {
 }  // namespace
 
 
+// roll-up launches of the first wave form: contigs handed out by a work-queue counter (1) or
+// in static XCD order (0)
+#ifndef WF_WAVE_QUEUE
+#define WF_WAVE_QUEUE 1
+#endif
 // levels whose largest contig has 4,097..8,192 attachments: the per-contig LDS radix sort
 // (k_sort_radix, 1) or the device radix sort of the whole level (0)
 #ifndef WF_RADIX_LDS
@@ -1436,6 +1520,7 @@ struct StagedState {
   int64_t dump_cap = 0;              // WF_OPT_DUMP_CAP (0: max(32 N, 65536))
   int triage = 1;                    // WF_OPT_TRIAGE: level-0 triage before the first wave form
   Buf tri_list, tri_cnt;             // the contigs the triage hands on, and their count
+  Buf wq;                            // roll-up launches' work-queue counters
   Buf roll0, roll1, roll_cnt, anc;   // wave levels: contig lists, per-level counts, ancestors
   // per-phase timing (wf_phase): event pool, this call's spans (phase, begin, end)
   bool timing = false;
@@ -1877,6 +1962,10 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         ST_TRY(st->anc.ensure(s, (size_t)std::max(n_tax, 1) * 4));
         ST_TRY(hipMemsetAsync(st->roll_cnt.p, 0, (kMaxIter + 3) * sizeof(unsigned long long), s));
         rcnt = st->roll_cnt.as<unsigned long long>();
+        if (WF_WAVE_QUEUE) {                          // the roll-up launches' work queues
+          ST_TRY(st->wq.ensure(s, (kMaxIter + 2) * sizeof(unsigned long long)));
+          ST_TRY(hipMemsetAsync(st->wq.p, 0, (kMaxIter + 2) * sizeof(unsigned long long), s));
+        }
         da.n_tax = n_tax;
         da.wave_two = 1;
         da.roll_next = st->roll1.as<int32_t>();     // level L appends to roll[(L + 1) & 1]
@@ -1943,8 +2032,10 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
             la.dump_ctr_next = dctr + ((L + 1) & 1);
             la.roll_next = roll[(L + 1) & 1];
             la.roll_next_n = rcnt + L + 1;
+            la.wq = WF_WAVE_QUEUE ? st->wq.as<unsigned long long>() + L : nullptr;
             ST_TRY(launch_level(la, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                                 roll[L & 1], reinterpret_cast<const int64_t*>(rcnt + L), L, max_hits, st->cus, s));
+            la.wq = nullptr;
             hipLaunchKernelGGL(k_dump_sparse<1>, dim3(grid2), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
                                st->cnt_leaves.as<int64_t>(), L);
             hipLaunchKernelGGL(k_dump_sparse<0>, dim3(grid), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
@@ -2056,7 +2147,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     sa.sort_cap = 2;
     while (sa.sort_cap < max_att) sa.sort_cap <<= 1;
   } else if (WF_RADIX_LDS && max_att <= kRadixMax && sa.key_tb + sa.key_lb <= 32) {
-    sa.sort_cap = kRadixMax;                        // the LDS radix sort (k_sort_radix)
+    sa.sort_cap = (int)((max_att + 511) & ~int64_t(511));   // the LDS radix sort (k_sort_radix)
   }
   if (A >= st->att_limit || TLB >= (int64_t(1) << 31) - 1) {
     *err = "too many hit-locus attachments for one batch (split it)";
@@ -2192,9 +2283,11 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       if (sa.sort_cap > kSortMax) {
         static const hipError_t rattr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_radix),
                                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                            (int)kRadixLds);
+                                                            (int)radix_lds(kRadixMax));
         ST_TRY(rattr);
-        hipLaunchKernelGGL(k_sort_radix, dim3(std::min(n_act, st->cus)), dim3(kRadixNT), kRadixLds, s, sa, n_act,
+        const size_t lds = radix_lds(sa.sort_cap);
+        const int per_cu = std::max(1, (int)((160 * 1024) / lds));
+        hipLaunchKernelGGL(k_sort_radix, dim3(std::min(n_act, st->cus * per_cu)), dim3(kRadixNT), lds, s, sa, n_act,
                            level, kbuf.Current(), vbuf.Current());
       } else if (sa.sort_cap > 0) {
         const size_t lds = (size_t)sa.sort_cap * 8;
@@ -2222,8 +2315,12 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
           hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(kScanNT), 0, s, sa.seg_cnt, sa.crank_first, n_act + 1);
         else
           ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_cnt, sa.crank_first, n_act + 1, s));
-        hipLaunchKernelGGL(k_seg_build, dim3(std::min(n_act, st->cus * 32)), dim3(64), 0, s, sa, n_act,
-                           level, n_keys);
+        if (sa.sort_cap > kSortMax)                   // (the radix-sorted stress contigs)
+          hipLaunchKernelGGL(k_seg_build_wide, dim3(std::min(n_act, st->cus * 4)), dim3(kRadixNT), 0, s, sa, n_act,
+                             level, n_keys);
+        else
+          hipLaunchKernelGGL(k_seg_build, dim3(std::min(n_act, st->cus * 32)), dim3(64), 0, s, sa, n_act,
+                             level, n_keys);
       } else {
         hipLaunchKernelGGL(k_seg_flags, dim3(grid_for(n_keys)), dim3(256), 0, s, sa, n_keys);
         need = st->tmp.n;
