@@ -24,6 +24,10 @@ PHASES = ["loci+lut", "hits/attach", "annotations", "sort", "segments", "prune s
 TRIAGE_PHASES = ["offsets, hits, loci, set-up", "attachments", "candidate inserts",
                  "masks, annotation pass 1", "full-clade scan", "segments, annotation pass 2",
                  "gene scores", "mask, crit, rank", "explain_one, meld_one, record"]
+# sp_level laps (k_big_sparse / k_dump_sparse<0>, wf_sparse.h BLAP), every 8th contig
+SP_LEVEL_PHASES = ["pass 1 maxes", "pass 2 options, classes", "explain_one, meld, record",
+                   "class pairs", "pass 3 members", "groups, dense rows", "pass 4 sisters",
+                   "candidates pass 1", "candidates pass 2", "meld_two, record / raise"]
 STATS = {16: "contigs", 17: "attachments", 18: "segments", 19: "pass iterations",
          20: "segments listed", 21: "dumps", 22: "handed on", 23: "hits"}
 
@@ -92,6 +96,15 @@ def main():
     nt = max(1, t[15])
     out["triage"] = {"decided_sampled": t[15], "cycles_per_contig": sum(t[:9]) / nt,
                      "phases": {k: t[i] / nt for i, k in enumerate(TRIAGE_PHASES)}}
+    bg = (C.c_ulonglong * 16)()
+    so.wf_stamps_read_big.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    so.wf_stamps_read_big(bg, 16)
+    b = [int(x) for x in bg]
+    nb = max(1, b[15])
+    out["sp_level"] = {"sampled": b[15], "cycles_per_contig": sum(b[:10]) / nb,
+                       "phases": {k: b[i] / nb for i, k in enumerate(SP_LEVEL_PHASES)},
+                       "per_contig": {"segments": b[12] / nb, "potential clades": b[13] / nb,
+                                      "members": b[14] / nb}}
     print(json.dumps(out))
     for p, d in out["phases"].items():
         print("{:24s} {:10.0f} cyc  {:5.1f}%".format(p, d["cycles_per_contig"], 100 * d["frac"]),

@@ -514,6 +514,11 @@ __device__ __forceinline__ bool attaches(const DevParams& P, int qlo, int qhi, i
   const int ov = min(qhi, l2) - max(qlo, l1) + 1;
   const int den = min(qhi - qlo + 1, l2 - l1 + 1);
   if (ov == den) return 1.0 >= P.min_overlap;       // one interval inside the other: exactly 1.0
+  // RN(ov / den) >= m decided without the division when ov is clearly above or below den * m
+  // (rounding is monotone; the margins cover den * m's own rounding)
+  const double t = (double)den * P.min_overlap;
+  if ((double)ov > t + fabs(t) * 1e-9) return true;
+  if ((double)ov < t - fabs(t) * 1e-9) return false;
   return (double)ov / (double)den >= P.min_overlap;
 }
 

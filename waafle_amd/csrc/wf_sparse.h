@@ -398,6 +398,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   int* gidx = reinterpret_cast<int*>(ws + kSpOffGidx);
   SpParent* par = reinterpret_cast<SpParent*>(ws + kSpOffPar);
   double* drows = reinterpret_cast<double*>(ws + kSpOffDense);
+  BLAP_MARK(c);
+  BSTAT(15, 1);
+  BSTAT(12, se - so);
 
   // ---- pass 1: per-locus maxes over known clades, root present (:407-411) -------------
   sh.mx[lane] = 0;
@@ -438,6 +441,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   }
   const bool root_present = __ballot(root) != 0ull;
   __syncthreads();
+  BLAP(0);
   // weak loci: ignore -> mask (:420-427), penalize -> none (:413-414)
   const double mxv = __longlong_as_double((long long)sh.mx[lane]);
   const uint64_t keep = __ballot(lane < G && (P.weak != 0 || mxv >= P.kmin));
@@ -522,6 +526,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     if (lane == 0) ins_class(u_k2 & keep);
   }
   __syncthreads();
+  BLAP(1);
+  BSTAT(13, Pp);
 
   if (bk >= 0) {
     // meld_one (:621-631): options within --range of the best
@@ -583,6 +589,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       K.iters[c] = (int16_t)iteration;
       K.pair_evals[c] = pair_evals;
     }
+    BLAP(2);
     return true;
   }
 
@@ -612,6 +619,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     }
   }
   __syncthreads();
+  BLAP(3);
   bool have_ok = false;
   if (sh.n_pairs > 0) {
     if (sh.n_pairs > kSpPairs) return false;
@@ -660,7 +668,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     }
     __threadfence_block();
     __syncthreads();
+    BLAP(4);
     const int M = sh.cnt;
+    BSTAT(14, M);
     if (M > kSpMemG) return false;
     // members grouped by class (gidx), candidate counts per passing class pair
     if (lane == 0) {
@@ -708,6 +718,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     };
     __threadfence_block();
     __syncthreads();
+    BLAP(5);
     // ---- pass 4: per parent of a member, clades listed under it scoring >= threshold ----
     int pcap = 64;
     while (pcap < 2 * M) pcap <<= 1;
@@ -747,6 +758,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       __threadfence_block();
     }
     __syncthreads();
+    BLAP(6);
 
     // ---- pass 1 over the candidates: best by (rank, pair index) ------------------------
     double pr = -__builtin_inf();
@@ -779,6 +791,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     }
     for (int i = lane; i < kSpMemG / 32; i += 64) { sh.bm1[i] = 0; sh.bm2[i] = 0; }
     __syncthreads();
+    BLAP(7);
     // ---- pass 2 over the candidates: options within --range get the LGT filters --------
     sp_for_cands(sh, mem, gidx, [&](int u, int v, const SpMember& mu, const SpMember& mv) {
       const SpRowAcc a = acc(u, mu), b = acc(v, mv);
@@ -793,6 +806,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       atomicOr(&sh.bm2[q2 >> 5], 1u << (q2 & 31));
     });
     __syncthreads();
+    BLAP(8);
     // ---- meld_two (:640-669) ----------------------------------------------------------------
     int kind;   // 0 none, 1 best as is, 2 meld, 3 unchecked best, 4 upstream crash
     const int n_in = sh.n_in;
@@ -859,6 +873,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
         K.iters[c] = (int16_t)iteration;
         K.pair_evals[c] = pair_evals;
       }
+      BLAP(9);
       return true;
     }
   }
@@ -872,6 +887,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       return true;
     }
     sp_raise(S, c, pair_evals);                      // roll up (orgscorer.py:431-445)
+    BLAP(9);
     return true;
   }
   if (lane == 0) {                                   // unclassified after evaluation

@@ -1439,7 +1439,20 @@ __device__ unsigned long long g_sstamps[16];
     slap_ = n_;                                                                     \
   } while (0)
 #define SSTAT(i, v) do { if (ssamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_sstamps[i], (unsigned long long)(v)); } while (0)
+// ... and of sp_level (k_big_sparse, k_dump_sparse<0>) on every 8th contig
+__device__ unsigned long long g_bstamps[16];
+#define BLAP_MARK(c) unsigned long long blap_ = __builtin_amdgcn_s_memtime(); const bool bsamp_ = ((c) & 7) == 0
+#define BLAP(i)                                                                     \
+  do {                                                                              \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
+    if (bsamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_bstamps[i], n_ - blap_);    \
+    blap_ = n_;                                                                     \
+  } while (0)
+#define BSTAT(i, v) do { if (bsamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_bstamps[i], (unsigned long long)(v)); } while (0)
 #else
+#define BLAP_MARK(c) do {} while (0)
+#define BLAP(i) do {} while (0)
+#define BSTAT(i, v) do {} while (0)
 #define SLAP_MARK(c) do {} while (0)
 #define SLAP(i) do {} while (0)
 #define SSTAT(i, v) do {} while (0)
@@ -1452,7 +1465,12 @@ extern "C" int wf_stamps_read_sparse(unsigned long long* out, int n) {
 }
 extern "C" int wf_stamps_reset_sparse(void) {
   unsigned long long z[16] = {0};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_bstamps), z, sizeof z) != hipSuccess) return -2;
   return hipMemcpyToSymbol(HIP_SYMBOL(g_sstamps), z, sizeof z) == hipSuccess ? 0 : -2;
+}
+extern "C" int wf_stamps_read_big(unsigned long long* out, int n) {
+  if (n > 16) n = 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -1494,6 +1512,10 @@ struct Buf {
 // in static XCD order (0)
 #ifndef WF_WAVE_QUEUE
 #define WF_WAVE_QUEUE 1
+#endif
+// ... and the level-0 launch over the triage's list
+#ifndef WF_L0_QUEUE
+#define WF_L0_QUEUE 1
 #endif
 // levels whose largest contig has 4,097..8,192 attachments: the per-contig LDS radix sort
 // (k_sort_radix, 1) or the device radix sort of the whole level (0)
@@ -1962,16 +1984,16 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         ST_TRY(st->anc.ensure(s, (size_t)std::max(n_tax, 1) * 4));
         ST_TRY(hipMemsetAsync(st->roll_cnt.p, 0, (kMaxIter + 3) * sizeof(unsigned long long), s));
         rcnt = st->roll_cnt.as<unsigned long long>();
-        if (WF_WAVE_QUEUE) {                          // the roll-up launches' work queues
-          ST_TRY(st->wq.ensure(s, (kMaxIter + 2) * sizeof(unsigned long long)));
-          ST_TRY(hipMemsetAsync(st->wq.p, 0, (kMaxIter + 2) * sizeof(unsigned long long), s));
-        }
         da.n_tax = n_tax;
         da.wave_two = 1;
         da.roll_next = st->roll1.as<int32_t>();     // level L appends to roll[(L + 1) & 1]
         da.roll_next_n = rcnt + 1;
         da.fail_ctr = rcnt + kMaxIter + 2;
       }
+    }
+    if (WF_WAVE_QUEUE && (levels || st->triage)) {   // work queues: [0] the level-0 list, [L] level L
+      ST_TRY(st->wq.ensure(s, (kMaxIter + 2) * sizeof(unsigned long long)));
+      ST_TRY(hipMemsetAsync(st->wq.p, 0, (kMaxIter + 2) * sizeof(unsigned long long), s));
     }
     if (st->triage) {
       // the triage (wf_triage.hip) decides the contigs explain_one settles from their full
@@ -1988,7 +2010,9 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       using PendItT = hipcub::TransformInputIterator<bool, PendIs, const int32_t*>;
       ST_TRY(select_list(st, s, PendItT(st->pend.as<int32_t>(), PendIs{kPendTriage}), st->tri_list.as<int32_t>(),
                          st->tri_cnt.as<int64_t>(), N));
-      ST_TRY(launch_fast_list(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
+      SArgs ta = da;                                   // (the list's contigs vary in cost as the roll-up lists')
+      ta.wq = WF_WAVE_QUEUE && WF_L0_QUEUE ? st->wq.as<unsigned long long>() : nullptr;
+      ST_TRY(launch_fast_list(ta, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                               st->tri_list.as<int32_t>(), st->tri_cnt.as<int64_t>(), max_hits, st->cus, s));
     } else {
       ST_TRY(launch_fast(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,

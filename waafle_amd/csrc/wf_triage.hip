@@ -71,12 +71,12 @@ struct TriSmem {
   uint64_t tmask[kTrTab];              // loci it is attached to
   uint64_t abest[kTrLoc];              // (locus, system): best annotation score bits
   int ahit[kTrLoc];                    // ... and the last hit at that score
-  // the full clades' segments, slot i * G + g (full clade i, locus g): attachments (bit 16:
-  // one not dominated by a whole-locus attachment), the last attachment's site range and
-  // score, the best score of its whole-locus attachments
+  // the full clades' segments, slot i * G + g (full clade i, locus g): attachments, the last
+  // attachment's site range, the best score of its attachments of a non-empty range and of
+  // its whole-locus attachments (score bits: scores are >= 0)
   int scnt[kTrSeg];
   uint32_t slohi[kTrSeg];
-  double ssc[kTrSeg];
+  uint64_t spart[kTrSeg];
   uint64_t sfw[kTrSeg];
   int fcl[kTrSeg];                     // full clade i: its id
   int8_t tfull[kTrTab];                // table slot -> full clade index (-1: not full)
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
     F.tkey[lane] = kTrEmpty; F.tkey[lane + 64] = kTrEmpty;
     F.tmask[lane] = 0ull; F.tmask[lane + 64] = 0ull;
     F.abest[lane] = 0ull; F.ahit[lane] = -1;
-    F.scnt[lane] = 0; F.sfw[lane] = 0ull;
+    F.scnt[lane] = 0; F.sfw[lane] = 0ull; F.spart[lane] = 0ull;
     wave_sync();
     TLAP(0);                                           // (stamps: offsets, hits, loci, slice set-up)
     // ---- hits -> attachments (orgscorer.py:359-369): per batch, the first locus ending at or
@@ -286,9 +286,11 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
             const uint32_t lh = tr_lohi(r_qlo[b], r_qhi[b], llo, len);
             atomicAdd(&F.scnt[q], 1);
             F.slohi[q] = lh;
-            F.ssc[q] = r_sc[b];
-            // (k_wave's Fw: the best whole-locus score above 0.0)
-            if ((int)(lh & 0xFFFFu) <= 0 && (int)(lh >> 16) >= len && r_sc[b] > 0.0) atomicMax(&F.sfw[q], dbits(r_sc[b]));
+            // (k_wave's Fw: the best whole-locus score above 0.0; an attachment k_wave keeps
+            // has a non-empty range and a score above it, so one exists iff spart > Fw)
+            const int lo = (int)(lh & 0xFFFFu), hi = (int)(lh >> 16);
+            if (lo < hi) atomicMax(&F.spart[q], dbits(r_sc[b]));
+            if (lo <= 0 && hi >= len && r_sc[b] > 0.0) atomicMax(&F.sfw[q], dbits(r_sc[b]));
           }
         if (ann_on && r_m[b] != 0u && r_sc[b] >= P.annot_ref) {
           const int h = (int)(h0 + 64 * b + lane);
@@ -298,24 +300,6 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
               if (((r_m[b] >> s) & 1u) && F.abest[g * nsys + s] == dbits(r_sc[b])) atomicMax(&F.ahit[g * nsys + s], h);
           }
         }
-      }
-      r_cl[b] = fi;
-    }
-    wave_sync();
-    // an attachment the best whole-locus one does not cover (k_wave's "kept")
-#pragma unroll
-    for (int b = 0; b < kTrHB; ++b) {
-      const uint32_t am = r_am[b];
-      const int fi = r_cl[b];
-      if (am == 0u || fi < 0) continue;
-      const int g0 = (int)(am & 63u);
-      for (uint32_t rel = am >> 6; rel; rel &= rel - 1) {
-        const int g = g0 + __builtin_ctz(rel);
-        const int q = fi * G + g;
-        const int llo = F.lo[g], len = F.hi[g] - llo + 1;
-        const uint32_t lh = tr_lohi(r_qlo[b], r_qhi[b], llo, len);
-        if ((int)(lh & 0xFFFFu) < (int)(lh >> 16) && r_sc[b] > __longlong_as_double((long long)F.sfw[q]))
-          atomicOr(&F.scnt[q], 1 << 16);
       }
     }
     wave_sync();
@@ -330,11 +314,13 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       const int len = F.hi[my_g] - F.lo[my_g] + 1;
       int lo = 0, hi = len;
       double v = 0.0;
-      if ((n & 0xFFFF) == 1) {
+      const double vp = __longlong_as_double((long long)F.spart[lane]);
+      const double vw = __longlong_as_double((long long)F.sfw[lane]);
+      if (n == 1) {                                    // (an empty range sums to 0.0 at any v)
         const uint32_t lh = F.slohi[lane];
-        lo = (int)(lh & 0xFFFFu); hi = (int)(lh >> 16); v = F.ssc[lane];
-      } else if ((n >> 16) == 0) {
-        v = __longlong_as_double((long long)F.sfw[lane]);   // dominated by a whole-locus run
+        lo = (int)(lh & 0xFFFFu); hi = (int)(lh >> 16); v = vp;
+      } else if (!(vp > vw)) {
+        v = vw;                                        // dominated by a whole-locus run
       } else {
         fail = true;                                   // several envelope runs: the wave form
       }
@@ -412,9 +398,11 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
         wave_sync();
         continue;
       }
-      int acc = in ? my_cl : -1;
-      each_stride([&](auto J) { acc = lca2(K, acc, xor_lanes<decltype(J)::value>(acc)); });
-      lca = acc;
+      if (nm > 1) {                                    // (one option: its own clade)
+        int acc = in ? my_cl : -1;
+        each_stride([&](auto J) { acc = lca2(K, acc, xor_lanes<decltype(J)::value>(acc)); });
+        lca = acc;
+      }
       // melded clades in ascending id order (the wave form's segment order)
       int pos = 0;
       for (uint64_t rest = inm; rest; rest &= rest - 1) pos += lane_bcast(my_cl, __builtin_ctzll(rest)) < my_cl ? 1 : 0;
