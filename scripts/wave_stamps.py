@@ -103,6 +103,7 @@ def main():
     nb = max(1, b[15])
     out["sp_level"] = {"sampled": b[15], "cycles_per_contig": sum(b[:10]) / nb,
                        "phases": {k: b[i] / nb for i, k in enumerate(SP_LEVEL_PHASES)},
+                       "pass 2 split": {"row summaries": b[10] / nb, "class inserts": b[11] / nb},
                        "per_contig": {"segments": b[12] / nb, "potential clades": b[13] / nb,
                                       "members": b[14] / nb}}
     print(json.dumps(out))

@@ -4,6 +4,7 @@ Bar: bit-exact for every integer/index/string field and for the float64 crit/ran
 (the kernels follow numpy's summation order), TSV bytes identical to the reference
 goldens except tie-flagged contigs (output must be one of the reference's outcomes).
 """
+import ctypes as C
 import os
 import subprocess
 import sys
@@ -245,6 +246,57 @@ def test_empty_and_degenerate_contigs(scorer, tmp_path):
         batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
         got = gpu_score(scorer, batch, tax, flags)
         assert_same_results(got, oracle_for(("degenerate",) + tuple(flags), paths, flags, batch, tax), batch)
+
+
+def _decline_case(tmp_path):
+    """One contig, 16 loci of 300 sites, 240 species each with one full-length hit on one
+    locus, two species per genus on the 120 distinct locus pairs, every genus under one
+    family.  Level 0: 240 potential clades (the whole table: sp_level), 16 one-locus classes,
+    no pair covers the contig -> raised.  Level 1: 120 genera with 120 distinct two-locus
+    masks, past sp_level's class table (96 of 128 slots) -> the wave levels decline the
+    contig after a raise.  Level 2: the family covers every locus -> explain_one."""
+    import itertools
+    pairs = list(itertools.combinations(range(16), 2))
+    starts = [1 + 350 * g for g in range(16)]
+    clen = starts[-1] + 400
+    (tmp_path / "d.fna").write_text(">dec\n" + "N" * clen + "\n")
+    (tmp_path / "d.gff").write_text("".join("dec\tx\tgene\t{}\t{}\t.\t+\t0\t.\n".format(s, s + 299)
+                                            for s in starts))
+    rows, tax = [], ["f__F\tr__Root"]
+    for j, (a, b) in enumerate(pairs):
+        tax.append("g__G{}\tf__F".format(j))
+        for k, g in enumerate((a, b)):
+            sp = "s__S{}_{}".format(j, k)
+            tax.append("{}\tg__G{}".format(sp, j))
+            rows.append("dec\tH{}_{}|{}|KO=K1\t{}\t300\t300\t{}\t{}\t1\t300\t99.{:03d}\t300\t0\t0.0\t9\tplus"
+                        .format(j, k, sp, clen, starts[g], starts[g] + 299, (7 * j + k) % 1000))
+    (tmp_path / "d.blastout").write_text("\n".join(rows) + "\n")
+    (tmp_path / "d.tsv").write_text("\n".join(tax) + "\n")
+    return [str(tmp_path / f) for f in ("d.fna", "d.blastout", "d.gff", "d.tsv")]
+
+
+def test_wave_levels_decline_after_a_raise(scorer, tmp_path):
+    """A contig the wave levels decline at roll-up level 1 (sp_level's class
+    table outgrown after the level-0 raise) is rescored from level 0 by the staged kernels:
+    the records equal the oracle's, no contig is left pending, and in the default form the
+    staged phases ran (the early return after the levels did not fire)."""
+    paths = _decline_case(tmp_path)
+    batch, tax = inputs.load_inputs(*paths, 200.0, warn=None)
+    assert batch.n_contigs == 1 and int(batch.hit_off[1]) == 240 and int(batch.loc_off[1]) == 16
+    want = oracle_for(("decline",), paths, [], batch, tax)
+    assert int(want.iterations[0]) == 3 and int(want.call[0]) == lib.CALL_NO_LGT
+    tm = lib.WfTiming()
+    scorer.lib.wf_timing_enable(scorer.h, 1)
+    try:
+        got = gpu_score(scorer, batch, tax, [])
+        assert scorer.lib.wf_timing_read(scorer.h, C.byref(tm)) == 0
+    finally:
+        scorer.lib.wf_timing_enable(scorer.h, 0)
+    assert_same_results(got, want, batch)
+    assert int(got.status[0]) == 0
+    if scorer.form == "level0":
+        ph = tm.phases()
+        assert ph["rollup"][1] > 0 and ph["attach"][1] > 0, ph
 
 
 def test_full_size_cfg2_properties():

@@ -485,7 +485,13 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       h = (h + 1) & (kSpCls - 1);
     }
   };
+#ifdef WF_STAMPS
+  unsigned long long p2_row = 0, p2_ins = 0;        // (stamps: pass 2's row summaries / class inserts)
+#endif
   sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
+#ifdef WF_STAMPS
+    const unsigned long long q0 = __builtin_amdgcn_s_memtime();
+#endif
     bool pot = false;
     uint64_t cmask = 0;
     if (st && !(vu && cl == K.unknown)) {          // (a real "Unknown" run is replaced)
@@ -499,8 +505,20 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     }
     Pp += __popcll(__ballot(pot));
     upi += __popcll(__ballot(pot && cl < K.unknown));
+#ifdef WF_STAMPS
+    const unsigned long long q1 = __builtin_amdgcn_s_memtime();
+#endif
     if (pot) ins_class(cmask);
+#ifdef WF_STAMPS
+    const unsigned long long q2 = __builtin_amdgcn_s_memtime();
+    p2_row += q1 - q0;
+    p2_ins += q2 - q1;
+#endif
   });
+#ifdef WF_STAMPS
+  BSTAT(10, p2_row);
+  BSTAT(11, p2_ins);
+#endif
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const double r2 = __shfl_xor(br, off, 64);
