@@ -96,16 +96,19 @@ def main():
     nt = max(1, t[15])
     out["triage"] = {"decided_sampled": t[15], "cycles_per_contig": sum(t[:9]) / nt,
                      "phases": {k: t[i] / nt for i, k in enumerate(TRIAGE_PHASES)}}
-    bg = (C.c_ulonglong * 16)()
+    bg = (C.c_ulonglong * 24)()
     so.wf_stamps_read_big.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    so.wf_stamps_read_big(bg, 16)
+    so.wf_stamps_read_big(bg, 24)
     b = [int(x) for x in bg]
     nb = max(1, b[15])
     out["sp_level"] = {"sampled": b[15], "cycles_per_contig": sum(b[:10]) / nb,
                        "phases": {k: b[i] / nb for i, k in enumerate(SP_LEVEL_PHASES)},
                        "pass 2 split": {"row summaries": b[10] / nb, "class inserts": b[11] / nb},
                        "per_contig": {"segments": b[12] / nb, "potential clades": b[13] / nb,
-                                      "members": b[14] / nb}}
+                                      "members": b[14] / nb},
+                       "outcomes": {"declined: class table": b[16], "declined: class pairs": b[17],
+                                    "explain_one": b[18]},
+                       "calls_by_level": {"0": b[19], "1": b[20], "2+": b[21]}}
     print(json.dumps(out))
     for p, d in out["phases"].items():
         print("{:24s} {:10.0f} cyc  {:5.1f}%".format(p, d["cycles_per_contig"], 100 * d["frac"]),

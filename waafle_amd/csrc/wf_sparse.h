@@ -39,6 +39,7 @@ constexpr int kSpParG = 4096;    // parent hash slots (HBM scratch), >= 2 * memb
 constexpr int kSpDense = 16384;  // dense member rows (members x loci doubles, HBM scratch)
 constexpr int kSpWin = 256;      // segments staged per step
 constexpr int kSpMaxG = 63;      // loci per contig (mask bits; ~0 marks an empty class slot)
+constexpr int kSpP1 = 8;         // pass 1: 64-segment chunks per step (one round trip each)
 
 struct SpMember {                // 32 B
   int rs, cl, pi, sp;            // run start (-1: the virtual "Unknown" row), clade,
@@ -191,6 +192,54 @@ __device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, in
       const int cl = sh.wcg[w].x;
       const int prev = w == 0 ? carry : sh.wcg[w - 1].x;
       f(base + w < se && cl != prev, base + w, w, cl);
+    }
+    carry = sh.wcg[kSpWin - 1].x;
+  }
+  __syncthreads();
+}
+
+// sp_rows with one dependent global load per run start hoisted out of the run walks:
+// pre(t, cl) is evaluated for the window's four 64-segment chunks first (their loads issue
+// together), then f(is_start, t, w, cl, pre value) per chunk.  Chunks unrolled (the
+// prefetched values stay in registers).
+template <class Pre, class F>
+__device__ __forceinline__ void sp_rows_pf(const SArgs& S, SpShared& sh, int so, int se, Pre pre, F f) {
+  const int lane = threadIdx.x & 63;
+  int carry = -1;
+  int2 cg[5];
+  double v[5];
+  auto fetch = [&](int base) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const int t = base + 64 * j + lane;
+      cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
+      v[j] = t < se ? S.seg_mean[t] : 0.0;
+    }
+  };
+  if (so < se) fetch(so);
+  for (int base = so; base < se; base += kSpWin) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      sh.wcg[64 * j + lane] = cg[j];
+      sh.wv[64 * j + lane] = v[j];
+    }
+    __syncthreads();
+    if (base + kSpWin < se) fetch(base + kSpWin);
+    int pv[kSpWin / 64];
+    bool st[kSpWin / 64];
+#pragma unroll
+    for (int j = 0; j < kSpWin / 64; ++j) {
+      const int w = 64 * j + lane;
+      const int cl = sh.wcg[w].x;
+      const int prev = w == 0 ? carry : sh.wcg[w - 1].x;
+      st[j] = base + w < se && cl != prev;
+      pv[j] = pre(st[j], cl);
+    }
+#pragma unroll
+    for (int j = 0; j < kSpWin / 64; ++j) {
+      const int w = 64 * j + lane;
+      f(st[j], base + w, w, sh.wcg[w].x, pv[j]);
     }
     carry = sh.wcg[kSpWin - 1].x;
   }
@@ -401,6 +450,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   BLAP_MARK(c);
   BSTAT(15, 1);
   BSTAT(12, se - so);
+  BSTAT(19 + min(level, 2), 1);
 
   // ---- pass 1: per-locus maxes over known clades, root present (:407-411) -------------
   sh.mx[lane] = 0;
@@ -415,25 +465,25 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   __syncthreads();
   bool root = false;
   {
-    int2 cg[4];
-    double v[4];
+    int2 cg[kSpP1];
+    double v[kSpP1];
     auto fetch = [&](int base) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < kSpP1; ++j) {
         const int t = base + 64 * j + lane;
         cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
         v[j] = t < se ? S.seg_mean[t] : 0.0;
       }
     };
     if (so < se) fetch(so);
-    for (int base = so; base < se; base += 256) {
-      int2 c2[4];
-      double v2[4];
+    for (int base = so; base < se; base += 64 * kSpP1) {
+      int2 c2[kSpP1];
+      double v2[kSpP1];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { c2[j] = cg[j]; v2[j] = v[j]; }
-      if (base + 256 < se) fetch(base + 256);        // (the next step's loads in flight)
+      for (int j = 0; j < kSpP1; ++j) { c2[j] = cg[j]; v2[j] = v[j]; }
+      if (base + 64 * kSpP1 < se) fetch(base + 64 * kSpP1);   // (the next step's loads in flight)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < kSpP1; ++j) {
         root |= c2[j].x == K.root;
         if (c2[j].x >= 0 && c2[j].x != K.unknown && v2[j] > 0.0) atomicMax(&sh.mx[c2[j].y], dbits(v2[j]));
       }
@@ -492,6 +542,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
 #ifdef WF_STAMPS
     const unsigned long long q0 = __builtin_amdgcn_s_memtime();
 #endif
+    // past 3/4 of the class table the contig goes to the dense decision unless it has an
+    // explain_one option: stop inserting (a full table made every new class probe all of it)
+    const bool cls_full = sh.n_used * 4 > kSpCls * 3;
     bool pot = false;
     uint64_t cmask = 0;
     if (st && !(vu && cl == K.unknown)) {          // (a real "Unknown" run is replaced)
@@ -508,7 +561,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
 #ifdef WF_STAMPS
     const unsigned long long q1 = __builtin_amdgcn_s_memtime();
 #endif
-    if (pot) ins_class(cmask);
+    if (pot && !cls_full) ins_class(cmask);
 #ifdef WF_STAMPS
     const unsigned long long q2 = __builtin_amdgcn_s_memtime();
     p2_row += q1 - q0;
@@ -541,13 +594,14 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   }
   if (u_pot) {
     Pp += 1;
-    if (lane == 0) ins_class(u_k2 & keep);
+    if (lane == 0 && sh.n_used * 4 <= kSpCls * 3) ins_class(u_k2 & keep);
   }
   __syncthreads();
   BLAP(1);
   BSTAT(13, Pp);
 
   if (bk >= 0) {
+    BSTAT(18, 1);
     // meld_one (:621-631): options within --range of the best
     const int best = (int)bk;
     int acc = -1;
@@ -613,7 +667,10 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
 
   // ---- explain_two (:599-619) --------------------------------------------------------
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
-  if (sh.n_used * 4 > kSpCls * 3) return false;    // too many classes for the table
+  if (sh.n_used * 4 > kSpCls * 3) {                // too many classes for the table
+    BSTAT(16, 1);
+    return false;
+  }
   // passing class pairs: (ma | mb) == keep (a == b: at least 2 clades)
   int U = 0;
   for (int base = 0; base < kSpCls; base += 64) {  // the occupied slots, compacted
@@ -640,7 +697,10 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   BLAP(3);
   bool have_ok = false;
   if (sh.n_pairs > 0) {
-    if (sh.n_pairs > kSpPairs) return false;
+    if (sh.n_pairs > kSpPairs) {
+      BSTAT(17, 1);
+      return false;
+    }
     // ---- pass 3: members (potential clades of passing classes), counted per class -------
     int pbase = 0;
     sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
@@ -766,12 +826,13 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
           if (o2 & t2) atomicOr(&x->c3, (unsigned long long)(o2 & t2));
         }
       };
-      sp_rows(S, sh, so, se, [&](bool st, int, int w, int cl) {
-        if (!st || (vu && cl == K.unknown)) return;
-        const int sp = K.sibp[cl];
-        if (sp < 0) return;
-        count(sp, sp_row(sh, P, w, cl, allg).mhs);
-      });
+      // (each window's listed parents loaded at once: one round trip per window, not per chunk)
+      sp_rows_pf(S, sh, so, se,
+                 [&](bool st, int cl) { return st && !(vu && cl == K.unknown) ? K.sibp[cl] : -1; },
+                 [&](bool, int, int w, int cl, int sp) {
+                   if (sp < 0) return;
+                   count(sp, sp_row(sh, P, w, cl, allg).mhs);
+                 });
       if (vu && lane == 0) count(K.sibp[K.unknown], u_hs);
       __threadfence_block();
     }
@@ -1332,7 +1393,7 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
 // S_arg stays the first parameter: the loop body re-reads the argument block through
 // kernarg_fresh (wf_device.h) per contig -- held across the loop, its fields overflowed the
 // SGPR file (309 SGPRs spilled to VGPR lanes: a v_readlane per use, the kernel's SALU excess).
-__global__ __launch_bounds__(64) void k_big_sparse(const SArgs S_arg, int level, int64_t n_keys) {
+__global__ __launch_bounds__(64, 3) void k_big_sparse(const SArgs S_arg, int level, int64_t n_keys) {
   __shared__ SpShared sh;
   char* ws = S_arg.sp_ws + (int64_t)blockIdx.x * kSpSlot;
   const int count = (int)S_arg.counters[2];

@@ -100,24 +100,29 @@ __global__ void k_init(const KArgs K) {
 // paints sites in (orgscorer.py:359-382).  Pass 0 only counts (attachments, a leaf bound
 // and the largest contig); pass 1 writes them at the contig's offset and does the
 // annotation transfer (orgscorer.py:383-392) for the contig's loci in LDS.
-constexpr int kAttNT = 64;       // one wave per contig: many contigs in flight
+#ifndef WF_ATT_NT_FORCE64
+#define WF_ATT_NT_FORCE64 0
+#endif
+constexpr int kAttNT = 64;       // one wave per contig: many contigs in flight ...
+constexpr int kAttNTBig = 512;   // ... or 8 when the batch's contigs have thousands of hits (the
+constexpr int kAttBigHits = 2048;   // cfg5 stress shape: one wave stepped ~80 dependent chunks)
 constexpr int kAttLoc = 128;      // loci staged in LDS (more: read from HBM)
 
 struct LocView {
   int lo, len, st;
 };
 
-template <int PASS>
+template <int PASS, int NT>
 // (S_arg first: the per-contig loop re-reads the argument block through kernarg_fresh)
-__global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_t* ccnt,
+__global__ __launch_bounds__(NT) void k_att_contig(const SArgs S_arg, int64_t* ccnt,
                                                        int64_t* cleaves, unsigned long long* cmax,
                                                        const int32_t* list, int n_list) {
   __shared__ int s_lo[kAttLoc], s_len[kAttLoc], s_nl[kAttLoc];
   __shared__ int8_t s_st[kAttLoc];
   __shared__ unsigned long long s_best[kAnnSlots];
   __shared__ int s_hit[kAnnSlots];
-  __shared__ int s_scan[kAttNT / 64];
-  __shared__ long long s_red[2][kAttNT / 64];
+  __shared__ int s_scan[NT / 64];
+  __shared__ long long s_red[2][NT / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   for (int i = blockIdx.x; i < n_list; i += gridDim.x) {
     const SArgs& S = kernarg_fresh<SArgs>(S_arg);
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
     const int G = (int)(K.loc_off[c + 1] - l0);
     const bool lds_loc = G <= kAttLoc;
     if (lds_loc)
-      for (int g = tid; g < G; g += kAttNT) {
+      for (int g = tid; g < G; g += NT) {
         const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
         s_lo[g] = min(a, b);
         const int len = max(a, b) - min(a, b) + 1;
@@ -142,7 +147,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
     const int ns = K.n_sys;
     const bool lds_ann = PASS == 1 && (int64_t)G * ns <= kAnnSlots;
     if (lds_ann)
-      for (int i = tid; i < G * ns; i += kAttNT) { s_best[i] = 0ull; s_hit[i] = -1; }
+      for (int i = tid; i < G * ns; i += NT) { s_best[i] = 0ull; s_hit[i] = -1; }
     __syncthreads();
     auto locus = [&](int g) -> LocView {
       if (lds_loc) return LocView{s_lo[g], s_len[g], s_st[g]};
@@ -155,7 +160,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
     bool ordered = lds_loc && P.min_overlap > 0.0;
     if (ordered) {
       bool bad = false;
-      for (int g = 1 + tid; g < G; g += kAttNT) bad = bad || s_lo[g] <= s_lo[g - 1] + s_len[g - 1] - 1;
+      for (int g = 1 + tid; g < G; g += NT) bad = bad || s_lo[g] <= s_lo[g - 1] + s_len[g - 1] - 1;
       ordered = !__syncthreads_or(bad);
     }
     // the loci hit h attaches to, in GFF order: f(g, L) for each
@@ -178,14 +183,24 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
     };
     long long n_tot = 0, nl_tot = 0;
     int64_t base = PASS == 1 ? S.catt_off[c] : 0;
-    for (int64_t hb = h0; hb < h1; hb += kAttNT) {
+    for (int64_t hb = h0; hb < h1; hb += NT) {
       const int64_t h = hb + tid;
       int n = 0;
       long long nl = 0;
-      int qlo = 0, qhi = 0, hs = 0;
-      const bool live = h < h1 && K.scov[h] >= P.min_scov;
-      if (live) {
+      int qlo = 0, qhi = 0, hs = 0, clade = 0;
+      double sc = 0.0, scv = 0.0;
+      uint32_t m = 0u;
+      if (h < h1) {                                 // every field of the hit in one round of loads
+        scv = K.scov[h];
         qlo = K.qlo[h]; qhi = K.qhi[h]; hs = K.hstrand[h];
+        if (PASS == 1) {
+          clade = K.taxon[h];
+          sc = K.score[h];
+          m = ns > 0 ? K.sysmask[h] : 0u;
+        }
+      }
+      const bool live = h < h1 && scv >= P.min_scov;
+      if (live) {
         each_locus(qlo, qhi, hs, [&](int g, const LocView& L) {
           ++n;
           if (PASS == 0)
@@ -210,7 +225,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
       __syncthreads();
       int wbase = 0, total = 0;
 #pragma unroll
-      for (int i = 0; i < kAttNT / 64; ++i) {
+      for (int i = 0; i < NT / 64; ++i) {
         wbase += i < w ? s_scan[i] : 0;
         total += s_scan[i];
       }
@@ -218,10 +233,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
       int64_t o = base + wbase + x - n;
       base += total;
       if (n == 0) continue;
-      int clade = K.taxon[h];
       for (int j = 0; j < P.jump; ++j) clade = K.parent[clade];   // orgscorer.py:955-957
-      const double sc = K.score[h];
-      const uint32_t m = ns > 0 ? K.sysmask[h] : 0u;
       const bool ann = m != 0 && sc >= P.annot_ref;
       each_locus(qlo, qhi, hs, [&](int g, const LocView& L) {
         const int h1s = max(0, qlo - L.lo);
@@ -256,7 +268,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
       __syncthreads();
       if (tid == 0) {
         long long ta = 0, tb = 0;
-        for (int i = 0; i < kAttNT / 64; ++i) { ta += s_red[0][i]; tb += s_red[1][i]; }
+        for (int i = 0; i < NT / 64; ++i) { ta += s_red[0][i]; tb += s_red[1][i]; }
         ccnt[c] = ta;
         cleaves[c] = tb;
       }
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
       // system); every attachment of this contig is in [catt_off[c], base)
       __syncthreads();
       const int64_t a0 = S.catt_off[c];
-      for (int64_t a = a0 + tid; a < base; a += kAttNT) {
+      for (int64_t a = a0 + tid; a < base; a += NT) {
         const int h = S.att_hit[a];
         const uint32_t m = K.sysmask[h];
         const double sc = S.att_sc[a];
@@ -285,7 +297,7 @@ __global__ __launch_bounds__(kAttNT) void k_att_contig(const SArgs S_arg, int64_
       }
       __syncthreads();
       if (lds_ann)
-        for (int i = tid; i < G * ns; i += kAttNT) K.annot[l0 * ns + i] = s_hit[i];
+        for (int i = tid; i < G * ns; i += NT) K.annot[l0 * ns + i] = s_hit[i];
     }
     __syncthreads();
   }
@@ -1440,7 +1452,7 @@ __device__ unsigned long long g_sstamps[16];
   } while (0)
 #define SSTAT(i, v) do { if (ssamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_sstamps[i], (unsigned long long)(v)); } while (0)
 // ... and of sp_level (k_big_sparse, k_dump_sparse<0>) on every 8th contig
-__device__ unsigned long long g_bstamps[16];
+__device__ unsigned long long g_bstamps[24];
 #define BLAP_MARK(c) unsigned long long blap_ = __builtin_amdgcn_s_memtime(); const bool bsamp_ = ((c) & 7) == 0
 #define BLAP(i)                                                                     \
   do {                                                                              \
@@ -1464,12 +1476,12 @@ extern "C" int wf_stamps_read_sparse(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
 }
 extern "C" int wf_stamps_reset_sparse(void) {
-  unsigned long long z[16] = {0};
+  unsigned long long z[24] = {0};
   if (hipMemcpyToSymbol(HIP_SYMBOL(g_bstamps), z, sizeof z) != hipSuccess) return -2;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_sstamps), z, sizeof z) == hipSuccess ? 0 : -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sstamps), z, 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
 }
 extern "C" int wf_stamps_read_big(unsigned long long* out, int n) {
-  if (n > 16) n = 16;
+  if (n > 24) n = 24;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
 }
 #endif
@@ -2094,7 +2106,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
                        st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
 #endif
   } else {
-    hipLaunchKernelGGL(k_att_contig<0>, dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
+    hipLaunchKernelGGL((k_att_contig<0, kAttNT>), dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
                        st->cnt_leaves.as<int64_t>(),
                        reinterpret_cast<unsigned long long*>(st->red.as<int64_t>() + 1), nullptr, N);
   }
@@ -2241,8 +2253,12 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     ST_TRY(hipMemsetAsync(st->annot_best.p, 0, (size_t)n_annot * 8, s));
     ST_TRY(hipMemsetAsync(k.annot, 0xFF, (size_t)n_annot * 4, s));     // -1: no winner
   }
-  hipLaunchKernelGGL(k_att_contig<1>, dim3(std::min<unsigned>(agrid, (unsigned)n_first)), dim3(kAttNT), 0, s, sa,
-                     nullptr, nullptr, nullptr, level0 ? st->act0.as<int32_t>() : nullptr, n_first);
+  if (max_hits >= kAttBigHits && !WF_ATT_NT_FORCE64)
+    hipLaunchKernelGGL((k_att_contig<1, kAttNTBig>), dim3(std::min<unsigned>(agrid, (unsigned)n_first)), dim3(kAttNTBig), 0,
+                       s, sa, nullptr, nullptr, nullptr, level0 ? st->act0.as<int32_t>() : nullptr, n_first);
+  else
+    hipLaunchKernelGGL((k_att_contig<1, kAttNT>), dim3(std::min<unsigned>(agrid, (unsigned)n_first)), dim3(kAttNT), 0, s,
+                       sa, nullptr, nullptr, nullptr, level0 ? st->act0.as<int32_t>() : nullptr, n_first);
   ST_TRY(hipGetLastError());
   t_span(st, WF_PHASE_ATTACH, t_attach, t_mark(st, s));
 
