@@ -63,6 +63,7 @@ constexpr int64_t kSpOffDense = kSpOffPar + (int64_t)kSpParG * sizeof(SpParent);
 constexpr int64_t kSpSlot = kSpOffDense + (int64_t)kSpDense * sizeof(double);
 
 struct SpShared {
+  // (wcg and wv are contiguous: after pass 4 they hold the members' dense rows, kSpLdsRows)
   int2 wcg[kSpWin + 64];                     // staged segments: (clade, locus) ...
   double wv[kSpWin + 64];                    // ... and gene score
   unsigned long long mx[64];                 // per-locus max score bits (known clades)
@@ -86,6 +87,9 @@ struct SpShared {
   unsigned bm1[kSpMemG / 32], bm2[kSpMemG / 32];   // members melded as clade 1 / 2
   int n_used, n_pairs, n_in, all_ok, all_same, cnt, over;
 };
+
+constexpr int kSpLdsRows = 2 * (kSpWin + 64);      // doubles over wcg + wv
+static_assert(offsetof(SpShared, wv) == sizeof(int2) * (kSpWin + 64), "wcg, wv contiguous");
 
 __device__ __forceinline__ int sp_hash(uint64_t m, int cap) {
   return (int)((m * 0x9E3779B97F4A7C15ull) >> 40) & (cap - 1);
@@ -125,15 +129,24 @@ struct SpRow {
   uint64_t mk1, mk2, mhs;
 };
 
+// (w is a run start, so wcg[w].x == cl; the next entry's load issues with this one's, so a
+// one-segment run -- most of them -- costs one LDS round trip; runs end before the window's
+// last entry: <= 63 segments from a start below kSpWin)
 __device__ __forceinline__ SpRow sp_row(const SpShared& sh, const DevParams& P, int w, int cl, uint64_t allg) {
   uint64_t cov = 0, k1 = 0, k2 = 0, hs = 0;
-  for (; sh.wcg[w].x == cl; ++w) {
-    const double v = sh.wv[w];
-    const uint64_t bit = 1ull << sh.wcg[w].y;
+  int2 cg = sh.wcg[w], nx = sh.wcg[w + 1];
+  double v = sh.wv[w];
+  for (;;) {
+    const uint64_t bit = 1ull << cg.y;
     cov |= bit;
     if (v >= P.k1) k1 |= bit;
     if (v >= P.k2) k2 |= bit;
     if (v >= P.sister_thr) hs |= bit;
+    if (nx.x != cl) break;
+    ++w;
+    cg = nx;
+    v = sh.wv[w];
+    nx = sh.wcg[w + 1];
   }
   const uint64_t z = allg & ~cov;
   SpRow r;
@@ -791,8 +804,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
           }
         }
       }
+    const double* rows = dense ? drows : nullptr;     // (after pass 4: an LDS copy when it fits)
     auto acc = [&](int q, const SpMember& m) -> SpRowAcc {
-      return SpRowAcc{dense ? drows + (int64_t)q * G : nullptr, SpCursor{m.rs, m.cl, se, m.rs < 0 ? sh.urow : nullptr}};
+      return SpRowAcc{rows ? rows + (int64_t)q * G : nullptr, SpCursor{m.rs, m.cl, se, m.rs < 0 ? sh.urow : nullptr}};
     };
     __threadfence_block();
     __syncthreads();
@@ -837,6 +851,14 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       __threadfence_block();
     }
     __syncthreads();
+    // the segment window is done with: the members' dense rows move into it when they fit, so
+    // the pair evaluations below read LDS instead of each taking dependent HBM round trips
+    if (dense && M * G <= kSpLdsRows) {
+      double* lrows = reinterpret_cast<double*>(sh.wcg);
+      for (int i = lane; i < M * G; i += 64) lrows[i] = drows[i];
+      __syncthreads();
+      rows = lrows;
+    }
     BLAP(6);
 
     // ---- pass 1 over the candidates: best by (rank, pair index) ------------------------
@@ -1449,6 +1471,65 @@ __global__ __launch_bounds__(64, KIND ? 4 : 2) void k_dump_sparse(const SArgs S_
   char* ws = KIND ? nullptr : S0.sp_ws + (int64_t)blockIdx.x * kSpSlot;
   const int count = (int)(*S0.dump_ctr >> 40);
   const int stride = (int)gridDim.x;
+  // a decided contig's pend / counts, a raised one onto the next level's list, a declined one
+  // back to the staged kernels
+  auto finish = [&](const SArgs& S, int c, bool ok) {
+    if (lane == 0) {
+      const int pd = S.seed_pend[c];
+      if (!ok) {
+        S.seed_pend[c] = 1;
+        if (S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);
+      } else if (pd == 3) {
+        S.seed_pend[c] = 0;
+        ccnt[c] = 0;
+        cleaves[c] = 0;
+      } else if (pd == 2 && S.roll_next) {
+        S.roll_next[atomicAdd(S.roll_next_n, 1ull)] = c;
+      }
+    }
+    __syncthreads();
+  };
+  if constexpr (KIND == 1) {
+    if (S0.wq) {
+      // work queue (the roll-up levels' ~20 k slots over ~4 k waves): a wave claims its next
+      // slot and loads that slot's header while it decides the current one
+      struct Hdr { int mc, so, se, G; uint64_t hdr; int64_t h0, l0; };
+      auto claim = [&]() {
+        unsigned long long q = 0;
+        if (lane == 0) q = atomicAdd(S0.wq, 1ull);
+        return __builtin_amdgcn_readfirstlane((int)q);
+      };
+      auto load = [&](int my) {
+        Hdr x{-1, 0, 0, 0, 0ull, 0, 0};
+        if (my < count) {
+          const int2 dl = reinterpret_cast<const int2*>(S0.dump_list)[my];
+          if (dl.x == 1 && dl.y >= 0) {
+            x.mc = dl.y;
+            x.so = S0.dump_first[my];
+            x.se = S0.dump_first[my + 1];
+            x.hdr = S0.dump_um[my];
+            x.h0 = S0.k.hit_off[x.mc];
+            x.l0 = S0.k.loc_off[x.mc];
+            x.G = (int)(S0.k.loc_off[x.mc + 1] - x.l0);
+          }
+        }
+        return x;
+      };
+      int my = claim();
+      Hdr cur = load(my);
+      while (my < count) {
+        const int nx = claim();
+        const Hdr nh = load(nx);
+        if (cur.mc >= 0) {
+          const SArgs& S = kernarg_fresh<SArgs>(S_arg);
+          finish(S, cur.mc, sp_two(S, sh, cur.mc, cur.so, cur.se, cur.hdr, cur.h0, cur.l0, cur.G, level));
+        }
+        my = nx;
+        cur = nh;
+      }
+      return;
+    }
+  }
   for (int base = blockIdx.x; base < count; base += 64 * stride) {
     const int my = base + lane * stride;
     int mc = -1, so = 0, se = 0, G = 0;
@@ -1480,20 +1561,7 @@ __global__ __launch_bounds__(64, KIND ? 4 : 2) void k_dump_sparse(const SArgs S_
       } else {
         ok = sp_level(S, sh, ws, c, base + src * stride, level, 1);
       }
-      if (lane == 0) {
-        const int pd = S.seed_pend[c];
-        if (!ok) {
-          S.seed_pend[c] = 1;
-          if (S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);
-        } else if (pd == 3) {
-          S.seed_pend[c] = 0;
-          ccnt[c] = 0;
-          cleaves[c] = 0;
-        } else if (pd == 2 && S.roll_next) {
-          S.roll_next[atomicAdd(S.roll_next_n, 1ull)] = c;
-        }
-      }
-      __syncthreads();
+      finish(S, c, ok);
     }
   }
 }

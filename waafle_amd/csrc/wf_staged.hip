@@ -441,9 +441,22 @@ __global__ __launch_bounds__(kRadixNT) void k_sort_radix(const SArgs S, int n_ac
       if (tid == 0) S.seg_cnt[cr] = 0;
       continue;
     }
-    for (int i = tid; i < n; i += kRadixNT) {
-      kb(0)[i] = (uint32_t)make_key(S, 0, (int)(a0 + i));
-      ib(0)[i] = (uint16_t)i;
+    // (the attachments' clade and locus loads of four strides issued together)
+    for (int i0 = 0; i0 < n; i0 += 4 * kRadixNT) {
+      uint32_t kk[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + r * kRadixNT + tid;
+        kk[r] = i < n ? (uint32_t)make_key(S, 0, (int)(a0 + i)) : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + r * kRadixNT + tid;
+        if (i < n) {
+          kb(0)[i] = kk[r];
+          ib(0)[i] = (uint16_t)i;
+        }
+      }
     }
     // wave w's slice [lo, hi) of the elements
     const int per = (n + kW - 1) / kW;
@@ -618,44 +631,64 @@ __global__ __launch_bounds__(kRadixNT) void k_seg_build_wide(const SArgs S, int 
       s_glen[tid] = max(a, b) - min(a, b) + 1;
     }
     __syncthreads();
-    for (int t0 = 0; t0 < n; t0 += kRadixNT) {
-      const int t = t0 + tid;
-      const bool live = t < n;
-      uint64_t key = 0, prev = 0;
-      if (live) {
-        key = S.keys[base + t];
-        prev = t > 0 ? S.keys[base + t - 1] : ~key;
-        const int a = S.vals[base + t];
-        S.satt_lohi[base + t] = make_int2(S.att_lo[a], S.att_hi[a]);
-        S.satt_sc[base + t] = S.att_sc[a];
-      }
-      const bool head = live && key != prev;
-      const uint64_t hm = __ballot(head);
-      if (lane == 0) s_cnt[w] = __popcll(hm);
-      __syncthreads();
-      int before = 0, total = 0;
+    // kSbR chunks of kRadixNT keys per step: their key, index and attachment loads issued
+    // together (one dependent gather round per step, not per chunk)
+    constexpr int kSbR = 4;
+    for (int t00 = 0; t00 < n; t00 += kSbR * kRadixNT) {
+      uint64_t key[kSbR], prev[kSbR];
+      int av[kSbR];
 #pragma unroll
-      for (int x = 0; x < kW; ++x) {
-        before += x < w ? s_cnt[x] : 0;
-        total += s_cnt[x];
-      }
-      if (head) {
-        const int g = (int)(key & lmask);
-        int len;
-        if (G <= 64) {
-          len = s_glen[g];
-        } else {
-          const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
-          len = max(a, b) - min(a, b) + 1;
+      for (int r = 0; r < kSbR; ++r) {
+        const int t = t00 + r * kRadixNT + tid;
+        key[r] = 0; prev[r] = 0; av[r] = 0;
+        if (t < n) {
+          key[r] = S.keys[base + t];
+          prev[r] = t > 0 ? S.keys[base + t - 1] : ~key[r];
+          av[r] = S.vals[base + t];
         }
-        const int seg = sbase + before + __popcll(hm & ((1ull << lane) - 1ull));
-        S.seg_start[seg] = (int)(base + t);
-        S.seg_crank[seg] = cr;
-        S.seg_cg[seg] = make_int2((int)((key >> S.key_lb) & tmask), g);
-        S.seg_len[seg] = len;
       }
-      sbase += total;
-      __syncthreads();                               // (s_cnt reused by the next chunk)
+#pragma unroll
+      for (int r = 0; r < kSbR; ++r) {
+        const int t = t00 + r * kRadixNT + tid;
+        if (t < n) {
+          const int a = av[r];
+          S.satt_lohi[base + t] = make_int2(S.att_lo[a], S.att_hi[a]);
+          S.satt_sc[base + t] = S.att_sc[a];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kSbR; ++r) {
+        const int t0 = t00 + r * kRadixNT;
+        if (t0 >= n) break;                            // (uniform)
+        const int t = t0 + tid;
+        const bool head = t < n && key[r] != prev[r];
+        const uint64_t hm = __ballot(head);
+        if (lane == 0) s_cnt[w] = __popcll(hm);
+        __syncthreads();
+        int before = 0, total = 0;
+#pragma unroll
+        for (int x = 0; x < kW; ++x) {
+          before += x < w ? s_cnt[x] : 0;
+          total += s_cnt[x];
+        }
+        if (head) {
+          const int g = (int)(key[r] & lmask);
+          int len;
+          if (G <= 64) {
+            len = s_glen[g];
+          } else {
+            const int a = K.lstart[l0 + g], b = K.lend[l0 + g];
+            len = max(a, b) - min(a, b) + 1;
+          }
+          const int seg = sbase + before + __popcll(hm & ((1ull << lane) - 1ull));
+          S.seg_start[seg] = (int)(base + t);
+          S.seg_crank[seg] = cr;
+          S.seg_cg[seg] = make_int2((int)((key[r] >> S.key_lb) & tmask), g);
+          S.seg_len[seg] = len;
+        }
+        sbase += total;
+        __syncthreads();                             // (s_cnt reused by the next chunk)
+      }
     }
   }
 }
@@ -1529,6 +1562,10 @@ struct Buf {
 #ifndef WF_L0_QUEUE
 #define WF_L0_QUEUE 1
 #endif
+// ... and the roll-up levels' compact explain_two (k_dump_sparse<1>)
+#ifndef WF_DUMP_QUEUE
+#define WF_DUMP_QUEUE 1
+#endif
 // levels whose largest contig has 4,097..8,192 attachments: the per-contig LDS radix sort
 // (k_sort_radix, 1) or the device radix sort of the whole level (0)
 #ifndef WF_RADIX_LDS
@@ -2003,9 +2040,10 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         da.fail_ctr = rcnt + kMaxIter + 2;
       }
     }
-    if (WF_WAVE_QUEUE && (levels || st->triage)) {   // work queues: [0] the level-0 list, [L] level L
-      ST_TRY(st->wq.ensure(s, (kMaxIter + 2) * sizeof(unsigned long long)));
-      ST_TRY(hipMemsetAsync(st->wq.p, 0, (kMaxIter + 2) * sizeof(unsigned long long), s));
+    if (WF_WAVE_QUEUE && (levels || st->triage)) {
+      // work queues: [0] the level-0 list, [L] level L's launch, [kMaxIter + 2 + L] its sp_two
+      ST_TRY(st->wq.ensure(s, 2 * (kMaxIter + 2) * sizeof(unsigned long long)));
+      ST_TRY(hipMemsetAsync(st->wq.p, 0, 2 * (kMaxIter + 2) * sizeof(unsigned long long), s));
     }
     if (st->triage) {
       // the triage (wf_triage.hip) decides the contigs explain_one settles from their full
@@ -2071,9 +2109,10 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
             la.wq = WF_WAVE_QUEUE ? st->wq.as<unsigned long long>() + L : nullptr;
             ST_TRY(launch_level(la, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                                 roll[L & 1], reinterpret_cast<const int64_t*>(rcnt + L), L, max_hits, st->cus, s));
-            la.wq = nullptr;
+            la.wq = WF_WAVE_QUEUE && WF_DUMP_QUEUE ? st->wq.as<unsigned long long>() + kMaxIter + 2 + L : nullptr;
             hipLaunchKernelGGL(k_dump_sparse<1>, dim3(grid2), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
                                st->cnt_leaves.as<int64_t>(), L);
+            la.wq = nullptr;
             hipLaunchKernelGGL(k_dump_sparse<0>, dim3(grid), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
                                st->cnt_leaves.as<int64_t>(), L);
             ST_TRY(hipGetLastError());

@@ -64,6 +64,7 @@ constexpr int kTrSpan = 26;            // loci one hit may attach to, from its f
 constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
 constexpr int kTrXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
 constexpr int kTrBig = 512;            // more hits than any wave slice: k_count
+constexpr int kCntR = 4;               // k_count: hit batches per round of loads
 
 struct TriSmem {
   int lo[kTrLoc], hi[kTrLoc];          // locus site ranges (min, max of start/end)
@@ -462,22 +463,32 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
     if (lane < G) { s_lo[lane] = clo; s_hi[lane] = chi; s_st[lane] = (int8_t)cst; }
     wave_sync();
     long long n_att = 0, nl = 0;
-    for (int64_t hb = h0; hb < h1; hb += 64) {
-      const int64_t h = hb + lane;
-      if (h >= h1 || !(K.scov[h] >= P.min_scov)) continue;
-      const int qlo = K.qlo[h], qhi = K.qhi[h], hs = K.hstrand[h];
-      int g = 0;
+    for (int64_t hb = h0; hb < h1; hb += 64 * kCntR) {   // kCntR batches' loads issued together
+      double r_scv[kCntR];
+      int r_qlo[kCntR], r_qhi[kCntR], r_hs[kCntR];
 #pragma unroll
-      for (int k = 32; k > 0; k >>= 1)
-        if (g + k <= G && s_hi[g + k - 1] < qlo) g += k;
-      for (; g < G; ++g) {
-        const int lo = s_lo[g];
-        if (lo > qhi) break;
-        const int len = s_hi[g] - lo + 1;
-        if (attaches(P, qlo, qhi, hs, lo, len, s_st[g])) {
-          ++n_att;
-          nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
-                (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+      for (int r = 0; r < kCntR; ++r) {
+        const int64_t h = hb + 64 * r + lane;
+        r_scv[r] = -1.0; r_qlo[r] = 0; r_qhi[r] = 0; r_hs[r] = 0;
+        if (h < h1) { r_scv[r] = K.scov[h]; r_qlo[r] = K.qlo[h]; r_qhi[r] = K.qhi[h]; r_hs[r] = K.hstrand[h]; }
+      }
+#pragma unroll
+      for (int r = 0; r < kCntR; ++r) {
+        if (hb + 64 * r + lane >= h1 || !(r_scv[r] >= P.min_scov)) continue;
+        const int qlo = r_qlo[r], qhi = r_qhi[r], hs = r_hs[r];
+        int g = 0;
+#pragma unroll
+        for (int k = 32; k > 0; k >>= 1)
+          if (g + k <= G && s_hi[g + k - 1] < qlo) g += k;
+        for (; g < G; ++g) {
+          const int lo = s_lo[g];
+          if (lo > qhi) break;
+          const int len = s_hi[g] - lo + 1;
+          if (attaches(P, qlo, qhi, hs, lo, len, s_st[g])) {
+            ++n_att;
+            nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+                  (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+          }
         }
       }
     }
