@@ -85,6 +85,8 @@ def parse_args():
     ap.add_argument("--traffic-json", default=None)
     ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r05", "cfg4_valu.json"),
                     help="PMC VALU counts of the main pass (scripts/pmc_main.py, optional)")
+    ap.add_argument("--k2-traffic-json", default=os.path.join(PROFILES, "r05", "traffic_cfg5.json"),
+                    help="FETCH/WRITE of the k2 leg's kernels (scripts/pmc_k2_r5.sh)")
     ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r05", "k2_pmc.json"),
                     help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
     return ap.parse_args()
@@ -311,7 +313,7 @@ def timed_passes(so, h, chk, db, params, steps, warmup, dist, dev, cdev=None):
     return wdist.max_over_ranks(t1 - t0, dist, cdev), tm
 
 
-def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=None):
+def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=None, traffic_json=None):
     """The explain_two stress leg (BASELINE configs[4]) on this rank's cfg5 share."""
     import torch
     db = DeviceBatch(kbatch, dev)
@@ -370,6 +372,34 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
             out["valu"] = {"insts_per_pass": insts, "achieved_insts_per_s": insts / (k2_max),
                            "peak_insts_per_s": peak, "frac": insts / k2_max / peak,
                            "source": pj.get("source")}
+            bs = {k: v for k, v in pj.get("per_kernel", {}).items() if k.startswith("k_big_sparse")}
+            if bs:
+                b = next(iter(bs.values()))
+                out["valu"]["k_big_sparse"] = {"valu_insts_per_pass": b.get("SQ_INSTS_VALU"),
+                                               "salu_insts_per_pass": b.get("SQ_INSTS_SALU"),
+                                               "lds_insts_per_pass": b.get("SQ_INSTS_LDS")}
+        else:
+            out["valu"] = {"skipped": "k2 PMC file of another library build or shape"}
+    # what the explain_two kernel actually moved (FETCH_SIZE / WRITE_SIZE of k_big_sparse, PMC
+    # runs of this library build): b_k2_actual beside the notional B_k2
+    if traffic_json and os.path.exists(traffic_json):
+        with open(traffic_json) as fh:
+            tj = json.load(fh)
+        from waafle_amd import lib as L
+        if tj.get("contigs") == kbatch.n_contigs and tj.get("lib_sha") == file_sha(L.LIB_PATH):
+            kb = tj.get("per_kernel_kb", {}).get("k_big_sparse", {})
+            f, w = kb.get("FETCH_SIZE", 0.0) * 1024.0, kb.get("WRITE_SIZE", 0.0) * 1024.0
+            big_ms = per("big")
+            out["b_k2_actual"] = {
+                "kernel": "k_big_sparse", "fetch_bytes_raw": f, "fetch_bytes_x2": 2.0 * f, "write_bytes": w,
+                "bytes_per_pass": f + w, "achieved_GBs": (f + w) / max(big_ms * 1e-3, 1e-12) / 1e9,
+                "frac": (f + w) / max(big_ms * 1e-3, 1e-12) / 1e9 / HBM_PEAK_GBS,
+                "rule": "k_big_sparse FETCH_SIZE (raw) + WRITE_SIZE per pass (rocprofv3 --pmc, separate "
+                        "runs, this build) / this run's 'big' phase time (k_big_sparse and the dense "
+                        "decisions it declines)",
+                "source": tj.get("source")}
+        else:
+            out["b_k2_actual"] = {"skipped": "traffic file of another library build or shape"}
     return out
 
 
@@ -609,7 +639,7 @@ def main():
             tk = engine.taxonomy_struct(ktax)
             chk(so.wf_set_taxonomy(h, C.byref(tk)))
         result["k2"] = k2_leg(so, h, chk, kbatch, k2_params, args.k2_steps, dist, dev, world,
-                              args.k2_pmc_json, cdev)
+                              args.k2_pmc_json, cdev, args.k2_traffic_json)
         result["k2_pair_evals_per_sec"] = result["k2"]["k2_pair_evals_per_sec"]
     if rank == 0 and world == 1 and args.pcie:
         # scope (ii): host (pageable numpy) arrays in, host results out, second call timed

@@ -129,24 +129,15 @@ struct SpRow {
   uint64_t mk1, mk2, mhs;
 };
 
-// (w is a run start, so wcg[w].x == cl; the next entry's load issues with this one's, so a
-// one-segment run -- most of them -- costs one LDS round trip; runs end before the window's
-// last entry: <= 63 segments from a start below kSpWin)
 __device__ __forceinline__ SpRow sp_row(const SpShared& sh, const DevParams& P, int w, int cl, uint64_t allg) {
   uint64_t cov = 0, k1 = 0, k2 = 0, hs = 0;
-  int2 cg = sh.wcg[w], nx = sh.wcg[w + 1];
-  double v = sh.wv[w];
-  for (;;) {
-    const uint64_t bit = 1ull << cg.y;
+  for (; sh.wcg[w].x == cl; ++w) {
+    const double v = sh.wv[w];
+    const uint64_t bit = 1ull << sh.wcg[w].y;
     cov |= bit;
     if (v >= P.k1) k1 |= bit;
     if (v >= P.k2) k2 |= bit;
     if (v >= P.sister_thr) hs |= bit;
-    if (nx.x != cl) break;
-    ++w;
-    cg = nx;
-    v = sh.wv[w];
-    nx = sh.wcg[w + 1];
   }
   const uint64_t z = allg & ~cov;
   SpRow r;
@@ -1489,47 +1480,6 @@ __global__ __launch_bounds__(64, KIND ? 4 : 2) void k_dump_sparse(const SArgs S_
     }
     __syncthreads();
   };
-  if constexpr (KIND == 1) {
-    if (S0.wq) {
-      // work queue (the roll-up levels' ~20 k slots over ~4 k waves): a wave claims its next
-      // slot and loads that slot's header while it decides the current one
-      struct Hdr { int mc, so, se, G; uint64_t hdr; int64_t h0, l0; };
-      auto claim = [&]() {
-        unsigned long long q = 0;
-        if (lane == 0) q = atomicAdd(S0.wq, 1ull);
-        return __builtin_amdgcn_readfirstlane((int)q);
-      };
-      auto load = [&](int my) {
-        Hdr x{-1, 0, 0, 0, 0ull, 0, 0};
-        if (my < count) {
-          const int2 dl = reinterpret_cast<const int2*>(S0.dump_list)[my];
-          if (dl.x == 1 && dl.y >= 0) {
-            x.mc = dl.y;
-            x.so = S0.dump_first[my];
-            x.se = S0.dump_first[my + 1];
-            x.hdr = S0.dump_um[my];
-            x.h0 = S0.k.hit_off[x.mc];
-            x.l0 = S0.k.loc_off[x.mc];
-            x.G = (int)(S0.k.loc_off[x.mc + 1] - x.l0);
-          }
-        }
-        return x;
-      };
-      int my = claim();
-      Hdr cur = load(my);
-      while (my < count) {
-        const int nx = claim();
-        const Hdr nh = load(nx);
-        if (cur.mc >= 0) {
-          const SArgs& S = kernarg_fresh<SArgs>(S_arg);
-          finish(S, cur.mc, sp_two(S, sh, cur.mc, cur.so, cur.se, cur.hdr, cur.h0, cur.l0, cur.G, level));
-        }
-        my = nx;
-        cur = nh;
-      }
-      return;
-    }
-  }
   for (int base = blockIdx.x; base < count; base += 64 * stride) {
     const int my = base + lane * stride;
     int mc = -1, so = 0, se = 0, G = 0;

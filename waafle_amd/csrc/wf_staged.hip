@@ -1562,10 +1562,6 @@ struct Buf {
 #ifndef WF_L0_QUEUE
 #define WF_L0_QUEUE 1
 #endif
-// ... and the roll-up levels' compact explain_two (k_dump_sparse<1>)
-#ifndef WF_DUMP_QUEUE
-#define WF_DUMP_QUEUE 1
-#endif
 // levels whose largest contig has 4,097..8,192 attachments: the per-contig LDS radix sort
 // (k_sort_radix, 1) or the device radix sort of the whole level (0)
 #ifndef WF_RADIX_LDS
@@ -2041,9 +2037,9 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       }
     }
     if (WF_WAVE_QUEUE && (levels || st->triage)) {
-      // work queues: [0] the level-0 list, [L] level L's launch, [kMaxIter + 2 + L] its sp_two
-      ST_TRY(st->wq.ensure(s, 2 * (kMaxIter + 2) * sizeof(unsigned long long)));
-      ST_TRY(hipMemsetAsync(st->wq.p, 0, 2 * (kMaxIter + 2) * sizeof(unsigned long long), s));
+      // work queues: [0] the level-0 list, [L] level L's launch
+      ST_TRY(st->wq.ensure(s, (kMaxIter + 2) * sizeof(unsigned long long)));
+      ST_TRY(hipMemsetAsync(st->wq.p, 0, (kMaxIter + 2) * sizeof(unsigned long long), s));
     }
     if (st->triage) {
       // the triage (wf_triage.hip) decides the contigs explain_one settles from their full
@@ -2109,10 +2105,9 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
             la.wq = WF_WAVE_QUEUE ? st->wq.as<unsigned long long>() + L : nullptr;
             ST_TRY(launch_level(la, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                                 roll[L & 1], reinterpret_cast<const int64_t*>(rcnt + L), L, max_hits, st->cus, s));
-            la.wq = WF_WAVE_QUEUE && WF_DUMP_QUEUE ? st->wq.as<unsigned long long>() + kMaxIter + 2 + L : nullptr;
+            la.wq = nullptr;                             // (a queue for sp_two: r5t, 0.35 ms slower)
             hipLaunchKernelGGL(k_dump_sparse<1>, dim3(grid2), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
                                st->cnt_leaves.as<int64_t>(), L);
-            la.wq = nullptr;
             hipLaunchKernelGGL(k_dump_sparse<0>, dim3(grid), dim3(64), 0, s, la, st->cnt.as<int64_t>(),
                                st->cnt_leaves.as<int64_t>(), L);
             ST_TRY(hipGetLastError());
