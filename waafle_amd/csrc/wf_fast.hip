@@ -47,6 +47,11 @@
 // resident waves per SIMD of the roll-up launches: 4 (128 VGPRs, some spilled) beat 3 (168,
 // none) by 0.35 ms of roll-up per cfg4 pass on one box (r4f: their few contigs per wave
 // want occupancy more than registers)
+// hand-over: only candidate-pair members' rows evaluated whole (1), or every potential
+// clade's (0)
+#ifndef WF_E2_MEMBERS
+#define WF_E2_MEMBERS 1
+#endif
 #ifndef WF_ROLL_WAVES
 #define WF_ROLL_WAVES 4
 #endif
@@ -1270,7 +1275,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
                 in = v[t] < 0.0 && best_score(t) >= bound2;
               } else if (pass == 5) {
                 if (v[t] < 0.0) {
-                  in = rc[t] != 0;                     // a potential clade's row
+                  in = rc[t] == 1;                     // a (member) potential clade's row
                   if (!in && P.sister_on && best_score(t) >= bound_s) {
                     const int sp = K.sibp[cg.x];
                     for (int i = 0; i < npp && !in; ++i) in = pp[i] == sp;
@@ -1433,18 +1438,60 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
               for (int q = t; q < t + cnt; ++q) rc[q] = pot ? 1 : 0;
             }
           wave_sync();
+          if (!FULL && WF_E2_MEMBERS) {
+            // Hand-over: only potential clades that form a candidate pair (crit >= k2 <=>
+            // (m_i | m_j) == um, m = loci >= k2: exact here, every segment that can reach k2
+            // was evaluated by pass 4) have their rows read by explain_two's ranks and LGT
+            // checks; the others (rc 2) keep what pass 4 evaluated -- enough to find them
+            // potential and to build their masks -- and count as sisters through pass 5's
+            // sister candidates like any other clade.  Lane i: potential clade i's run start
+            // and mask (<= 64 of them, else pass 6 below).
+            int ph = -1;
+            uint64_t pm = 0;
+            int np0 = 0;
+            for (int t0 = 0; t0 < ns; t0 += 64) {
+              const int t = t0 + lane;
+              const bool in = t < ns && rc[t] && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
+              const uint64_t im = __ballot(in);
+              uint64_t m = 0;
+              if (in)
+                for (int q = t; q < ns && cg_of(F, q).x == cg_of(F, t).x; ++q)
+                  if (v[q] >= P.k2) m |= 1ull << cg_of(F, q).y;
+              m &= um;
+              for (uint64_t r = im; r; r &= r - 1) {     // potential clade np0 + k -> lane np0 + k
+                const int src = __builtin_ctzll(r);
+                const int dst = np0 + __popcll(im & ((1ull << src) - 1ull));
+                const int hsrc = lane_bcast(t, src);
+                const uint64_t msrc = lane_bcast(m, src);
+                if (lane == dst && dst < 64) { ph = hsrc; pm = msrc; }
+              }
+              np0 += __popcll(im);
+            }
+            if (np0 <= 64) {
+              bool member = false;
+              for (int j = 0; j < np0; ++j) {
+                const uint64_t mj = lane_bcast(pm, j);
+                member = member || (lane < np0 && lane != j && (pm | mj) == um);
+              }
+              if (lane < np0 && !member)
+                for (int q = ph; q < ns && cg_of(F, q).x == cg_of(F, ph).x; ++q) rc[q] = 2;
+              wave_sync();
+            }
+          }
           npp = 0;                                     // their parents (sister checks, :717-744)
           int npot = 0;
           for (int t0 = 0; t0 < ns; t0 += 64) {
             const int t = t0 + lane;
             const bool in = t < ns && rc[t] && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
             const uint64_t im = __ballot(in);
+            const bool mem_in = in && rc[t] == 1;        // (the parents of candidate-pair members)
+            const uint64_t mm = __ballot(mem_in);
             // the sisters of X are the clades listed under parent(X) (get_sisters, utils.py:428-434):
             // pass 5 evaluates clades whose listed parent is one of these.  (Not sibp(X): an
             // unlisted X has sibp -1 but parent r__Root, whose listed children are its sisters.)
-            if (in && npp + __popcll(im & lanes_below()) < 64)
-              pp[npp + __popcll(im & lanes_below())] = K.parent[cg_of(F, t).x];
-            npp = min(npp + __popcll(im), 64);
+            if (mem_in && npp + __popcll(mm & lanes_below()) < 64)
+              pp[npp + __popcll(mm & lanes_below())] = K.parent[cg_of(F, t).x];
+            npp = min(npp + __popcll(mm), 64);
             npot += __popcll(im);
           }
           wave_sync();
@@ -1633,7 +1680,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         bool compact = !FULL && compact_ok && S.wave_two && G <= kE2MaxG && P.weak != 2;
         int n_out = ns;
         bool rootp = false;
-        auto want = [&](int t) { return rc[t] != 0 || (P.sister_on && v[t] >= P.sister_thr); };
+        // (rc 2: a potential clade in no candidate pair -- its evaluated segments only)
+        auto want = [&](int t) {
+          return rc[t] == 1 || (rc[t] == 2 && v[t] >= 0.0) || (P.sister_on && v[t] >= P.sister_thr);
+        };
         if (compact) {
           int n2 = 0;
           for (int t0 = 0; t0 < ns; t0 += 64) {
@@ -1666,7 +1716,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
             if (w) {
               const int q = o + __popcll(wm & lanes_below());
               S.dump_cg[base + q] = cg_of(F, t);
-              S.dump_mean[base + q] = v[t];          // (evaluated: potential rows are whole)
+              S.dump_mean[base + q] = v[t];          // (evaluated: member rows are whole)
             }
             o += __popcll(wm);
           }

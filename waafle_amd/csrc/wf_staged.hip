@@ -1071,6 +1071,49 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S_arg, int n_act, int le
   __shared__ unsigned long long s_head[kOneCap / 64];   // clade-run heads, one ballot per 64
   __shared__ int s_cnt;
   const int lane = threadIdx.x;
+  // straight to the segment-table decision (k_big_sparse): the dense matrix cannot fit the
+  // arena (or every decision is routed there; routed ones with few segments take explain_one
+  // here first)
+  auto straight_big = [](const SArgs& S, int G, int ns) {
+    return S.sparse_on && G <= 63 &&
+           (S.route_sparse || (ns > kOneCap && arena_bound(ns + 1, G) + 4096 > S.dec_lds_bytes)) &&
+           !(S.route_sparse && !S.force_big && ns <= kOneCap && S.k.p.weak != 2);
+  };
+  // those first, a contig per lane: one list append (and one need_bytes max) per wave instead
+  // of one contended atomic per contig (the cfg5 stress levels: every contig goes there)
+  for (int base = blockIdx.x * 64; base < n_act; base += gridDim.x * 64) {
+    const SArgs& S = kernarg_fresh<SArgs>(S_arg);
+    const KArgs& K = S.k;
+    const int cr = base + lane;
+    bool big = false;
+    int c = 0;
+    int64_t need = 0;
+    if (cr < n_act) {
+      c = S.act ? S.act[cr] : cr;
+      const int64_t l0 = K.loc_off[c];
+      const int G = (int)(K.loc_off[c + 1] - l0);
+      const int so = n_keys > 0 ? S.crank_first[cr] : 0;
+      const int ns = (n_keys > 0 ? S.crank_first[cr + 1] : 0) - so;
+      big = K.hit_off[c + 1] != K.hit_off[c] && G != 0 && straight_big(S, G, ns);
+      if (big) need = arena_bound(ns + 1, G) + 4096;    // (the HBM-slot decision, should it decline)
+    }
+    const uint64_t bm = __ballot(big);
+    if (bm) {
+      const int leader = __builtin_ctzll(bm);
+      unsigned long long first = 0;
+      if (lane == leader) first = atomicAdd(&S.counters[2], (unsigned long long)__popcll(bm));
+      const int slot = (int)__shfl((long long)first, leader, 64) + __popcll(bm & ((1ull << lane) - 1ull));
+      if (big) {
+        K.need[c] = need;
+        S.big_list[2 * slot] = cr;
+        S.big_list[2 * slot + 1] = c;
+      }
+      long long mx = need;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) mx = max(mx, (long long)__shfl_xor(mx, off, 64));
+      if (lane == leader) atomicMax(&S.counters[3], (unsigned long long)mx);
+    }
+  }
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const SArgs& S = kernarg_fresh<SArgs>(S_arg);
     const KArgs& K = S.k;
@@ -1082,8 +1125,9 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S_arg, int n_act, int le
     if (K.hit_off[c + 1] == h0 || G == 0) continue;       // never evaluated (orgscorer.py:959)
     const int so = n_keys > 0 ? S.crank_first[cr] : 0;
     const int ns = (n_keys > 0 ? S.crank_first[cr + 1] : 0) - so;
-    // straight to the segment-table decision (k_big_sparse), with need_bytes for the
-    // HBM-slot decision should it decline the contig
+    if (straight_big(S, G, ns)) continue;               // (listed above)
+    const bool to_sparse = S.sparse_on && G <= 63;
+    // routed decisions without an explain_one option go to k_big_sparse for explain_two
     auto push_big = [&]() {
       if (lane == 0) {
         const int64_t need = arena_bound(ns + 1, G) + 4096;
@@ -1094,15 +1138,6 @@ __global__ __launch_bounds__(64) void k_one(const SArgs S_arg, int n_act, int le
         atomicMax(&S.counters[3], (unsigned long long)need);
       }
     };
-    const bool to_sparse = S.sparse_on && G <= 63;
-    if (to_sparse && (S.route_sparse || (ns > kOneCap && arena_bound(ns + 1, G) + 4096 > S.dec_lds_bytes))) {
-      if (S.route_sparse && !S.force_big && ns <= kOneCap && P.weak != 2) {
-        // (routed decisions: explain_one here first, explain_two there)
-      } else {
-        push_big();                                     // the dense matrix cannot fit the arena
-        continue;
-      }
-    }
     if (ns > kOneCap || G > 64 || P.weak == 2 || S.force_big) {
       if (lane == 0) {
         const int slot = (int)atomicAdd(&S.counters[6], 1ull);

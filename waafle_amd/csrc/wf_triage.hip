@@ -445,6 +445,7 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const int lane = threadIdx.x;
+  unsigned long long n_staged = 0;
   for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     if (h1 - h0 <= kTrBig) continue;                 // (k_triage handed it on: pend kPendTriage)
@@ -498,10 +499,11 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
       ccnt[c] = n_att;
       cleaves[c] = nl;
       pend[c] = 1;                                   // staged from level 0
-      if (S.fail_ctr) atomicAdd(S.fail_ctr, 1ull);
     }
+    ++n_staged;
     wave_sync();
   }
+  if (lane == 0 && n_staged && S.fail_ctr) atomicAdd(S.fail_ctr, n_staged);   // (one add per wave)
 }
 
 }  // namespace
