@@ -52,6 +52,10 @@
 #ifndef WF_E2_MEMBERS
 #define WF_E2_MEMBERS 1
 #endif
+// ... and pass-4 segments surely above every threshold left unevaluated (1)
+#ifndef WF_E2_LB
+#define WF_E2_LB 1
+#endif
 #ifndef WF_ROLL_WAVES
 #define WF_ROLL_WAVES 4
 #endif
@@ -1174,6 +1178,25 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
       auto best_score = [&](int t) -> double {       // (callers: v[t] < 0)
         return FULL ? scan_best(t) : -1.0 - v[t];
       };
+      // Hand-over (WF_E2_LB): a pass-4 candidate whose mean is surely >= every threshold the
+      // table's non-member readers compare it with (k2, the sister threshold, kmin) -- some
+      // attachment's run alone gives the envelope a mean >= score x share, numpy's rounding
+      // inside the 2e-12 slack -- is not evaluated in pass 4 (rc bit 0x80); its clade's mask
+      // and potential flag count it, a member's row evaluates it in pass 5, and otherwise the
+      // table carries lb_thr in its place (the same answer to every such comparison).
+      const double lb_thr = fmax(fmax(P.k2, P.sister_on ? P.sister_thr : 0.0), P.kmin);
+      auto lb_sure = [&](int t) -> bool {
+        const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
+        const double len = (double)F.len[cg_of(F, t).y];
+        double lb = 0.0;
+        for (int q = kb; q < ke; ++q) {
+          const int slot = slot_at(q);
+          const uint32_t x = F.lohi[slot];
+          const int run = max(0, hi16(x) - lo16(x));
+          lb = fmax(lb, F.sc[slot] * ((double)run / len) * (1.0 - 2e-12));
+        }
+        return lb >= lb_thr;
+      };
       int n_pass0 = -1;                                // pass 0's list, built with the run sizes
       if (prune) {
         // every segment's clade-run size, from the run heads' ballot masks: a lane's run
@@ -1273,9 +1296,13 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
                 in = v[t] < 0.0 && ((um >> cg.y) & 1ull) && (int)rc[t] == gu;
               } else if (pass == 4) {
                 in = v[t] < 0.0 && best_score(t) >= bound2;
+                if (!FULL && WF_E2_LB && in && lb_sure(t)) {
+                  in = false;
+                  rc[t] |= 0x80;                       // (run sizes < 0x80: pass 4's post replaces them)
+                }
               } else if (pass == 5) {
                 if (v[t] < 0.0) {
-                  in = rc[t] == 1;                     // a (member) potential clade's row
+                  in = (rc[t] & 3) == 1;               // a (member) potential clade's row
                   if (!in && P.sister_on && best_score(t) >= bound_s) {
                     const int sp = K.sibp[cg.x];
                     for (int i = 0; i < npp && !in; ++i) in = pp[i] == sp;
@@ -1430,61 +1457,63 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           um = __ballot(lane < G && (P.weak != 0 || mxl >= P.kmin));
           e1_now = true;
         } else if (pass == 4) {                        // potential clades: a mean >= k2 (:603-605)
-          for (int t = lane; t < ns; t += 64)
-            if (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x) {
-              const int cnt = run_count(t, ~0ull);
-              bool pot = false;
-              for (int q = t; q < t + cnt; ++q) pot = pot || (v[q] >= P.k2);
-              for (int q = t; q < t + cnt; ++q) rc[q] = pot ? 1 : 0;
+          // One walk per clade run: its size, whether it is potential, and (hand-over) its
+          // loci >= k2 on the unmasked set.  Hand-over: only potential clades that form a
+          // candidate pair (crit >= k2 <=> (m_i | m_j) == um: exact here, every segment that
+          // can reach k2 was evaluated by pass 4) have their rows read by explain_two's ranks
+          // and LGT checks; the others (rc 2) keep what pass 4 evaluated -- enough to find them
+          // potential and to build their masks -- and count as sisters through pass 5's sister
+          // candidates like any other clade.  Lane i: potential clade i's run (<= 64 of them,
+          // else pass 6 below).
+          const bool members = !FULL && WF_E2_MEMBERS;
+          int ph = -1, pcnt = 0, np0 = 0;
+          uint64_t pm = 0;
+          for (int t0 = 0; t0 < ns; t0 += 64) {
+            const int t = t0 + lane;
+            const bool head = t < ns && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
+            bool pot = false;
+            uint64_t m = 0;
+            int cnt = 0;
+            if (head) {
+              const int clade = cg_of(F, t).x;
+              for (int q = t; q < ns; ++q) {
+                const int2 cq = cg_of(F, q);
+                if (cq.x != clade) break;
+                ++cnt;
+                if (v[q] >= P.k2 || (rc[q] & 0x80)) { pot = true; m |= 1ull << cq.y; }
+              }
+              for (int q = t; q < t + cnt; ++q) rc[q] = (uint8_t)((rc[q] & 0x80) | (pot ? 1 : 0));
             }
-          wave_sync();
-          if (!FULL && WF_E2_MEMBERS) {
-            // Hand-over: only potential clades that form a candidate pair (crit >= k2 <=>
-            // (m_i | m_j) == um, m = loci >= k2: exact here, every segment that can reach k2
-            // was evaluated by pass 4) have their rows read by explain_two's ranks and LGT
-            // checks; the others (rc 2) keep what pass 4 evaluated -- enough to find them
-            // potential and to build their masks -- and count as sisters through pass 5's
-            // sister candidates like any other clade.  Lane i: potential clade i's run start
-            // and mask (<= 64 of them, else pass 6 below).
-            int ph = -1;
-            uint64_t pm = 0;
-            int np0 = 0;
-            for (int t0 = 0; t0 < ns; t0 += 64) {
-              const int t = t0 + lane;
-              const bool in = t < ns && rc[t] && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
-              const uint64_t im = __ballot(in);
-              uint64_t m = 0;
-              if (in)
-                for (int q = t; q < ns && cg_of(F, q).x == cg_of(F, t).x; ++q)
-                  if (v[q] >= P.k2) m |= 1ull << cg_of(F, q).y;
-              m &= um;
+            m &= um;
+            const uint64_t im = __ballot(head && pot);
+            if (members)
               for (uint64_t r = im; r; r &= r - 1) {     // potential clade np0 + k -> lane np0 + k
                 const int src = __builtin_ctzll(r);
                 const int dst = np0 + __popcll(im & ((1ull << src) - 1ull));
-                const int hsrc = lane_bcast(t, src);
-                const uint64_t msrc = lane_bcast(m, src);
-                if (lane == dst && dst < 64) { ph = hsrc; pm = msrc; }
+                const int hs = lane_bcast(t, src), hc = lane_bcast(cnt, src);
+                const uint64_t ms = lane_bcast(m, src);
+                if (lane == dst) { ph = hs; pcnt = hc; pm = ms; }
               }
-              np0 += __popcll(im);
+            np0 += __popcll(im);
+          }
+          wave_sync();
+          if (members && np0 <= 64) {
+            bool member = false;
+            for (int j = 0; j < np0; ++j) {
+              const uint64_t mj = lane_bcast(pm, j);
+              member = member || (lane != j && (pm | mj) == um);
             }
-            if (np0 <= 64) {
-              bool member = false;
-              for (int j = 0; j < np0; ++j) {
-                const uint64_t mj = lane_bcast(pm, j);
-                member = member || (lane < np0 && lane != j && (pm | mj) == um);
-              }
-              if (lane < np0 && !member)
-                for (int q = ph; q < ns && cg_of(F, q).x == cg_of(F, ph).x; ++q) rc[q] = 2;
-              wave_sync();
-            }
+            if (lane < np0 && !member)
+              for (int q = ph; q < ph + pcnt; ++q) rc[q] = (uint8_t)((rc[q] & 0x80) | 2);
+            wave_sync();
           }
           npp = 0;                                     // their parents (sister checks, :717-744)
           int npot = 0;
           for (int t0 = 0; t0 < ns; t0 += 64) {
             const int t = t0 + lane;
-            const bool in = t < ns && rc[t] && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
+            const bool in = t < ns && (rc[t] & 3) && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
             const uint64_t im = __ballot(in);
-            const bool mem_in = in && rc[t] == 1;        // (the parents of candidate-pair members)
+            const bool mem_in = in && (rc[t] & 3) == 1;  // (the parents of candidate-pair members)
             const uint64_t mm = __ballot(mem_in);
             // the sisters of X are the clades listed under parent(X) (get_sisters, utils.py:428-434):
             // pass 5 evaluates clades whose listed parent is one of these.  (Not sibp(X): an
@@ -1682,8 +1711,11 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         bool rootp = false;
         // (rc 2: a potential clade in no candidate pair -- its evaluated segments only)
         auto want = [&](int t) {
-          return rc[t] == 1 || (rc[t] == 2 && v[t] >= 0.0) || (P.sister_on && v[t] >= P.sister_thr);
+          const int k = rc[t] & 3;
+          return k == 1 || (k == 2 && (v[t] >= 0.0 || (rc[t] & 0x80))) || (P.sister_on && v[t] >= P.sister_thr);
         };
+        // (not evaluated: lb_thr for a pass-4 segment known >= it, else 0.0 -- see prune2d)
+        auto out_v = [&](int t) { return v[t] >= 0.0 ? v[t] : ((rc[t] & 0x80) ? lb_thr : 0.0); };
         if (compact) {
           int n2 = 0;
           for (int t0 = 0; t0 < ns; t0 += 64) {
@@ -1716,14 +1748,14 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
             if (w) {
               const int q = o + __popcll(wm & lanes_below());
               S.dump_cg[base + q] = cg_of(F, t);
-              S.dump_mean[base + q] = v[t];          // (evaluated: member rows are whole)
+              S.dump_mean[base + q] = out_v(t);      // (member rows are whole)
             }
             o += __popcll(wm);
           }
         } else if (dumped) {
           for (int t = lane; t < ns; t += 64) {
             S.dump_cg[base + t] = cg_of(F, t);
-            S.dump_mean[base + t] = v[t] < 0.0 ? 0.0 : v[t];   // (not evaluated: see prune2d)
+            S.dump_mean[base + t] = out_v(t);
           }
         }
         if (lane == 0) {
