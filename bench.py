@@ -410,6 +410,11 @@ def wdist_max(x, dist, dev):
 
 def main():
     args = parse_args()
+    # stdout carries the one JSON line alone: anything a library prints there (gloo's
+    # connection notices, runtime messages) goes to stderr instead
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     from waafle_amd import dist as wdist
     from waafle_amd import synth
     rank, world, local = wdist.rank_env()
@@ -661,7 +666,7 @@ def main():
     if e2e_lines:
         result["cli_end_to_end"] = e2e_lines
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     if dist:
         dist.destroy_process_group()
 

@@ -85,8 +85,8 @@ def main():
            "sp_two": {"sampled": w[8],
                       "cycles_per_contig": sum(w[:6]) / max(1, w[8]),
                       "phases": {k: w[i] / max(1, w[8]) for i, k in enumerate(
-                          ["table + loci loads", "run heads / potentials", "parents + sister masks",
-                           "candidate pairs", "pass 1 ranks", "pass 2, eval_two, meld, record"])},
+                          ["table + loci loads", "run heads / potentials", "candidate pairs",
+                           "members' parents + sister masks", "pass 1 ranks", "pass 2, eval_two, meld, record"])},
                       "per_contig": {"segments": w[9] / max(1, w[8]), "potential clades": w[10] / max(1, w[8]),
                                      "candidate pairs": w[11] / max(1, w[8])}}}
     tr = (C.c_ulonglong * 16)()

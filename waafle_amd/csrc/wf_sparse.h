@@ -1212,49 +1212,14 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
   __syncthreads();
   SLAP(1);
   SSTAT(10, Pp);
-  int hsp[kCh];                                        // listed parents of the runs' clades
-#pragma unroll
-  for (int k = 0; k < kCh; ++k) hsp[k] = (P.sister_on && hcl[k] >= 0 && hh[k] != 0ull) ? K.sibp[hcl[k]] : -1;
-  const int my_cl = lane < Pp ? sh.cl[lane] : -1;
-  const int my_par = lane < Pp ? K.parent[my_cl] : -2;
-  if (lane < Pp) {
-    sh.par[lane] = my_par;
-    sh.sibp[lane] = K.sibp[my_cl];
-  }
   const uint64_t my_pm = lane < Pp ? sh.pm[lane] : 0ull;   // (cand overwrites pm and cg)
-  __syncthreads();
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
-  if (P.sister_on) {
-    // per potential clade, the present clades listed under its parent (itself excluded) at
-    // or above the threshold (a segment left out of the table scores below it)
-    uint64_t s1 = 0, s2 = 0;
-#pragma unroll
-    for (int k = 0; k < kCh; ++k) {
-      if (64 * k >= ns) break;
-      const int sp = hsp[k], cl = hcl[k];
-      const uint64_t h = hh[k];
-      bool match = false;
-      for (int i = 0; i < Pp; ++i) match = match || (sp >= 0 && sp == lane_bcast(my_par, i));
-      for (uint64_t mb = __ballot(match); mb; mb &= mb - 1) {
-        const int src = __builtin_ctzll(mb);
-        const int sp_r = lane_bcast(sp, src), cl_r = lane_bcast(cl, src);
-        const uint64_t h_r = lane_bcast(h, src);
-        if (my_par == sp_r && my_cl != cl_r) {
-          s2 |= s1 & h_r;
-          s1 |= h_r;
-        }
-      }
-    }
-    if (lane < Pp) { sh.s1[lane] = s1; sh.s2[lane] = s2; }
-    __syncthreads();
-  }
-  SLAP(2);
   // the candidate pairs, crit >= k2 <=> (m_i | m_j) == um, listed so that their ranks are
   // taken 64 at a time (one pair per lane): the Pp (Pp - 1) / 2 pairs are tested 64 at a
   // time too, pair p = j (j - 1) / 2 + i (i < j) on lane p mod 64, the two masks fetched
   // from lanes i and j (the list order does not matter: pass 1 selects by (rank, pair
   // index), pass 2 only aggregates)
-  __syncthreads();                                   // (every read of cg done)
+  __syncthreads();                                   // (every read of cg and pm done)
   int nc = 0;
   const int n_pairs = Pp * (Pp - 1) / 2;
   for (int p0 = 0; p0 < n_pairs; p0 += 64) {
@@ -1270,8 +1235,49 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
     nc += __popcll(cb);
   }
   __syncthreads();
-  SLAP(3);
+  // the potential clades in some candidate pair: the only ones whose parent, listed parent
+  // and sister masks the LGT checks read (e2_eval)
+  uint64_t memb = 0;
+  for (int q = lane; q < nc; q += 64) memb |= (1ull << (sh.cand[q] & 0xFF)) | (1ull << (sh.cand[q] >> 8));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) memb |= (uint64_t)__shfl_xor((long long)memb, off, 64);
+  SLAP(2);
   SSTAT(11, nc);
+  if (P.sister_on && memb) {
+    const bool me = (memb >> lane) & 1ull;
+    const int my_cl = me ? sh.cl[lane] : -1;
+    const int my_par = me ? K.parent[my_cl] : -2;
+    if (me) {
+      sh.par[lane] = my_par;
+      sh.sibp[lane] = K.sibp[my_cl];
+    }
+    int hsp[kCh];                                      // listed parents of the runs' clades
+#pragma unroll
+    for (int k = 0; k < kCh; ++k) hsp[k] = (hcl[k] >= 0 && hh[k] != 0ull) ? K.sibp[hcl[k]] : -1;
+    // per member, the present clades listed under its parent (itself excluded) at or above
+    // the threshold (a segment left out of the table scores below it)
+    uint64_t s1 = 0, s2 = 0;
+#pragma unroll
+    for (int k = 0; k < kCh; ++k) {
+      if (64 * k >= ns) break;
+      const int sp = hsp[k], cl = hcl[k];
+      const uint64_t h = hh[k];
+      bool match = false;
+      for (uint64_t r = memb; r; r &= r - 1) match = match || (sp >= 0 && sp == lane_bcast(my_par, __builtin_ctzll(r)));
+      for (uint64_t mb = __ballot(match); mb; mb &= mb - 1) {
+        const int src = __builtin_ctzll(mb);
+        const int sp_r = lane_bcast(sp, src), cl_r = lane_bcast(cl, src);
+        const uint64_t h_r = lane_bcast(h, src);
+        if (my_par == sp_r && my_cl != cl_r) {
+          s2 |= s1 & h_r;
+          s1 |= h_r;
+        }
+      }
+    }
+    if (me) { sh.s1[lane] = s1; sh.s2[lane] = s2; }
+    __syncthreads();
+  }
+  SLAP(3);
   // pass 1: the best candidate pair by (rank, pair index)
   double pr = -__builtin_inf();
   long long pk = -1;
