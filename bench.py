@@ -390,13 +390,14 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
             kb = tj.get("per_kernel_kb", {}).get("k_big_sparse", {})
             f, w = kb.get("FETCH_SIZE", 0.0) * 1024.0, kb.get("WRITE_SIZE", 0.0) * 1024.0
             big_ms = per("big")
+            moved = 2.0 * f + w
             out["b_k2_actual"] = {
                 "kernel": "k_big_sparse", "fetch_bytes_raw": f, "fetch_bytes_x2": 2.0 * f, "write_bytes": w,
-                "bytes_per_pass": f + w, "achieved_GBs": (f + w) / max(big_ms * 1e-3, 1e-12) / 1e9,
-                "frac": (f + w) / max(big_ms * 1e-3, 1e-12) / 1e9 / HBM_PEAK_GBS,
-                "rule": "k_big_sparse FETCH_SIZE (raw) + WRITE_SIZE per pass (rocprofv3 --pmc, separate "
-                        "runs, this build) / this run's 'big' phase time (k_big_sparse and the dense "
-                        "decisions it declines)",
+                "bytes_per_pass": moved, "achieved_GBs": moved / max(big_ms * 1e-3, 1e-12) / 1e9,
+                "frac": moved / max(big_ms * 1e-3, 1e-12) / 1e9 / HBM_PEAK_GBS,
+                "rule": "k_big_sparse 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE per pass (rocprofv3 "
+                        "--pmc, separate runs, this build) / this run's 'big' phase time (k_big_sparse and "
+                        "the dense decisions it declines)",
                 "source": tj.get("source")}
         else:
             out["b_k2_actual"] = {"skipped": "traffic file of another library build or shape"}
@@ -563,11 +564,14 @@ def main():
     tj, why_t = pmc_file(args.traffic_json or os.path.join(PROFILES, "r05", "traffic_{}.json".format(args.config)),
                          "traffic")
     if tj:
-        traffic = tj.get("dominant_hbm_bytes_raw")
-        tsrc = {k: tj.get(k) for k in ("dominant_kernel", "dominant_fetch_bytes_raw",
+        # per launch, corrected as MI355X_MICROARCH.md's HBM / rocprofv3 section prescribes:
+        # gfx950's FETCH_SIZE counts half the bytes of a coalesced streaming read (x2)
+        traffic = 2.0 * tj["dominant_fetch_bytes_raw"] + tj["dominant_write_bytes"]
+        tsrc = {"rule": "2 x FETCH_SIZE + WRITE_SIZE of the dominant kernel per launch (gfx950 FETCH x2)"}
+        tsrc.update({k: tj.get(k) for k in ("dominant_kernel", "dominant_fetch_bytes_raw",
                                        "dominant_write_bytes", "fetch_bytes_raw",
                                        "fetch_bytes_x2", "write_bytes", "hbm_bytes_raw",
-                                       "hbm_bytes_x2", "dispatches_per_pass", "source")}
+                                       "hbm_bytes_x2", "dispatches_per_pass", "source")})
     else:
         tsrc = {"skipped": why_t}
     valu = None

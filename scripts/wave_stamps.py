@@ -79,6 +79,7 @@ def main():
                       for i, p in enumerate(PHASES)},
            "stats_per_contig": {name: v[i] / nc for i, name in STATS.items()},
            "pass_entries_per_contig": {str(p): v[24 + p] / nc for p in range(8)},
+           "segments_listed_per_contig_by_pass": {str(p): v[40 + p] / nc for p in range(8)},
            "explain_one": {k: v[32 + i] / nc for i, k in enumerate(
                ["sure bits/pass choice", "option scan", "reduction", "meld_one+LCA"])},
            # sp_two (k_dump_sparse<1>, every launch of the pass), every 8th contig

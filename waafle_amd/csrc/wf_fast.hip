@@ -56,6 +56,10 @@
 #ifndef WF_E2_LB
 #define WF_E2_LB 1
 #endif
+// unmasked loci settled by lower bounds where the hand-over is the compact table (1)
+#ifndef WF_UM_LB
+#define WF_UM_LB 1
+#endif
 #ifndef WF_ROLL_WAVES
 #define WF_ROLL_WAVES 4
 #endif
@@ -1185,7 +1189,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
       // and potential flag count it, a member's row evaluates it in pass 5, and otherwise the
       // table carries lb_thr in its place (the same answer to every such comparison).
       const double lb_thr = fmax(fmax(P.k2, P.sister_on ? P.sister_thr : 0.0), P.kmin);
-      auto lb_sure = [&](int t) -> bool {
+      auto lb_mean = [&](int t) -> double {
         const int kb = seg_first(F, t), ke = t + 1 < ns ? seg_first(F, t + 1) : n_att;
         const double len = (double)F.len[cg_of(F, t).y];
         double lb = 0.0;
@@ -1195,7 +1199,25 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           const int run = max(0, hi16(x) - lo16(x));
           lb = fmax(lb, F.sc[slot] * ((double)run / len) * (1.0 - 2e-12));
         }
-        return lb >= lb_thr;
+        return lb;
+      };
+      auto lb_sure = [&](int t) -> bool { return lb_mean(t) >= lb_thr; };
+      // Unmasked loci settled by lower bounds (WF_UM_LB): a known clade's segment whose bound
+      // reaches kmin unmasks its locus (:420-427) without its mean.  Only where the contig's
+      // hand-over is sure to be the compact table (whose explain_two takes um from the header;
+      // a whole table would rebuild um from the values it holds) or everything gets evaluated
+      // (pass 6), and explain_one reads only the means of the clades it ranks.
+      const bool lb_um = !FULL && WF_UM_LB && prune2d && S.wave_two && S.dump_cap > 0 && G <= kE2MaxG &&
+                         ns <= kE2Seg && P.weak == 0 && P.kmin > 0.0;
+      auto lb_um_bits = [&](uint64_t open_) -> uint64_t {
+        uint64_t b = 0;
+        for (int t = lane; t < ns; t += 64) {
+          const int2 cg = cg_of(F, t);
+          if (cg.x != K.unknown && ((open_ >> cg.y) & 1ull) && v[t] < 0.0 && -1.0 - v[t] >= P.kmin &&
+              lb_mean(t) >= P.kmin * (1.0 + 1e-12))
+            b |= 1ull << cg.y;
+        }
+        return wave_or_dpp(b);
       };
       int n_pass0 = -1;                                // pass 0's list, built with the run sizes
       if (prune) {
@@ -1321,6 +1343,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         }
         WLAP(6);
         WSTAT(20, n);
+        WSTAT(40 + pass, n);                          // (segments listed per pass)
         for (int s0 = 0; s0 < n; s0 += 64) {
           const int s = s0 + lane < n ? (list ? (int)list[s0 + lane] : s0 + lane) : ns;
           bool multi = false, big = false;               // big: too many attachments for the wave path
@@ -1420,6 +1443,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           } else {
             um = sure_bits();
             open = allG & ~um;                         // loci no full clade settles
+            if (open && lb_um) {
+              um |= lb_um_bits(open);
+              open = allG & ~um;
+            }
             if (open) { pass = 1; continue; }
             e1_now = true;
           }
