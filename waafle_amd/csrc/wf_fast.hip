@@ -856,7 +856,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           r_scv[b] = K.scov[h];
           r_qlo[b] = K.qlo[h];
           r_qhi[b] = K.qhi[h];
-          r_hs[b] = K.hstrand[h];
+          if (P.stranded) r_hs[b] = K.hstrand[h];      // (the strand only matters --stranded)
           r_cl[b] = K.taxon[h];
           r_sc[b] = K.score[h];
           if (ann_on) r_m[b] = K.sysmask[h];

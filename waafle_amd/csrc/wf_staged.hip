@@ -192,7 +192,7 @@ __global__ __launch_bounds__(NT) void k_att_contig(const SArgs S_arg, int64_t* c
       uint32_t m = 0u;
       if (h < h1) {                                 // every field of the hit in one round of loads
         scv = K.scov[h];
-        qlo = K.qlo[h]; qhi = K.qhi[h]; hs = K.hstrand[h];
+        qlo = K.qlo[h]; qhi = K.qhi[h]; hs = P.stranded ? K.hstrand[h] : 0;
         if (PASS == 1) {
           clade = K.taxon[h];
           sc = K.score[h];

@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
         r_scv[b] = K.scov[h];
         r_qlo[b] = K.qlo[h];
         r_qhi[b] = K.qhi[h];
-        r_hs[b] = K.hstrand[h];
+        if (P.stranded) r_hs[b] = K.hstrand[h];        // (the strand only matters --stranded)
         r_cl[b] = K.taxon[h];
         r_sc[b] = K.score[h];
         if (nsys > 0) r_m[b] = K.sysmask[h];
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
       for (int r = 0; r < kCntR; ++r) {
         const int64_t h = hb + 64 * r + lane;
         r_scv[r] = -1.0; r_qlo[r] = 0; r_qhi[r] = 0; r_hs[r] = 0;
-        if (h < h1) { r_scv[r] = K.scov[h]; r_qlo[r] = K.qlo[h]; r_qhi[r] = K.qhi[h]; r_hs[r] = K.hstrand[h]; }
+        if (h < h1) { r_scv[r] = K.scov[h]; r_qlo[r] = K.qlo[h]; r_qhi[r] = K.qhi[h]; if (P.stranded) r_hs[r] = K.hstrand[h]; }
       }
 #pragma unroll
       for (int r = 0; r < kCntR; ++r) {
