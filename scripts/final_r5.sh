@@ -4,8 +4,8 @@
 #           SQ -> cfg4_valu.json, dominant kernel k_triage), of the cfg5 k2 leg (pmc_k2_r5.sh:
 #           SQ -> k2_pmc.json, FETCH/WRITE -> traffic_cfg5.json) and rocprofv3 kernel-trace
 #           summaries of the cfg4 and cfg5 commands
-#   BENCH=1 the full bench line (CPU legs, k2 leg, PCIe and CLI scopes); run after PMC=1 has
-#           been copied into profiles/r05 so the line carries this build's counters
+#   BENCH=1 the full bench line (CPU legs, k2 leg, PCIe and CLI scopes); with PMC=1 in the same
+#           call it reads the counters just taken (copied into this tree's profiles/r05)
 #   N2=1    bench.py's N > 1 branch as two gloo ranks on device 0 (a rehearsal line)
 # OUT names gpurun_out/<OUT>; copy what is judged into profiles/r05/.
 set -u
@@ -27,6 +27,8 @@ if [ "${PMC:-0}" = 1 ]; then
   python3 scripts/lvl.py $f > $O/cfg4_levels.txt 2>&1
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/kt5 -o run --output-format csv -- python3 bench.py --config cfg5 --contigs 6250 $Q --steps 3 --warmup 1 > $O/kt5.json 2> $O/kt5.err || exit $?
   python3 scripts/show_prof.py $O/kt5/run_kernel_stats.csv > $O/cfg5_6250_kernel_stats.txt 2>&1
+  # (this copy of the tree: the bench step below reads this build's counters from profiles/r05)
+  cp $O/traffic_cfg4.json $O/cfg4_valu.json $O/k2_pmc.json $O/traffic_cfg5.json profiles/r05/
 fi
 if [ "${BENCH:-0}" = 1 ]; then
   timeout -k 10 900 python3 bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
