@@ -47,11 +47,6 @@
 // resident waves per SIMD of the roll-up launches: 4 (128 VGPRs, some spilled) beat 3 (168,
 // none) by 0.35 ms of roll-up per cfg4 pass on one box (r4f: their few contigs per wave
 // want occupancy more than registers)
-// work queues: each wave's first contig is its own index and the counter is read before a
-// claim (1), or every contig claimed by an atomic (0)
-#ifndef WF_WQ_STATIC_FIRST
-#define WF_WQ_STATIC_FIRST 1
-#endif
 // hand-over: only candidate-pair members' rows evaluated whole (1), or every potential
 // clade's (0)
 #ifndef WF_E2_MEMBERS
@@ -822,23 +817,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
     if (S_arg.wq) {
       // a work queue: a wave takes the list's next contig when it finishes one (the roll-up
       // lists are ~20 k contigs of very different cost over ~4 k waves: static striding left
-      // the launches tail-bound).  Each wave's first contig is its own index, and a wave
-      // reads the counter before it claims: one contended atomic per wave at the start and
-      // at the end of a launch cost ~50 us each (an empty level's launch took 52 us).
-      if (WF_WQ_STATIC_FIRST && it == 0) {
-        ci = (int)blockIdx.x;
-      } else if (!WF_WQ_STATIC_FIRST) {
-        unsigned long long q = 0;
-        if (lane == 0) q = atomicAdd(S_arg.wq, 1ull);
-        ci = __builtin_amdgcn_readfirstlane((int)q);
-      } else {
-        const int done = (int)gridDim.x + (int)__builtin_amdgcn_readfirstlane(
-                                              (int)*reinterpret_cast<volatile unsigned long long*>(S_arg.wq));
-        if (done >= n_list) break;
-        unsigned long long q = 0;
-        if (lane == 0) q = atomicAdd(S_arg.wq, 1ull);
-        ci = (int)gridDim.x + __builtin_amdgcn_readfirstlane((int)q);
-      }
+      // the launches tail-bound)
+      unsigned long long q = 0;
+      if (lane == 0) q = atomicAdd(S_arg.wq, 1ull);
+      ci = __builtin_amdgcn_readfirstlane((int)q);
     } else {
       ci = xmap ? (it * kXcds + xx) * xb + xj : (int)blockIdx.x + it * (int)gridDim.x;
     }
