@@ -65,6 +65,9 @@ constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
 constexpr int kTrXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
 constexpr int kTrBig = 512;            // more hits than any wave slice: k_count
 constexpr int kCntR = 4;               // k_count: hit batches per round of loads
+#ifndef WF_COUNT_WIDE
+#define WF_COUNT_WIDE 0                // 512-thread k_count for contigs of thousands of hits
+#endif
 
 struct TriSmem {
   int lo[kTrLoc], hi[kTrLoc];          // locus site ranges (min, max of start/end)
@@ -506,6 +509,93 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
   if (lane == 0 && n_staged && S.fail_ctr) atomicAdd(S.fail_ctr, n_staged);   // (one add per wave)
 }
 
+#if WF_COUNT_WIDE
+template <int NT>
+__global__ __launch_bounds__(NT) void k_count_wide(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend) {
+  constexpr int kW = NT / 64;                      // (NT 512: contigs of thousands of hits, 8 waves each)
+  __shared__ int s_lo[kTrLoc], s_hi[kTrLoc];
+  __shared__ int8_t s_st[kTrLoc];
+  __shared__ int s_ok;
+  __shared__ long long s_red[2][kW];
+  const KArgs& K = S.k;
+  const DevParams& P = K.p;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  unsigned long long n_staged = 0;
+  for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
+    const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
+    if (h1 - h0 <= kTrBig) continue;                 // (k_triage handed it on: pend kPendTriage)
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    if (w == 0) {
+      int clo = 0, chi = -1, cst = 0;
+      if (lane < G && G <= kTrLoc) {
+        const int a = K.lstart[l0 + lane], e = K.lend[l0 + lane];
+        clo = min(a, e);
+        chi = max(a, e);
+        cst = K.lstrand[l0 + lane];
+      }
+      const int cprev = __shfl_up(chi, 1, 64);
+      const bool ok = G > 0 && G <= kTrLoc && P.min_overlap > 0.0 &&
+                      __ballot(lane < G && lane >= 1 && clo <= cprev) == 0ull;
+      if (lane == 0) s_ok = ok ? 1 : 0;
+      if (ok && lane < G) { s_lo[lane] = clo; s_hi[lane] = chi; s_st[lane] = (int8_t)cst; }
+    }
+    __syncthreads();
+    if (!s_ok) {                                     // (uniform) left to the wave form
+      __syncthreads();
+      continue;
+    }
+    long long n_att = 0, nl = 0;
+    for (int64_t hb = h0; hb < h1; hb += NT * kCntR) {   // kCntR batches' loads issued together
+      double r_scv[kCntR];
+      int r_qlo[kCntR], r_qhi[kCntR], r_hs[kCntR];
+#pragma unroll
+      for (int r = 0; r < kCntR; ++r) {
+        const int64_t h = hb + NT * r + tid;
+        r_scv[r] = -1.0; r_qlo[r] = 0; r_qhi[r] = 0; r_hs[r] = 0;
+        if (h < h1) { r_scv[r] = K.scov[h]; r_qlo[r] = K.qlo[h]; r_qhi[r] = K.qhi[h]; if (P.stranded) r_hs[r] = K.hstrand[h]; }
+      }
+#pragma unroll
+      for (int r = 0; r < kCntR; ++r) {
+        if (hb + NT * r + tid >= h1 || !(r_scv[r] >= P.min_scov)) continue;
+        const int qlo = r_qlo[r], qhi = r_qhi[r], hs = r_hs[r];
+        int g = 0;
+#pragma unroll
+        for (int k = 32; k > 0; k >>= 1)
+          if (g + k <= G && s_hi[g + k - 1] < qlo) g += k;
+        for (; g < G; ++g) {
+          const int lo = s_lo[g];
+          if (lo > qhi) break;
+          const int len = s_hi[g] - lo + 1;
+          if (attaches(P, qlo, qhi, hs, lo, len, s_st[g])) {
+            ++n_att;
+            nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+                  (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+          }
+        }
+      }
+    }
+    n_att = wave_sum_dpp(n_att);
+    nl = wave_sum_dpp(nl);
+    if (kW > 1) {
+      if (lane == 0) { s_red[0][w] = n_att; s_red[1][w] = nl; }
+      __syncthreads();
+      if (tid == 0)
+        for (int x = 1; x < kW; ++x) { n_att += s_red[0][x]; nl += s_red[1][x]; }
+    }
+    if (tid == 0) {
+      ccnt[c] = n_att;
+      cleaves[c] = nl;
+      pend[c] = 1;                                   // staged from level 0
+    }
+    ++n_staged;
+    __syncthreads();                                 // (the loci and s_ok are the next contig's)
+  }
+  if (tid == 0 && n_staged && S.fail_ctr) atomicAdd(S.fail_ctr, n_staged);   // (one add per workgroup)
+}
+
+#endif
+
 }  // namespace
 
 #ifdef WF_STAMPS
@@ -536,6 +626,12 @@ hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * triage_per_cu()));
   hipLaunchKernelGGL(k_triage, dim3(grid), dim3(64), 0, s, sa, ccnt, cleaves, pend);
   if (max_hits > kTrBig)
+#if WF_COUNT_WIDE
+    if (max_hits >= 2048)                             // thousands of hits per contig: 8 waves each
+      hipLaunchKernelGGL(k_count_wide<512>, dim3((unsigned)std::min<int64_t>(N, (int64_t)cus * 4)), dim3(512), 0, s,
+                         sa, ccnt, cleaves, pend);
+    else
+#endif
     hipLaunchKernelGGL(k_count, dim3((unsigned)std::min<int64_t>(N, (int64_t)cus * 32)), dim3(64), 0, s, sa, ccnt,
                        cleaves, pend);
   return hipGetLastError();
