@@ -234,3 +234,40 @@ def test_cfg5_shard_and_embedded_fixture(tmp_path):
     texts = {k: "\n".join(v) + "\n" for k, v in rows.items()}
     assert gc.compare_tsv(fx, texts) == []
     assert_same(slice_results(res, both, gb.n_contigs, both.n_contigs), whole, batch)
+
+
+FORM_FLAGS = [[], ["--sister-penalty", "lenient"], ["--sister-penalty", "off"],
+              ["-k1", "0.6", "-k2", "0.7"], ["-k1", "0.9"], ["--ambiguous-threshold", "strict", "--range", "0.1"],
+              ["--ambiguous-threshold", "off"], ["--disambiguate-two", "report-best"],
+              ["--weak-loci", "penalize"], ["--annotation-threshold", "strict"], ["--range", "0"],
+              ["--clade-genes", "2", "--clade-leaves", "2"]]
+
+
+@pytest.fixture(scope="module")
+def lgt_heavy():
+    """3,000 contigs with 30% LGT candidates and 20 decoys per gene over 300 clades: many
+    explain_two hand-overs and roll-ups (the pruned passes' inputs)."""
+    data = synth.generate(n=3000, genes=10, clades=300, decoys=20, lgt_frac=0.3, seed=57)
+    return synth.to_batch(data)
+
+
+@pytest.mark.parametrize("flags", FORM_FLAGS, ids=[" ".join(f) or "default" for f in FORM_FLAGS])
+def test_pruned_forms_agree_with_staged(lgt_heavy, flags):
+    """The default LEVEL0 form -- the triage, the first form's bounds (one-attachment upper
+    bounds, lower bounds for the unmasked loci and for pass 4), candidate-pair members' rows
+    only, the compact hand-over -- against the staged form, which evaluates every segment
+    mean and decides from whole tables, over flag sets that move every threshold those
+    shortcuts compare with (k1, k2, kmin, the sister and ambiguity thresholds, --range)."""
+    batch, tax = lgt_heavy
+    params = cli.param_dict(cli.parse_flags(flags))
+    got = {}
+    for form, kw in (("level0", {}), ("notriage", dict(options={lib.OPT_TRIAGE: 0})), ("staged", dict(mode="staged"))):
+        s = engine.GpuScorer(0, **kw)
+        try:
+            s.set_taxonomy(tax)
+            got[form] = s.score(batch, params)
+        finally:
+            s.close()
+    assert (got["staged"].call == 2).sum() > 100           # (the shortcuts' inputs are there)
+    assert_same(got["level0"], got["staged"], batch)
+    assert_same(got["notriage"], got["staged"], batch)
