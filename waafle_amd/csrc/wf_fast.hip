@@ -60,10 +60,6 @@
 #ifndef WF_UM_LB
 #define WF_UM_LB 1
 #endif
-// pass 4's run flags and masks from ballots (1), or a walk per clade run (0)
-#ifndef WF_P4_BALLOT
-#define WF_P4_BALLOT 0
-#endif
 #ifndef WF_ROLL_WAVES
 #define WF_ROLL_WAVES 4
 #endif
@@ -1499,58 +1495,6 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           const bool members = !FULL && WF_E2_MEMBERS;
           int ph = -1, pcnt = 0, np0 = 0;
           uint64_t pm = 0;
-#if WF_P4_BALLOT
-          // segment-parallel: each lane tests its own segment, a run's potential flag and
-          // mask come from ballots over the run's lanes (one per locus), and a lane takes its
-          // run's flag from the run head (a run crossing into the next chunk: its head walks
-          // the rest, the next chunk's lanes take the carried flag)
-          int carry_pot = 0;
-          const uint64_t le = lane == 63 ? ~0ull : (2ull << lane) - 1ull;
-          for (int t0 = 0; t0 < ns; t0 += 64) {
-            const int t = t0 + lane;
-            const bool live = t < ns;
-            const int2 cg = live ? cg_of(F, t) : make_int2(-1, 0);
-            const bool b = live && (v[t] >= P.k2 || (rc[t] & 0x80));
-            const bool head = live && (t == 0 || cg_of(F, t - 1).x != cg.x);
-            const uint64_t hd = __ballot(head), bb = __ballot(b);
-            const uint64_t gt = hd & ~le;
-            const int re = gt ? __builtin_ctzll(gt) : 64;          // run end (lane, exclusive)
-            const uint64_t run = (re == 64 ? ~0ull : ((1ull << re) - 1ull)) & ~((1ull << lane) - 1ull);
-            bool pot = head && (bb & run) != 0ull;
-            uint64_t m = 0;
-            for (int g = 0; g < G; ++g) {
-              const uint64_t bg = __ballot(b && cg.y == g);
-              if ((bg & run) != 0ull) m |= 1ull << g;
-            }
-            int cnt = re - lane;
-            if (head && re == 64)                                  // (may continue past the chunk)
-              for (int q = t0 + 64; q < ns; ++q) {
-                const int2 cq = cg_of(F, q);
-                if (cq.x != cg.x) break;
-                ++cnt;
-                if (v[q] >= P.k2 || (rc[q] & 0x80)) { pot = true; m |= 1ull << cq.y; }
-              }
-            pot = pot && head;
-            // each segment's run flag: from its head in this chunk, or carried from the last one
-            const uint64_t hl = hd & le;
-            const int rs = hl ? 63 - __clzll(hl) : -1;
-            const int potv = __shfl(pot ? 1 : 0, rs < 0 ? 0 : rs, 64);
-            const int mine = rs < 0 ? carry_pot : potv;
-            if (live) rc[t] = (uint8_t)((rc[t] & 0x80) | mine);
-            carry_pot = __shfl(mine, 63, 64);                     // (the chunk's last run)
-            m &= um;
-            const uint64_t im = __ballot(head && pot);
-            if (members)
-              for (uint64_t r = im; r; r &= r - 1) {     // potential clade np0 + k -> lane np0 + k
-                const int src = __builtin_ctzll(r);
-                const int dst = np0 + __popcll(im & ((1ull << src) - 1ull));
-                const int hs = lane_bcast(t, src), hc = lane_bcast(cnt, src);
-                const uint64_t ms = lane_bcast(m, src);
-                if (lane == dst) { ph = hs; pcnt = hc; pm = ms; }
-              }
-            np0 += __popcll(im);
-          }
-#else
           for (int t0 = 0; t0 < ns; t0 += 64) {
             const int t = t0 + lane;
             const bool head = t < ns && (t == 0 || cg_of(F, t - 1).x != cg_of(F, t).x);
@@ -1579,7 +1523,6 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
               }
             np0 += __popcll(im);
           }
-#endif
           wave_sync();
           if (members && np0 <= 64) {
             bool member = false;
