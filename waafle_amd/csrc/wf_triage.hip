@@ -65,6 +65,9 @@ constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
 constexpr int kTrXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
 constexpr int kTrBig = 512;            // more hits than any wave slice: k_count
 constexpr int kCntR = 4;               // k_count: hit batches per round of loads
+#ifndef WF_TRI_BF
+#define WF_TRI_BF 1                    // branch-free binary search and rank accumulation
+#endif
 #ifndef WF_COUNT_WIDE
 #define WF_COUNT_WIDE 0                // 512-thread k_count for contigs of thousands of hits
 #endif
@@ -185,8 +188,14 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
         const int qlo = r_qlo[b], qhi = r_qhi[b];
         int g = 0;
 #pragma unroll
-        for (int k = 32; k > 0; k >>= 1)
+        for (int k = 32; k > 0; k >>= 1) {
+#if WF_TRI_BF
+          const int gk = g + k;                      // (a select, not a branch per step)
+          g = (gk <= G && F.hi[min(gk, G) - 1] < qlo) ? gk : g;
+#else
           if (g + k <= G && F.hi[g + k - 1] < qlo) g += k;
+#endif
+        }
         const int g0 = g;
         uint32_t rel = 0u;
         for (; g < G; ++g) {
@@ -352,6 +361,17 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       const int m8 = G < 8 ? 0 : G - (G & 7);
       double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
       double mn = __builtin_inf();
+#if WF_TRI_BF
+      for (int u = 0; u < m8; u += 8) {                // (u % 8 -> accumulator, in order: straight-line)
+        const double x0 = lane_bcast(mean, base + u), x1 = lane_bcast(mean, base + u + 1);
+        const double x2 = lane_bcast(mean, base + u + 2), x3 = lane_bcast(mean, base + u + 3);
+        const double x4 = lane_bcast(mean, base + u + 4), x5 = lane_bcast(mean, base + u + 5);
+        const double x6 = lane_bcast(mean, base + u + 6), x7 = lane_bcast(mean, base + u + 7);
+        r0 += x0; r1 += x1; r2 += x2; r3 += x3; r4 += x4; r5 += x5; r6 += x6; r7 += x7;
+        mn = x0 < mn ? x0 : mn; mn = x1 < mn ? x1 : mn; mn = x2 < mn ? x2 : mn; mn = x3 < mn ? x3 : mn;
+        mn = x4 < mn ? x4 : mn; mn = x5 < mn ? x5 : mn; mn = x6 < mn ? x6 : mn; mn = x7 < mn ? x7 : mn;
+      }
+#else
       for (int u = 0; u < m8; ++u) {
         const double x = lane_bcast(mean, base + u);
         mn = x < mn ? x : mn;
@@ -366,6 +386,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
           default: r7 += x; break;
         }
       }
+#endif
       double res = m8 > 0 ? leaf_tree(r0, r1, r2, r3, r4, r5, r6, r7) : 0.0;
       for (int u = m8; u < G; ++u) {
         const double x = lane_bcast(mean, base + u);
