@@ -566,8 +566,11 @@ def write_details(details, C, iteration):
 
 
 def evaluate_contig(C, tax, details=None):
-    """orgscorer.py:566-583 (roll-up loop; runaway guard at 100 iterations)."""
+    """orgscorer.py:566-583 (roll-up loop; runaway guard at 100 iterations).  pair_evals
+    (a diagnostic the reference does not report) counts this evaluation's pairs: a contig of
+    an ungrouped blastout is evaluated once per run and reports its last evaluation."""
     it = 1
+    C.pair_evals = 0
     write_details(details, C, it)
     one = one_clade(C, tax)
     two = two_clade(C, tax) if not _ok(one) else None

@@ -150,3 +150,41 @@ def test_cli_two_ranks_one_device_match_one_rank(tmp_path):
     for r, (a, b) in enumerate(bounds):
         assert seen[r] == (a, b, int(batch.hit_off[b] - batch.hit_off[a]))
     assert 0 < bounds[0][1] < batch.n_contigs
+
+
+def test_ungrouped_blastout_cli_one_and_two_ranks(tmp_path):
+    """A blastout not grouped by query (tests/golden/make_ungrouped.py): the CLI on one rank
+    and as 2 ranks on device 0 (rank 0 scores the earlier runs, regroup.py, before the
+    split) writes the reference's TSVs; engine.score in two shards on one device agrees."""
+    import golden_cases as gc
+    from waafle_amd import cli, engine, inputs
+    for case in ("ungrouped_default", "ungrouped_jump-taxonomy_1"):
+        fx = gc.load(case)
+        paths = gc.materialize(fx, tmp_path)
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", WAAFLE_DEVICE_MAP="0,0")
+        one, two = tmp_path / (case + "_one"), tmp_path / (case + "_two")
+        one.mkdir()
+        two.mkdir()
+        r1 = subprocess.run([sys.executable, "-m", "waafle_amd.orgscorer"] + paths +
+                            ["--outdir", str(one), "--basename", "u", "--quiet"] + fx["flags"],
+                            capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+        assert r1.returncode == 0, r1.stderr[-2000:]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m",
+               "waafle_amd.orgscorer"] + paths + ["--outdir", str(two), "--basename", "u",
+                                                  "--quiet"] + fx["flags"]
+        r2 = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+        assert r2.returncode == 0, r2.stderr[-3000:]
+        texts = {}
+        for kind in ("lgt", "no_lgt", "unclassified"):
+            texts[kind] = (one / "u.{}.tsv".format(kind)).read_text()
+            assert (two / "u.{}.tsv".format(kind)).read_text() == texts[kind], kind
+        assert gc.compare_tsv(fx, texts) == []
+        args = cli.parse_flags(fx["flags"])
+        batch, tax = inputs.load_inputs(*paths, args.min_gene_length, warn=None)
+        assert batch.hit_group is not None
+        params = cli.param_dict(args)
+        a = engine.score(batch, tax, params, gpus=1)
+        b = engine.score(batch, tax, params, gpus=2, devices=[0, 0])
+        for f in ("call", "crit", "rank", "clade1", "clade2", "iterations", "annot_hit"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), f

@@ -87,11 +87,48 @@ def test_taxonomy_tables():
         TaxonomyTables([("s__C", "g__B"), ("s__C", "g__Z")])
 
 
-def test_ungrouped_blastout_is_rejected(tmp_path):
+def test_ungrouped_blastout_keeps_its_runs(tmp_path):
     fx = gc.load("tie_default")
     paths = gc.materialize(fx, tmp_path)
     lines = open(paths[1]).read().splitlines()
     bad = tmp_path / "bad.blastout"
     bad.write_text("\n".join([lines[0], lines[4], lines[1]]) + "\n")
-    with pytest.raises(inputs.InputError):
-        inputs.load_inputs(paths[0], str(bad), paths[2], paths[3], 200.0, warn=None)
+    b, _ = inputs.load_inputs(paths[0], str(bad), paths[2], paths[3], 200.0, warn=None)
+    q = [ln.split("\t", 1)[0] for ln in (lines[0], lines[4], lines[1])]
+    assert q[0] == q[2] != q[1]
+    c = b.contig_names.index(q[0])
+    h0, h1 = int(b.hit_off[c]), int(b.hit_off[c + 1])
+    assert b.hit_group[h0:h1].tolist() == [0, 1] and b.hit_row[h0:h1].tolist() == [0, 2]
+
+
+def test_regroup_raises_each_run_by_the_levels_it_has_been_through():
+    """regroup.resolve: run g's hits enter the last evaluation at ancestor^R(taxon),
+    R = sum over the evaluations since g of (jumps + iterations - 1) (orgscorer.py:941-960)."""
+    from waafle_amd import regroup
+    from waafle_amd.engine import Results
+    parent = np.array([0, 0, 1, 2, 3, 4, 5, 6, 7, 8], dtype=np.int32)   # a chain, 0 the root
+    H = 6
+    z = np.zeros(H, np.int32)
+    b = inputs.HostBatch(
+        contig_names=["a", "b"], contig_lengths=np.array([900, 900]), hit_off=np.array([0, 4, 6]),
+        hit_qlo=z + 1, hit_qhi=z + 300, hit_taxon=z + 9, hit_strand=z.astype(np.int8),
+        hit_score=np.ones(H), hit_scov=np.ones(H), hit_sysmask=z.astype(np.uint32),
+        loc_off=np.array([0, 1, 2]), loc_start=np.array([1, 1], np.int32),
+        loc_end=np.array([300, 300], np.int32), loc_strand=np.zeros(2, np.int8),
+        loc_codes=["1:300:+"] * 2,
+        hit_group=np.array([0, 0, 1, 2, 0, 1], np.int32))    # contig a: runs 0,0,1,2; b: 0,1
+    calls = []
+
+    def score_fn(sub):
+        calls.append((sub.n_contigs, sub.hit_off.tolist(), sub.hit_taxon.tolist()))
+        res = Results.empty(sub.n_contigs, sub.n_hits, sub.n_loci, 0)
+        res.iterations[:] = [3, 1][:sub.n_contigs] if len(calls) == 1 else [2]
+        return res
+
+    out = regroup.resolve(b, parent, {"jump_taxonomy": 1}, score_fn)
+    # evaluation 1: both contigs, their run-0 hits; evaluation 2: contig 0's runs 0-1
+    assert calls[0] == (2, [0, 2, 3], [9, 9, 9])
+    assert calls[1] == (1, [0, 3], [6, 6, 9])           # run 0 raised 1 + 2 = 3 levels
+    # contig 0: run 0 raised 3 + (1 + 1) = 5, run 1 raised 2, run 2 none; contig 1: run 0 1
+    assert out.hit_taxon.tolist() == [4, 4, 7, 9, 8, 9]
+    assert out.hit_group is None and b.hit_group is not None

@@ -54,7 +54,11 @@ def test_golden_inputs_native_equals_python(name, tmp_path):
     fx = gc.load(name)
     paths = gc.materialize(fx, tmp_path)
     args = cli.parse_flags(fx["flags"])
-    native_only(paths, args.min_gene_length)          # takes the native path (no fallback)
+    if name.startswith("ungrouped_"):                   # the Python reader's input
+        with pytest.raises(ingest.Fallback):
+            native_only(paths, args.min_gene_length)
+    else:
+        native_only(paths, args.min_gene_length)      # takes the native path (no fallback)
     a, b = both(paths, args.min_gene_length)
     assert_same(a, b)
 
@@ -144,7 +148,6 @@ def test_unusual_spelling_goes_to_python_reader(tmp_path, blast, gff, why):
     (BLAST.replace("\t1000\t300\t", "\t1000\t0\t", 1), GFF),             # slen 0
     (BLAST.replace("g2|s__B", "g2"), GFF),                               # bad sseqid
     (BLAST.replace("SYS=v1", "SYSv1"), GFF),                             # bad annotation
-    (BLAST + BLAST.splitlines(True)[0], GFF),                            # ungrouped contig
     (BLAST, GFF + "c1\tx\tgene\t1\t300\t.\t+\t0\tid=1\n"),               # ungrouped GFF
     (BLAST, GFF.replace("\t1.5\t", "\tabc\t")),                          # bad GFF score
     (BLAST, GFF + "\n"),                                                 # blank GFF line
@@ -158,6 +161,25 @@ def test_malformed_inputs_raise_the_python_error(tmp_path, blast, gff):
     with pytest.raises(type(want.value)) as got:
         inputs.load_inputs(*paths, 100, warn=None, native=True)
     assert str(got.value) == str(want.value)
+
+
+def test_ungrouped_blastout_goes_to_the_python_reader(tmp_path):
+    """A contig whose hits come in two runs: the native reader declines, the Python reader
+    keeps every hit in file order with its run number (regroup.py scores it run by run)."""
+    first = BLAST.splitlines(True)[0]
+    paths = _write(tmp_path, FNA, BLAST + first, GFF)
+    with pytest.raises(ingest.Fallback):
+        native_only(paths, 100)
+    b, _ = inputs.load_inputs(*paths, 100, warn=None, native=True)
+    (tmp_path / "g").mkdir()
+    grouped, _ = inputs.load_inputs(*_write(tmp_path / "g", FNA, BLAST, GFF), 100, warn=None,
+                                    native=False)
+    assert b.n_hits == grouped.n_hits + 1 and grouped.hit_group is None
+    c = b.contig_names.index(first.split("\t", 1)[0])
+    h0, h1 = int(b.hit_off[c]), int(b.hit_off[c + 1])
+    assert b.hit_group[h0:h1].tolist() == [0] * (h1 - h0 - 1) + [1]
+    assert int(b.hit_row[h1 - 1]) == len(BLAST.splitlines())
+    assert not b.hit_group[:h0].any() and not b.hit_group[h1:].any()
 
 
 def test_bad_rows_of_unknown_contigs_are_ignored(tmp_path):

@@ -14,6 +14,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import lib as L
+from . import regroup
 
 DIS_ONE = {"report-best": 0, "meld": 1}
 DIS_TWO = {"report-best": 0, "jump": 1, "meld": 2}
@@ -134,6 +135,7 @@ class GpuScorer:
             raise L.WaafleHipError(rc, self.lib.wf_last_error(self.h).decode())
 
     def set_taxonomy(self, tax):
+        self._tables = tax
         self._tax = taxonomy_struct(tax)
         self._check(self.lib.wf_set_taxonomy(self.h, C.byref(self._tax)))
 
@@ -141,7 +143,10 @@ class GpuScorer:
         """wf_score over the batch.  A batch whose hit-locus attachments exceed one call's
         limit (WF_E_TOOBIG: the device's 32-bit work indices, or WF_OPT_ATT_LIMIT) is
         scored in contig halves (contigs are independent, so the records are the same);
-        a failing half reports its contigs relative to this batch."""
+        a failing half reports its contigs relative to this batch.  A batch from an ungrouped
+        blastout (hit_group) is scored as the reference scores it, run by run (regroup.py)."""
+        if getattr(batch, "hit_group", None) is not None:
+            batch = regroup.resolve(batch, self._tables.parent, params, lambda b: self.score(b, params))
         try:
             return self._score_once(batch, params)
         except L.WaafleHipError as err:
@@ -172,7 +177,10 @@ class GpuScorer:
     def score_details(self, batch, params):
         """wf_score with --write-details records on: (Results, {name: numpy array}) with the
         evaluated (contig, level) pairs and the per-level segment records
-        (include/waafle_hip.h wf_details)."""
+        (include/waafle_hip.h wf_details).  Not for an ungrouped blastout: the reference
+        writes a contig's details once per run, from states this call does not keep."""
+        if getattr(batch, "hit_group", None) is not None:
+            raise ValueError("--write-details needs a blastout grouped by query")
         self._check(self.lib.wf_details_enable(self.h, 1))
         try:
             res = self.score(batch, params)

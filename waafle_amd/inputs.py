@@ -7,9 +7,10 @@ orgscorer.py:348-357, 908-946.  Columns are converted in bulk with numpy; any ro
 numpy refuses is re-parsed with the reference's own per-field casts so malformed
 input fails the same way.
 
-One deliberate difference: a contig whose BLAST hits (or GFF loci) appear in two
-separate runs of the file is rejected.  Upstream requires grouped files and would
-silently re-score such a contig from half-updated state.
+A contig whose BLAST hits appear in several separate runs of the file keeps them all, in
+file order, with each hit's run number (`hit_group`): the scorer reproduces the reference's
+evaluation per run (regroup.py).  A contig whose GFF loci appear in two runs is rejected
+(upstream re-numbers the second run's loci over the first's names, orgscorer.py:348-357).
 """
 from __future__ import annotations
 
@@ -58,6 +59,7 @@ class HostBatch:
     annot_values: list = field(default_factory=list)   # per system: list of value strings
     hit_row: np.ndarray = None                         # blastout row of each batch hit
     loci_fields: object = None                         # per contig: LOCI field (native ingest)
+    hit_group: np.ndarray = None                       # per hit: its run of the contig (ungrouped blastout)
 
     @property
     def n_contigs(self):
@@ -95,6 +97,7 @@ class HostBatch:
             annot_value_ids=None if self.annot_value_ids is None else self.annot_value_ids[h0:h1],
             annot_values=self.annot_values,
             hit_row=None if self.hit_row is None else self.hit_row[h0:h1],
+            hit_group=None if self.hit_group is None else self.hit_group[h0:h1],
             loci_fields=None if self.loci_fields is None else _ContigSlice(self.loci_fields, c0, c1))
 
 
@@ -211,7 +214,8 @@ def _columns(rows):
 
 
 def read_hits(path, contig_index, warn=say):
-    """Parse the blastout; returns (per-contig hit row ranges in file order, columns)."""
+    """Parse the blastout; returns (columns, the runs of known contigs in file order:
+    (contig index, row start, row end) -- a contig may have several, utils.py:255-270)."""
     with open(path) as fh:
         rows = list(csv.reader(fh, dialect="excel-tab"))
     for r in rows:
@@ -220,17 +224,12 @@ def read_hits(path, contig_index, warn=say):
     cols, ints, floats = _columns(rows)
     qseqid = cols[0]
     groups = []                       # (contig index, row start, row end)
-    seen = set()
     start = 0
     n = len(rows)
     for i in range(1, n + 1):
         if i == n or qseqid[i] != qseqid[start]:
             name = qseqid[start]
             if name in contig_index:
-                if name in seen:
-                    raise InputError("BLAST hits of contig {!r} are not contiguous "
-                                     "(the blastout must be grouped by query)".format(name))
-                seen.add(name)
                 groups.append((contig_index[name], start, i))
             elif warn:
                 warn("  Unknown contig in <blastout> file", name)
@@ -309,15 +308,22 @@ def _load_python(contigs_path, blastout_path, gff_path, edges, min_gene_length, 
     rows, cols, ints, floats, groups = read_hits(blastout_path, index, warn=warn)
     N = len(names)
 
-    # hits reordered into FASTA contig order (file order within a contig)
+    # hits reordered into FASTA contig order (file order within a contig, a contig's runs
+    # one after another with their run numbers)
     counts = np.zeros(N, dtype=np.int64)
     for ci, a, b in groups:
-        counts[ci] = b - a
+        counts[ci] += b - a
     hit_off = np.zeros(N + 1, dtype=np.int64)
     np.cumsum(counts, out=hit_off[1:])
     order = np.empty(int(hit_off[-1]), dtype=np.int64)
+    run_of = np.zeros(int(hit_off[-1]), dtype=np.int32)
+    fill = hit_off[:-1].copy()
+    nrun = np.zeros(N, dtype=np.int32)
     for ci, a, b in groups:
-        order[hit_off[ci]:hit_off[ci + 1]] = np.arange(a, b)
+        order[fill[ci]:fill[ci] + b - a] = np.arange(a, b)
+        run_of[fill[ci]:fill[ci] + b - a] = nrun[ci]
+        fill[ci] += b - a
+        nrun[ci] += 1
 
     qlen, slen = ints[2][order], ints[3][order]
     qstart, qend = ints[5][order], ints[6][order]
@@ -375,7 +381,8 @@ def _load_python(contigs_path, blastout_path, gff_path, edges, min_gene_length, 
         hit_scov=scov.astype(np.float64), hit_sysmask=sysmask, loc_off=loc_off,
         loc_start=loc_start.astype(np.int32), loc_end=loc_end.astype(np.int32),
         loc_strand=loc_strand, loc_codes=loc_codes, systems=systems,
-        annot_value_ids=value_ids, annot_values=values, hit_row=order)
+        annot_value_ids=value_ids, annot_values=values, hit_row=order,
+        hit_group=run_of if np.any(run_of) else None)
     return batch, tax
 
 

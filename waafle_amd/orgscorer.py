@@ -8,7 +8,7 @@ import os
 import sys
 import time
 
-from . import cli, engine, inputs, lib, output
+from . import cli, engine, inputs, lib, output, regroup
 from . import details as wdetails
 from . import dist as wdist
 
@@ -54,6 +54,9 @@ def main(argv=None):
             # per-level records come from one context (a diagnostic output: one GPU)
             if group is not None or args.gpus != 1:
                 die("--write-details runs on one GPU (--gpus 1, no torch.distributed launch)")
+            if batch.hit_group is not None:
+                die("--write-details needs a blastout grouped by query (the reference writes an "
+                    "ungrouped contig's details once per run)")
             scorer = engine.GpuScorer(0)
             try:
                 scorer.set_taxonomy(tax)
@@ -63,6 +66,17 @@ def main(argv=None):
         elif group is None:
             res = engine.score(batch, tax, cli.param_dict(args), gpus=args.gpus)
         else:
+            if rank == 0 and batch.hit_group is not None:
+                # an ungrouped blastout: the earlier runs' evaluations on rank 0, the ranks
+                # then score the batch of raised clades (regroup.py)
+                scorer = engine.GpuScorer(device)
+                try:
+                    scorer.set_taxonomy(tax)
+                    params = cli.param_dict(args)
+                    batch = regroup.resolve(batch, tax.parent, params, lambda b: scorer.score(b, params))
+                finally:
+                    scorer.close()
+
             def score_shard(sub, stax, a, b):
                 inputs.say("  rank {}: contigs {}..{} ({:,} hits) on device {}".format(
                     rank, a, b, sub.n_hits, device))

@@ -1,0 +1,99 @@
+"""A blastout whose hits of one contig come in several separate runs (not grouped by query).
+
+The reference scores every run as it reads it (orgscorer.py:941-960): `attach_hits` adds the
+run's hits to the contig's site scores -- which earlier evaluations have already rolled up
+(`raise_taxonomy`, :431-445) -- then the jumps (:955-957) and `evaluate_contig` (:566-583)
+run again over the whole state, and the last evaluation is the one reported.  Locus
+annotations carry over (:384-392: the same loci, the same running best score).
+
+The state after an evaluation is a max envelope per clade, and rolling an envelope up is
+the max over its children's, so that state is exactly the hits so far with each hit's
+clade raised by the levels its run has been through: run g's hits enter evaluation e at
+  ancestor^R(taxon),   R = sum over e' = g .. e-1 of (jumps + iterations(e') - 1)
+(an evaluation of i iterations raises i - 1 times; a skipped contig, 0 iterations, none;
+r__Root is its own parent, utils.py:386-387).  So the last evaluation is one ordinary
+wf_score of the contig's whole hit list in file order with those clades, and the counts
+come from scoring the earlier evaluations first -- one wf_score per extra run, over the
+contigs that have it.  `resolve` returns that batch; every hit index (annotations, melds)
+keeps its place in it.
+"""
+import numpy as np
+
+from .lib import WaafleHipError
+
+
+def _ancestors(parent, taxon, raises):
+    """ancestor^raises(taxon), per hit."""
+    out = taxon.astype(np.int32, copy=True)
+    todo = np.nonzero(raises > 0)[0]
+    r = raises[todo]
+    step = 0
+    while len(todo):
+        out[todo] = parent[out[todo]]
+        step += 1
+        keep = r > step
+        todo, r = todo[keep], r[keep]
+    return out
+
+
+def _with_hits(batch, contigs, hit_keep, taxon):
+    """A batch of `contigs` (ascending) holding the hits where hit_keep is set."""
+    from .inputs import HostBatch
+    ho, lo = batch.hit_off, batch.loc_off
+    hit_contig = np.repeat(np.arange(batch.n_contigs), np.diff(ho))
+    in_sel = np.zeros(batch.n_contigs, bool)
+    in_sel[contigs] = True
+    hits = np.nonzero(hit_keep & in_sel[hit_contig])[0]
+    counts = np.bincount(hit_contig[hits], minlength=batch.n_contigs)[contigs]
+    hit_off = np.zeros(len(contigs) + 1, np.int64)
+    np.cumsum(counts, out=hit_off[1:])
+    loc_idx = np.concatenate([np.arange(lo[c], lo[c + 1]) for c in contigs]) if len(contigs) else \
+        np.zeros(0, np.int64)
+    loc_off = np.zeros(len(contigs) + 1, np.int64)
+    np.cumsum(np.diff(lo)[contigs], out=loc_off[1:])
+    loc_idx = loc_idx.astype(np.int64)
+    return HostBatch(
+        contig_names=[batch.contig_names[c] for c in contigs],
+        contig_lengths=batch.contig_lengths[contigs], hit_off=hit_off,
+        hit_qlo=batch.hit_qlo[hits], hit_qhi=batch.hit_qhi[hits], hit_taxon=taxon[hits],
+        hit_strand=batch.hit_strand[hits], hit_score=batch.hit_score[hits],
+        hit_scov=batch.hit_scov[hits], hit_sysmask=batch.hit_sysmask[hits], loc_off=loc_off,
+        loc_start=batch.loc_start[loc_idx], loc_end=batch.loc_end[loc_idx],
+        loc_strand=batch.loc_strand[loc_idx], loc_codes=[batch.loc_codes[i] for i in loc_idx],
+        systems=batch.systems,
+        annot_value_ids=None if batch.annot_value_ids is None else batch.annot_value_ids[hits],
+        annot_values=batch.annot_values)
+
+
+def resolve(batch, parent, params, score_fn):
+    """-> the batch to score for the reference's records of an ungrouped blastout: each
+    hit's clade raised as above (`batch` itself when every contig's hits are one run).
+    parent: the taxonomy's parent array (TaxonomyTables.parent); score_fn(batch) -> Results
+    (one wf_score).  A failure of an earlier evaluation (e.g. WF_E_RUNAWAY: the reference
+    dies there too) is raised with its contigs relative to `batch`."""
+    g = getattr(batch, "hit_group", None)
+    if g is None or batch.n_hits == 0 or not np.any(g):
+        return batch
+    import dataclasses
+    N = batch.n_contigs
+    hit_contig = np.repeat(np.arange(N), np.diff(batch.hit_off))
+    runs = np.zeros(N, np.int64)
+    np.maximum.at(runs, hit_contig, g.astype(np.int64) + 1)
+    jumps = int((params.get("jump_taxonomy") if isinstance(params, dict) else 0) or 0)
+    raises = np.zeros(batch.n_hits, np.int64)
+    for k in range(1, int(runs.max())):
+        # evaluation k of the contigs with more than k runs: their runs 0 .. k-1
+        sel = np.nonzero(runs > k)[0]
+        sub = _with_hits(batch, sel, g < k, _ancestors(parent, batch.hit_taxon, raises))
+        try:
+            res = score_fn(sub)
+        except WaafleHipError as err:
+            bad = getattr(err, "contigs", None)
+            if bad is not None and len(bad):
+                err.contigs = sel[np.asarray(bad)]
+            raise
+        per = np.zeros(N, np.int64)
+        per[sel] = jumps + np.maximum(res.iterations.astype(np.int64) - 1, 0)
+        raises += np.where(g < k, per[hit_contig], 0)
+    return dataclasses.replace(batch, hit_taxon=_ancestors(parent, batch.hit_taxon, raises),
+                               hit_group=None)
