@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define WF_INGEST_ABI_VERSION 2
+#define WF_INGEST_ABI_VERSION 3
 
 enum wf_ingest_status {
   WF_INGEST_OK = 0,
@@ -80,6 +80,11 @@ typedef struct wf_ingest_view {
   /* per contig: the LOCI output field, the kept loci's codes "start:end:strand" joined by
      '|' (orgscorer.py:795-800), [n_contigs + 1] offsets */
   const char* loci_blob; const int64_t* loci_off;
+  /* a blastout not grouped by contig (ABI 3): per hit, its run of the contig's consecutive
+     rows (0, 1, ...; hits stay in file order within a contig), or NULL when every contig's
+     hits are one run.  The reference evaluates such a contig once per run
+     (waafle_orgscorer.py:941-960); waafle_amd/regroup.py does the same over wf_score */
+  const int32_t* hit_group;
 } wf_ingest_view;
 
 int wf_ingest_abi_version(void);

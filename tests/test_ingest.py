@@ -32,6 +32,9 @@ def assert_same(a, b):
     bn, tn, wn = a
     bp, tp, wp = b
     assert wn == wp
+    assert (bn.hit_group is None) == (bp.hit_group is None)
+    if bn.hit_group is not None:
+        assert np.array_equal(bn.hit_group, bp.hit_group)
     assert tn.names == tp.names
     assert bn.contig_names == bp.contig_names
     for f in ARRAYS:
@@ -54,11 +57,7 @@ def test_golden_inputs_native_equals_python(name, tmp_path):
     fx = gc.load(name)
     paths = gc.materialize(fx, tmp_path)
     args = cli.parse_flags(fx["flags"])
-    if name.startswith("ungrouped_"):                   # the Python reader's input
-        with pytest.raises(ingest.Fallback):
-            native_only(paths, args.min_gene_length)
-    else:
-        native_only(paths, args.min_gene_length)      # takes the native path (no fallback)
+    native_only(paths, args.min_gene_length)          # takes the native path (no fallback)
     a, b = both(paths, args.min_gene_length)
     assert_same(a, b)
 
@@ -163,14 +162,15 @@ def test_malformed_inputs_raise_the_python_error(tmp_path, blast, gff):
     assert str(got.value) == str(want.value)
 
 
-def test_ungrouped_blastout_goes_to_the_python_reader(tmp_path):
-    """A contig whose hits come in two runs: the native reader declines, the Python reader
-    keeps every hit in file order with its run number (regroup.py scores it run by run)."""
+@pytest.mark.parametrize("native", [True, False])
+def test_ungrouped_blastout_keeps_every_run(tmp_path, native):
+    """A contig whose hits come in two runs: both readers keep every hit in file order with
+    its run number (regroup.py scores it run by run)."""
     first = BLAST.splitlines(True)[0]
     paths = _write(tmp_path, FNA, BLAST + first, GFF)
-    with pytest.raises(ingest.Fallback):
-        native_only(paths, 100)
-    b, _ = inputs.load_inputs(*paths, 100, warn=None, native=True)
+    if native:
+        native_only(paths, 100)                           # (no fallback)
+    b, _ = inputs.load_inputs(*paths, 100, warn=None, native=native)
     (tmp_path / "g").mkdir()
     grouped, _ = inputs.load_inputs(*_write(tmp_path / "g", FNA, BLAST, GFF), 100, warn=None,
                                     native=False)
@@ -210,3 +210,27 @@ def test_dense_short_annotations_match(tmp_path):
     a, b = both(paths, 100)
     assert_same(a, b)
     assert a[0].systems == ["", "a"]
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_ungrouped_runs_across_chunks_native_equals_python(tmp_path, threads):
+    """Runs of one contig in separate parts of a large file (several parse chunks), some
+    split by a chunk boundary: the same hits, order and run numbers from both readers."""
+    data = synth.generate(n=200, genes=6, clades=40, seed=17)
+    paths = synth.write_text(data, str(tmp_path))
+    lines = open(paths[1]).read().splitlines(True)
+    by = {}
+    for ln in lines:
+        by.setdefault(ln.split("\t", 1)[0], []).append(ln)
+    rounds = [[], [], []]
+    for i, rows in enumerate(by.values()):
+        k = 1 + i % 3
+        for r in range(k):
+            rounds[r].append(rows[r::k])
+    with open(paths[1], "w") as fh:
+        for rnd in rounds:
+            for run in rnd:
+                fh.writelines(run)
+    a, b = both(paths, 200.0, threads=threads)
+    assert_same(a, b)
+    assert a[0].hit_group is not None and int(a[0].hit_group.max()) == 2

@@ -550,6 +550,7 @@ struct wf_ingest {
   // hits
   std::vector<int64_t> hit_off;
   PodArray<int64_t> hit_row;
+  PodArray<int32_t> hit_group;          // run of its contig per hit (allocated only when a contig has several)
   PodArray<int32_t> hit_qlo, hit_qhi, hit_taxon, hit_value;
   PodArray<int8_t> hit_strand;
   PodArray<double> hit_score, hit_scov;
@@ -807,9 +808,12 @@ bool parse_blast(const Mapped& m, wf_ingest& I, const std::unordered_map<sv, int
 
   // groups of consecutive qseqid (utils.py:262-266) -> FASTA contigs: the chunks' runs in
   // file order, a run continuing the previous chunk's last qseqid joining its group
-  struct Piece { int32_t contig; int32_t chunk; int64_t r0, r1; };   // rows [r0, r1) of a chunk
+  // rows [r0, r1) of a chunk; run: the contig's run number (a blastout not grouped by contig
+  // keeps every run, in file order -- the caller scores it run by run, regroup.py)
+  struct Piece { int32_t contig; int32_t chunk; int64_t r0, r1; int32_t run; };
   std::vector<Piece> runs;
-  std::vector<char> seen((size_t)N, 0);
+  std::vector<int32_t> nrun((size_t)N, 0);
+  bool regrouped = false;
   I.warn_blast_off.assign(1, 0);
   std::vector<int64_t> chunk_base((size_t)T + 1, 0);
   sv prev;
@@ -818,20 +822,21 @@ bool parse_blast(const Mapped& m, wf_ingest& I, const std::unordered_map<sv, int
     chunk_base[t + 1] = chunk_base[t] + (int64_t)ck[t].rows.size();
     for (const QRun& r : ck[t].runs) {
       if (have && r.q == prev) {                     // (only a chunk's first run can continue)
-        runs.push_back(Piece{runs.back().contig, t, r.r0, r.r1});
+        runs.push_back(Piece{runs.back().contig, t, r.r0, r.r1, runs.back().run});
         continue;
       }
       have = true;
       prev = r.q;
       auto it = index.find(r.q);
       const int32_t c = it == index.end() ? -1 : it->second;
+      int32_t run = 0;
       if (c < 0) {
         push_str(I.warn_blast_blob, I.warn_blast_off, r.q);
       } else {
-        if (seen[c]) { I.err = "BLAST hits of a contig are not contiguous"; return false; }
-        seen[c] = 1;
+        run = nrun[c]++;
+        regrouped |= run > 0;
       }
-      runs.push_back(Piece{c, t, r.r0, r.r1});
+      runs.push_back(Piece{c, t, r.r0, r.r1, run});
     }
   }
   std::vector<int64_t> counts((size_t)N, 0);
@@ -930,6 +935,7 @@ bool parse_blast(const Mapped& m, wf_ingest& I, const std::unordered_map<sv, int
   I.hit_qlo.alloc((size_t)H); I.hit_qhi.alloc((size_t)H); I.hit_taxon.alloc((size_t)H);
   I.hit_strand.alloc((size_t)H); I.hit_score.alloc((size_t)H); I.hit_scov.alloc((size_t)H);
   I.hit_sysmask.alloc((size_t)H); I.hit_row.alloc((size_t)H);
+  if (regrouped) I.hit_group.alloc((size_t)H);
   const int S = std::max(1, (int)I.n_systems);
   I.hit_value.alloc((size_t)H * S);
   parallel_for(threads, (int64_t)runs.size(), [&](int64_t k, int) {
@@ -949,6 +955,7 @@ bool parse_blast(const Mapped& m, wf_ingest& I, const std::unordered_map<sv, int
       I.hit_scov[o] = r.scov;
       I.hit_score[o] = r.score;
       I.hit_row[o] = chunk_base[g.chunk] + i;
+      if (regrouped) I.hit_group[o] = g.run;
       int32_t* hv = &I.hit_value[(size_t)o * S];
       for (int b = 0; b < S; ++b) hv[b] = -1;
       uint32_t mask = 0;
@@ -1023,6 +1030,7 @@ int wf_ingest_get_view(const wf_ingest* ing, wf_ingest_view* v) {
   v->hit_score = I.hit_score.data(); v->hit_scov = I.hit_scov.data();
   v->hit_sysmask = I.hit_sysmask.data(); v->hit_row = I.hit_row.data();
   v->hit_value = I.hit_value.data();
+  v->hit_group = I.hit_group.data();
   v->taxa_blob = I.taxa_blob.data(); v->taxa_off = I.taxa_off.data();
   v->system_blob = I.system_blob.data(); v->system_off = I.system_off.data();
   v->value_blob = I.value_blob.data(); v->value_off = I.value_off.data();

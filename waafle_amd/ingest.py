@@ -35,7 +35,7 @@ class WfIngestView(C.Structure):
                 ("loc_strand_blob", _P), ("loc_strand_off", _P),
                 ("warn_gff_blob", _P), ("warn_gff_off", _P),
                 ("warn_blast_blob", _P), ("warn_blast_off", _P),
-                ("loci_blob", _P), ("loci_off", _P)]
+                ("loci_blob", _P), ("loci_off", _P), ("hit_group", _P)]
 
 
 class IngestError(RuntimeError):
@@ -65,7 +65,7 @@ def load(path=LIB_PATH):
     so.wf_ingest_parse.restype = C.c_int
     so.wf_ingest_get_view.argtypes = [_P, C.POINTER(WfIngestView)]
     so.wf_ingest_get_view.restype = C.c_int
-    if so.wf_ingest_abi_version() != 2:
+    if so.wf_ingest_abi_version() != 3:
         raise IngestError("libwaafle_ingest.so ABI mismatch")
     _lib = so
     return so
@@ -235,7 +235,8 @@ def parse(contigs_path, blastout_path, gff_path, edges, min_gene_length, threads
             loc_codes=LociCodes(loc_start, loc_end, strands), systems=systems,
             annot_value_ids=value_ids, annot_values=[values] * len(systems),
             hit_row=_arr(v.hit_row, H, np.int64, owner),
-            loci_fields=_table(v.loci_blob, v.loci_off, N, owner))
+            loci_fields=_table(v.loci_blob, v.loci_off, N, owner),
+            hit_group=_arr(v.hit_group, H, np.int32, owner) if v.hit_group else None)
         return batch, tax
     except BaseException:
         owner.__del__()
