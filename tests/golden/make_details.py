@@ -7,7 +7,7 @@ the details file in text mode, which is the only change: upstream raises on Pyth
 when write_details() prints to the binary GzipFile.  Each fixture holds the case's input
 recipe, its flags and the reference's details TSV text.
 
-    python tests/golden/make_details.py
+    python tests/golden/make_details.py [ungrouped]     (ungrouped: only those cases)
 """
 import gzip
 import json
@@ -33,6 +33,9 @@ SYNTH = [("syn_small", dict(n=120, genes=6, clades=24, seed=11, lgt_frac=0.3, de
           [[], ["--weak-loci", "assign-unknown"], ["--weak-loci", "penalize"]]),
          ("syn_short", dict(n=80, genes=8, clades=60, seed=7, short_frac=0.25, decoys=8),
           [[], ["--min-gene-length", "100"]])]
+# the blastout of tests/golden/make_ungrouped.py (a contig's hits in 1-3 separate runs: the
+# reference writes a contig's rows once per run, each time it evaluates it)
+UNGROUPED = [[], ["--jump-taxonomy", "1"], ["--weak-loci", "penalize"]]
 
 
 def run(inputs, flags, outdir):
@@ -53,7 +56,16 @@ def save(name, flags, recipe, text):
 
 
 def main():
+    only_ungrouped = sys.argv[1:] == ["ungrouped"]
     with tempfile.TemporaryDirectory() as tmp:
+        d = os.path.join(HERE, "ungrouped_inputs")
+        inputs = [os.path.join(d, "ungrouped" + e) for e in (".fna", ".blastout", ".gff", ".taxonomy.tsv")]
+        for flags in UNGROUPED:
+            name = "ungrouped_{}".format(flag_tag(flags))
+            save(name, flags, dict(kind="files", dir="ungrouped_inputs", stem="ungrouped"),
+                 run(inputs, flags, os.path.join(tmp, name)))
+        if only_ungrouped:
+            return
         for kind, flags in CASES:
             name = "demo_{}_{}".format(kind, flag_tag(flags))
             inputs = [os.path.join(DEMO, r) for r in DEMO_INPUTS[kind]]

@@ -35,7 +35,20 @@ def _field(s):
 
 
 def render(batch, tax, params, det):
-    """Rows (lists of 5 strings) in the reference's order."""
+    """Rows (lists of 5 strings) in the reference's order.  det: one wf_score's records, or
+    {"parts": [(batch, records), ...]} for an ungrouped blastout (engine.score_details):
+    each evaluation's rows at the blastout row where the reference makes it."""
+    if "parts" in det:
+        keyed = []
+        for b, d in det["parts"]:
+            keyed.extend(_render_keyed(b, tax, params, d))
+        keyed.sort(key=lambda kr: kr[0])
+        return [r for _, rows in keyed for r in rows]
+    return [r for _, rows in _render_keyed(batch, tax, params, det) for r in rows]
+
+
+def _render_keyed(batch, tax, params, det):
+    """[(order key, rows of one contig's evaluation)], in key order."""
     N = batch.n_contigs
     hit_off = np.asarray(batch.hit_off)
     loc_off = np.asarray(batch.loc_off)
@@ -45,6 +58,8 @@ def render(batch, tax, params, det):
         first_row[has_rows] = np.asarray(batch.hit_row)[hit_off[:-1][has_rows]]
     else:
         first_row[has_rows] = hit_off[:-1][has_rows]
+    if getattr(batch, "eval_key", None) is not None:
+        first_row = np.asarray(batch.eval_key, dtype=np.int64)
     unknown = int(tax.unknown)
     weak = params["weak_loci"]                       # cli.param_dict keys
     assign_unknown = weak == "assign-unknown"
@@ -89,7 +104,7 @@ def render(batch, tax, params, det):
                         _field("|".join(sp.get(g, MISSING) for g in range(G)))])
         return out, scores
 
-    rows = []
+    keyed = []
     for c in sorted(np.nonzero(has_rows)[0].tolist(), key=lambda x: first_row[x]):
         G = int(loc_off[c + 1] - loc_off[c])
         if G == 0 or c not in evals:
@@ -103,10 +118,11 @@ def render(batch, tax, params, det):
                     top = np.maximum(top, row)
             if not np.any(top >= kmin):
                 continue                      # every locus ignored: not evaluated
-        rows.extend(first)
+        rows = list(first)
         for lv in levels[1:]:
             rows.extend(level_rows(c, lv, G)[0])
-    return rows
+        keyed.append((int(first_row[c]), rows))
+    return keyed
 
 
 def write(rows, outdir, basename):

@@ -177,10 +177,21 @@ class GpuScorer:
     def score_details(self, batch, params):
         """wf_score with --write-details records on: (Results, {name: numpy array}) with the
         evaluated (contig, level) pairs and the per-level segment records
-        (include/waafle_hip.h wf_details).  Not for an ungrouped blastout: the reference
-        writes a contig's details once per run, from states this call does not keep."""
+        (include/waafle_hip.h wf_details).  An ungrouped blastout (hit_group): the reference
+        writes a contig's details at each of its evaluations, so the records come as
+        {"parts": [(batch, records), ...]}, one per wf_score of regroup.resolve, each batch
+        with its eval_key (details.render orders the rows by it)."""
         if getattr(batch, "hit_group", None) is not None:
-            raise ValueError("--write-details needs a blastout grouped by query")
+            parts = []
+
+            def one(b):
+                res, det = self.score_details(b, params)
+                parts.append((b, det))
+                return res
+
+            final = regroup.resolve(batch, self._tables.parent, params, one)
+            res = one(final)
+            return res, {"parts": parts}
         self._check(self.lib.wf_details_enable(self.h, 1))
         try:
             res = self.score(batch, params)

@@ -54,9 +54,6 @@ def main(argv=None):
             # per-level records come from one context (a diagnostic output: one GPU)
             if group is not None or args.gpus != 1:
                 die("--write-details runs on one GPU (--gpus 1, no torch.distributed launch)")
-            if batch.hit_group is not None:
-                die("--write-details needs a blastout grouped by query (the reference writes an "
-                    "ungrouped contig's details once per run)")
             scorer = engine.GpuScorer(0)
             try:
                 scorer.set_taxonomy(tax)

@@ -62,7 +62,23 @@ def _with_hits(batch, contigs, hit_keep, taxon):
         loc_strand=batch.loc_strand[loc_idx], loc_codes=[batch.loc_codes[i] for i in loc_idx],
         systems=batch.systems,
         annot_value_ids=None if batch.annot_value_ids is None else batch.annot_value_ids[hits],
-        annot_values=batch.annot_values)
+        annot_values=batch.annot_values,
+        hit_row=None if batch.hit_row is None else batch.hit_row[hits])
+
+
+def _run_rows(batch, hit_contig, run):
+    """Per contig: the blastout row that starts its run number `run` (per contig), or of its
+    last run when run[c] < 0 -- the point in the file where the reference evaluates it (and
+    writes its --write-details rows)."""
+    g = batch.hit_group
+    last = np.zeros(batch.n_contigs, np.int64)
+    np.maximum.at(last, hit_contig, g.astype(np.int64))
+    want = np.where(run < 0, last, run)
+    rows = batch.hit_row if batch.hit_row is not None else np.arange(batch.n_hits)
+    key = np.full(batch.n_contigs, np.iinfo(np.int64).max, np.int64)
+    first = np.nonzero(g == want[hit_contig])[0]
+    np.minimum.at(key, hit_contig[first], np.asarray(rows)[first].astype(np.int64))
+    return key
 
 
 def resolve(batch, parent, params, score_fn):
@@ -70,7 +86,9 @@ def resolve(batch, parent, params, score_fn):
     hit's clade raised as above (`batch` itself when every contig's hits are one run).
     parent: the taxonomy's parent array (TaxonomyTables.parent); score_fn(batch) -> Results
     (one wf_score).  A failure of an earlier evaluation (e.g. WF_E_RUNAWAY: the reference
-    dies there too) is raised with its contigs relative to `batch`."""
+    dies there too) is raised with its contigs relative to `batch`.  Each batch scored and
+    the one returned carry `eval_key`: per contig, the blastout row where the reference
+    evaluates it (the start of the run it has just read), the order of --write-details rows."""
     g = getattr(batch, "hit_group", None)
     if g is None or batch.n_hits == 0 or not np.any(g):
         return batch
@@ -85,6 +103,7 @@ def resolve(batch, parent, params, score_fn):
         # evaluation k of the contigs with more than k runs: their runs 0 .. k-1
         sel = np.nonzero(runs > k)[0]
         sub = _with_hits(batch, sel, g < k, _ancestors(parent, batch.hit_taxon, raises))
+        sub.eval_key = _run_rows(batch, hit_contig, np.full(N, k - 1))[sel]
         try:
             res = score_fn(sub)
         except WaafleHipError as err:
@@ -95,5 +114,7 @@ def resolve(batch, parent, params, score_fn):
         per = np.zeros(N, np.int64)
         per[sel] = jumps + np.maximum(res.iterations.astype(np.int64) - 1, 0)
         raises += np.where(g < k, per[hit_contig], 0)
-    return dataclasses.replace(batch, hit_taxon=_ancestors(parent, batch.hit_taxon, raises),
-                               hit_group=None)
+    out = dataclasses.replace(batch, hit_taxon=_ancestors(parent, batch.hit_taxon, raises),
+                              hit_group=None)
+    out.eval_key = _run_rows(batch, hit_contig, np.full(N, -1))
+    return out
