@@ -119,8 +119,11 @@ def test_regroup_raises_each_run_by_the_levels_it_has_been_through():
         hit_group=np.array([0, 0, 1, 2, 0, 1], np.int32))    # contig a: runs 0,0,1,2; b: 0,1
     calls = []
 
+    keys = []
+
     def score_fn(sub):
         calls.append((sub.n_contigs, sub.hit_off.tolist(), sub.hit_taxon.tolist()))
+        keys.append(sub.eval_key.tolist())
         res = Results.empty(sub.n_contigs, sub.n_hits, sub.n_loci, 0)
         res.iterations[:] = [3, 1][:sub.n_contigs] if len(calls) == 1 else [2]
         return res
@@ -131,4 +134,7 @@ def test_regroup_raises_each_run_by_the_levels_it_has_been_through():
     assert calls[1] == (1, [0, 3], [6, 6, 9])           # run 0 raised 1 + 2 = 3 levels
     # contig 0: run 0 raised 3 + (1 + 1) = 5, run 1 raised 2, run 2 none; contig 1: run 0 1
     assert out.hit_taxon.tolist() == [4, 4, 7, 9, 8, 9]
+    # where the reference evaluates (and writes --write-details rows): the first row of the
+    # run just read -- evaluation 1 at run 0, evaluation 2 at run 1, the last at the last run
+    assert keys == [[0, 4], [2]] and out.eval_key.tolist() == [3, 5]
     assert out.hit_group is None and b.hit_group is not None
