@@ -169,3 +169,29 @@ def test_other_errors_do_not_split():
     with pytest.raises(L.WaafleHipError):
         s.score(batch, None)
     assert calls == [10]                       # the code decides, not the message text
+
+
+def test_cli_two_ranks_rank0_parse_failure_ends_every_rank(tmp_path):
+    """A parse failure on rank 0 (the only rank that reads the inputs) reaches every rank
+    before the scatter (dist.share_error): both ranks exit "EXITING.", rank 0 with the
+    reference's LETHAL ERROR line, and no rank waits in a recv.  CPU only (gloo)."""
+    import subprocess
+    import sys
+    import golden_cases as gc
+    paths = gc.materialize(gc.load("tie_default"), tmp_path)
+    bad = tmp_path / "bad.blastout"
+    bad.write_text("contig_1\tnot-enough-columns\n")
+    out = tmp_path / "out"
+    out.mkdir()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CUDA_VISIBLE_DEVICES="",
+               HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "waafle_amd.orgscorer", paths[0], str(bad), paths[2], paths[3],
+           "--outdir", str(out)]
+    run = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), env=env)
+    assert run.returncode != 0
+    assert run.stderr.count("LETHAL ERROR") == 1, run.stderr[-2000:]
+    assert run.stderr.count("EXITING.") >= 2, run.stderr[-2000:]
+    assert "Connection closed" not in run.stderr and "Gloo" not in run.stderr.split("LETHAL")[0]

@@ -138,3 +138,74 @@ def test_regroup_raises_each_run_by_the_levels_it_has_been_through():
     # run just read -- evaluation 1 at run 0, evaluation 2 at run 1, the last at the last run
     assert keys == [[0, 4], [2]] and out.eval_key.tolist() == [3, 5]
     assert out.hit_group is None and b.hit_group is not None
+
+
+def _chain_batch(hit_group, jumps_taxon=9):
+    z = np.zeros(len(hit_group), np.int32)
+    H = len(hit_group)
+    return inputs.HostBatch(
+        contig_names=["a"], contig_lengths=np.array([900]), hit_off=np.array([0, H]),
+        hit_qlo=z + 1, hit_qhi=z + 300, hit_taxon=z + jumps_taxon, hit_strand=z.astype(np.int8),
+        hit_score=np.ones(H), hit_scov=np.ones(H), hit_sysmask=z.astype(np.uint32),
+        loc_off=np.array([0, 1]), loc_start=np.array([1], np.int32),
+        loc_end=np.array([300], np.int32), loc_strand=np.zeros(1, np.int8),
+        loc_codes=["1:300:+"], hit_group=np.asarray(hit_group, np.int32))
+
+
+def test_regroup_negative_jump_makes_no_jumps():
+    """--jump-taxonomy -1 on a split blastout: range(-1) is empty upstream (orgscorer.py:
+    955-957), so each evaluation raises by iterations - 1 only (wf_api.cpp clamps the same)."""
+    from waafle_amd import regroup
+    from waafle_amd.engine import Results
+    parent = np.array([0, 0, 1, 2, 3, 4, 5, 6, 7, 8], dtype=np.int32)
+
+    def score_fn(sub):
+        res = Results.empty(sub.n_contigs, sub.n_hits, sub.n_loci, 0)
+        res.iterations[:] = 2
+        return res
+    for j in (-1, -5, 0):
+        out = regroup.resolve(_chain_batch([0, 1, 2]), parent, {"jump_taxonomy": j}, score_fn)
+        assert out.hit_taxon.tolist() == [7, 8, 9], j
+
+
+def test_regroup_all_zero_groups_and_details_do_not_recurse():
+    """hit_group present but all zero (one run per contig, e.g. after HostBatch.slice):
+    resolve returns the batch without hit_group, so score_details' second call ends."""
+    from waafle_amd import regroup
+    b = _chain_batch([0, 0, 0])
+    out = regroup.resolve(b, np.zeros(10, np.int32), {}, lambda s: 1 / 0)
+    assert out.hit_group is None and out.hit_taxon.tolist() == [9, 9, 9]
+    assert regroup.resolve(out, np.zeros(10, np.int32), {}, lambda s: 1 / 0) is out
+
+
+def test_regroup_one_run_per_hit_costs_only_the_split_contig():
+    """A blastout sorted by subject can give one contig one run per hit: evaluation k then
+    touches only the contigs with more than k runs, not every hit of the batch."""
+    import time
+    from waafle_amd import regroup
+    from waafle_amd.engine import Results
+    R, other = 400, 200_000                       # one contig of 400 runs, one of 200 k hits
+    H = R + other
+    z = np.zeros(H, np.int32)
+    g = np.concatenate([np.arange(R), np.zeros(other)]).astype(np.int32)
+    b = inputs.HostBatch(
+        contig_names=["a", "b"], contig_lengths=np.array([900, 900]), hit_off=np.array([0, R, H]),
+        hit_qlo=z + 1, hit_qhi=z + 300, hit_taxon=z + 9, hit_strand=z.astype(np.int8),
+        hit_score=np.ones(H), hit_scov=np.ones(H), hit_sysmask=z.astype(np.uint32),
+        loc_off=np.array([0, 1, 2]), loc_start=np.array([1, 1], np.int32),
+        loc_end=np.array([300, 300], np.int32), loc_strand=np.zeros(2, np.int8),
+        loc_codes=["1:300:+"] * 2, hit_group=g)
+    parent = np.array([0, 0, 1, 2, 3, 4, 5, 6, 7, 8], dtype=np.int32)
+    seen = []
+
+    def score_fn(sub):
+        seen.append(sub.n_hits)
+        res = Results.empty(sub.n_contigs, sub.n_hits, sub.n_loci, 0)
+        res.iterations[:] = 1
+        return res
+    t0 = time.perf_counter()
+    out = regroup.resolve(b, parent, {"jump_taxonomy": 0}, score_fn)
+    dt = time.perf_counter() - t0
+    assert seen == list(range(1, R))              # evaluation k: contig a's first k hits
+    assert out.hit_taxon.tolist() == [9] * H
+    assert dt < 5.0, dt                           # O(runs x the split contig), not O(runs x H)

@@ -48,6 +48,22 @@ def rank_bounds(cost, world):
     return [(cuts[k], cuts[k + 1]) for k in range(world)]
 
 
+def share_error(err, dist, group=None):
+    """Rank 0's error (an exception, or None) on every rank: a status word, then the
+    exception itself.  Every rank calls it before the scatter, so a parse or regroup failure
+    on rank 0 ends every rank the same way instead of leaving the others in a recv."""
+    if dist is None:
+        return err
+    import torch
+    status = torch.tensor([0 if err is None else 1], dtype=torch.int64)
+    dist.broadcast(status, 0, group=group)
+    if not status.item():
+        return None
+    box = [err if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(box, 0, group=group)
+    return box[0]
+
+
 def max_over_ranks(value, dist, device=None):
     """MAX of a float over all ranks (the bench's elapsed time)."""
     if dist is None:

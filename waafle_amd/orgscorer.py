@@ -34,15 +34,23 @@ def main(argv=None):
     device = int(dmap.split(",")[local]) if dmap else local
     t0 = time.time()
     batch = tax = None
+    load_err = None
     if rank == 0:
         say("Loading inputs.")
         try:
             batch, tax = inputs.load_inputs(args.contigs, args.blastout, args.gff, args.taxonomy,
                                             args.min_gene_length, warn=inputs.say)
         except (inputs.InputError, ValueError) as exc:
-            if group is not None:
-                group.destroy_process_group()
-            die(str(exc))
+            load_err = exc
+    if group is not None:                  # every rank learns of rank 0's failure first
+        load_err = wdist.share_error(load_err, group)
+    if load_err is not None:
+        if group is not None:
+            group.destroy_process_group()
+        if rank == 0:
+            die(str(load_err))
+        sys.exit("EXITING.")
+    if rank == 0:
         if args.basename is None:
             args.basename = inputs.basename_of(args.contigs)
         say("Analyzing {:,} contigs ({:,} hits, {:,} loci) on {} GPU(s).".format(
@@ -63,16 +71,23 @@ def main(argv=None):
         elif group is None:
             res = engine.score(batch, tax, cli.param_dict(args), gpus=args.gpus)
         else:
+            pre_err = None
             if rank == 0 and batch.hit_group is not None:
                 # an ungrouped blastout: the earlier runs' evaluations on rank 0, the ranks
                 # then score the batch of raised clades (regroup.py)
-                scorer = engine.GpuScorer(device)
                 try:
-                    scorer.set_taxonomy(tax)
-                    params = cli.param_dict(args)
-                    batch = regroup.resolve(batch, tax.parent, params, lambda b: scorer.score(b, params))
-                finally:
-                    scorer.close()
+                    scorer = engine.GpuScorer(device)
+                    try:
+                        scorer.set_taxonomy(tax)
+                        params = cli.param_dict(args)
+                        batch = regroup.resolve(batch, tax.parent, params, lambda b: scorer.score(b, params))
+                    finally:
+                        scorer.close()
+                except lib.WaafleHipError as exc:
+                    pre_err = exc
+            pre_err = wdist.share_error(pre_err, group)
+            if pre_err is not None:
+                raise pre_err
 
             def score_shard(sub, stax, a, b):
                 inputs.say("  rank {}: contigs {}..{} ({:,} hits) on device {}".format(

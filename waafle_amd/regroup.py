@@ -36,26 +36,34 @@ def _ancestors(parent, taxon, raises):
     return out
 
 
-def _with_hits(batch, contigs, hit_keep, taxon):
-    """A batch of `contigs` (ascending) holding the hits where hit_keep is set."""
+def _ranges(a, b):
+    """Concatenated [a[i], b[i]) index ranges (int64)."""
+    a = np.asarray(a, np.int64)
+    n = np.asarray(b, np.int64) - a
+    tot = int(n.sum())
+    if tot == 0:
+        return np.zeros(0, np.int64)
+    start = np.zeros(len(n), np.int64)
+    np.cumsum(n[:-1], out=start[1:])
+    return np.repeat(a - start, n) + np.arange(tot, dtype=np.int64)
+
+
+def _with_hits(batch, contigs, hits, taxon):
+    """A batch of `contigs` (ascending) holding the hits `hits` (ascending batch indices, all
+    of them hits of those contigs) with clades `taxon` (one per entry of `hits`)."""
     from .inputs import HostBatch
-    ho, lo = batch.hit_off, batch.loc_off
-    hit_contig = np.repeat(np.arange(batch.n_contigs), np.diff(ho))
-    in_sel = np.zeros(batch.n_contigs, bool)
-    in_sel[contigs] = True
-    hits = np.nonzero(hit_keep & in_sel[hit_contig])[0]
-    counts = np.bincount(hit_contig[hits], minlength=batch.n_contigs)[contigs]
+    lo = batch.loc_off
+    pos = np.searchsorted(contigs, np.searchsorted(batch.hit_off, hits, side="right") - 1)
+    counts = np.bincount(pos, minlength=len(contigs))
     hit_off = np.zeros(len(contigs) + 1, np.int64)
     np.cumsum(counts, out=hit_off[1:])
-    loc_idx = np.concatenate([np.arange(lo[c], lo[c + 1]) for c in contigs]) if len(contigs) else \
-        np.zeros(0, np.int64)
+    loc_idx = _ranges(lo[contigs], lo[contigs + 1])
     loc_off = np.zeros(len(contigs) + 1, np.int64)
     np.cumsum(np.diff(lo)[contigs], out=loc_off[1:])
-    loc_idx = loc_idx.astype(np.int64)
     return HostBatch(
         contig_names=[batch.contig_names[c] for c in contigs],
         contig_lengths=batch.contig_lengths[contigs], hit_off=hit_off,
-        hit_qlo=batch.hit_qlo[hits], hit_qhi=batch.hit_qhi[hits], hit_taxon=taxon[hits],
+        hit_qlo=batch.hit_qlo[hits], hit_qhi=batch.hit_qhi[hits], hit_taxon=taxon,
         hit_strand=batch.hit_strand[hits], hit_score=batch.hit_score[hits],
         hit_scov=batch.hit_scov[hits], hit_sysmask=batch.hit_sysmask[hits], loc_off=loc_off,
         loc_start=batch.loc_start[loc_idx], loc_end=batch.loc_end[loc_idx],
@@ -66,44 +74,54 @@ def _with_hits(batch, contigs, hit_keep, taxon):
         hit_row=None if batch.hit_row is None else batch.hit_row[hits])
 
 
-def _run_rows(batch, hit_contig, run):
-    """Per contig: the blastout row that starts its run number `run` (per contig), or of its
-    last run when run[c] < 0 -- the point in the file where the reference evaluates it (and
-    writes its --write-details rows)."""
-    g = batch.hit_group
-    last = np.zeros(batch.n_contigs, np.int64)
-    np.maximum.at(last, hit_contig, g.astype(np.int64))
-    want = np.where(run < 0, last, run)
-    rows = batch.hit_row if batch.hit_row is not None else np.arange(batch.n_hits)
-    key = np.full(batch.n_contigs, np.iinfo(np.int64).max, np.int64)
-    first = np.nonzero(g == want[hit_contig])[0]
-    np.minimum.at(key, hit_contig[first], np.asarray(rows)[first].astype(np.int64))
+def _run_rows(batch, hits, pos, n, want):
+    """Per contig (positions 0..n-1; `pos[i]` is the contig of batch hit `hits[i]`): the
+    blastout row that starts its run number want[contig] -- the point in the file where the
+    reference evaluates it (and writes its --write-details rows)."""
+    g = batch.hit_group[hits]
+    rows = batch.hit_row[hits] if batch.hit_row is not None else hits
+    key = np.full(n, np.iinfo(np.int64).max, np.int64)
+    first = np.nonzero(g == want[pos])[0]
+    np.minimum.at(key, pos[first], np.asarray(rows)[first].astype(np.int64))
     return key
 
 
 def resolve(batch, parent, params, score_fn):
     """-> the batch to score for the reference's records of an ungrouped blastout: each
-    hit's clade raised as above (`batch` itself when every contig's hits are one run).
-    parent: the taxonomy's parent array (TaxonomyTables.parent); score_fn(batch) -> Results
-    (one wf_score).  A failure of an earlier evaluation (e.g. WF_E_RUNAWAY: the reference
-    dies there too) is raised with its contigs relative to `batch`.  Each batch scored and
-    the one returned carry `eval_key`: per contig, the blastout row where the reference
-    evaluates it (the start of the run it has just read), the order of --write-details rows."""
-    g = getattr(batch, "hit_group", None)
-    if g is None or batch.n_hits == 0 or not np.any(g):
-        return batch
+    hit's clade raised as above (`batch` with hit_group dropped when every contig's hits are
+    one run).  parent: the taxonomy's parent array (TaxonomyTables.parent); score_fn(batch)
+    -> Results (one wf_score).  A failure of an earlier evaluation (e.g. WF_E_RUNAWAY: the
+    reference dies there too) is raised with its contigs relative to `batch`.  Each batch
+    scored and the one returned carry `eval_key`: per contig, the blastout row where the
+    reference evaluates it (the start of the run it has just read), the order of
+    --write-details rows.  Evaluation k touches only the hits of the contigs with more than k
+    runs (the reference re-evaluates only the contig whose run it has just read)."""
     import dataclasses
+    g = getattr(batch, "hit_group", None)
+    if g is None:
+        return batch
+    if batch.n_hits == 0 or not np.any(g):
+        return dataclasses.replace(batch, hit_group=None)
     N = batch.n_contigs
     hit_contig = np.repeat(np.arange(N), np.diff(batch.hit_off))
     runs = np.zeros(N, np.int64)
     np.maximum.at(runs, hit_contig, g.astype(np.int64) + 1)
-    jumps = int((params.get("jump_taxonomy") if isinstance(params, dict) else 0) or 0)
+    # (a negative --jump-taxonomy makes no jumps: range(negative), orgscorer.py:955-957)
+    jumps = max(0, int((params.get("jump_taxonomy") if isinstance(params, dict) else 0) or 0))
     raises = np.zeros(batch.n_hits, np.int64)
+    # the contigs of several runs, and their hits (batch indices, ascending)
+    multi = np.nonzero(runs > 1)[0]
+    mhits = _ranges(batch.hit_off[multi], batch.hit_off[multi + 1])
+    mpos = np.repeat(np.arange(len(multi)), np.diff(batch.hit_off)[multi])
     for k in range(1, int(runs.max())):
         # evaluation k of the contigs with more than k runs: their runs 0 .. k-1
-        sel = np.nonzero(runs > k)[0]
-        sub = _with_hits(batch, sel, g < k, _ancestors(parent, batch.hit_taxon, raises))
-        sub.eval_key = _run_rows(batch, hit_contig, np.full(N, k - 1))[sel]
+        keep = runs[multi] > k
+        multi, mhits, mpos = multi[keep], mhits[keep[mpos]], np.cumsum(keep)[mpos[keep[mpos]]] - 1
+        sel = multi
+        seen = g[mhits] < k
+        hits = mhits[seen]
+        sub = _with_hits(batch, sel, hits, _ancestors(parent, batch.hit_taxon[hits], raises[hits]))
+        sub.eval_key = _run_rows(batch, mhits, mpos, len(sel), np.full(len(sel), k - 1))
         try:
             res = score_fn(sub)
         except WaafleHipError as err:
@@ -111,10 +129,11 @@ def resolve(batch, parent, params, score_fn):
             if bad is not None and len(bad):
                 err.contigs = sel[np.asarray(bad)]
             raise
-        per = np.zeros(N, np.int64)
-        per[sel] = jumps + np.maximum(res.iterations.astype(np.int64) - 1, 0)
-        raises += np.where(g < k, per[hit_contig], 0)
+        per = jumps + np.maximum(res.iterations.astype(np.int64) - 1, 0)
+        raises[hits] += per[mpos[seen]]
     out = dataclasses.replace(batch, hit_taxon=_ancestors(parent, batch.hit_taxon, raises),
                               hit_group=None)
-    out.eval_key = _run_rows(batch, hit_contig, np.full(N, -1))
+    last = np.zeros(N, np.int64)
+    np.maximum.at(last, hit_contig, g.astype(np.int64))
+    out.eval_key = _run_rows(batch, np.arange(batch.n_hits), hit_contig, N, last)
     return out
