@@ -82,6 +82,9 @@ def parse_args():
                          "rehearsal of the N > 1 branch on one GPU, not a scaling number)")
     ap.add_argument("--weak", type=int, default=1,
                     help="N > 1: also time the weak-scaling workload (every rank its own n contigs)")
+    ap.add_argument("--shares", default="2,4,8",
+                    help="N = 1: time every rank's strong-scaling share of the workload at these "
+                         "N on this one GPU (`strong_share_projection`); '' disables")
     ap.add_argument("--traffic-json", default=None)
     ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r05", "cfg4_valu.json"),
                     help="PMC VALU counts of the main pass (scripts/pmc_main.py, optional)")
@@ -404,6 +407,42 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
     return out
 
 
+def share_projection(so, h, chk, batch, params, ns, steps, warmup, dev, t_full):
+    """The strong-scaling shares of this workload timed one at a time on this GPU: for each N,
+    every rank's contig range [r n / N, (r + 1) n / N) (exactly what bench.py --gpus N gives
+    rank r) as its own device-resident batch, W + K passes as the main line.  The path has no
+    collective, so an N-GPU pass is the slowest share's pass (plus the barrier): projected
+    value = n / that time, projected efficiency = t(n) / (N t(slowest share)).  What it leaves
+    out: host-side contention of N processes, and the per-device clocks."""
+    import torch
+    N = batch.n_contigs
+    out = {"rule": "each of the N contiguous shares timed alone on this GPU (W untimed + K "
+                   "timed passes, HIP-event phases); projected N-GPU time = the slowest share; "
+                   "efficiency = t(whole) / (N x t(slowest share))",
+           "t_whole_ms": t_full * 1e3, "per_n": {}}
+    for n in ns:
+        rows = []
+        for r in range(n):
+            a, b = r * N // n, (r + 1) * N // n
+            db = DeviceBatch(batch.slice(a, b), dev)
+            el, tm = timed_passes(so, h, chk, db, params, steps, warmup, None, dev)
+            del db
+            torch.cuda.empty_cache()
+            ph = {k: v[0] / max(1, tm.passes) for k, v in tm.phases().items() if v[0] > 0.0}
+            rows.append({"rank": r, "contigs": b - a, "ms_per_pass": el / steps * 1e3,
+                         "phases_ms": {k: round(v, 4) for k, v in ph.items()},
+                         "dispatch_ms": tm.pass_ms / max(1, tm.passes)})
+        slow = max(rows, key=lambda x: x["ms_per_pass"])
+        t = slow["ms_per_pass"] * 1e-3
+        out["per_n"][str(n)] = {
+            "contigs_per_gpu": slow["contigs"], "ms_slowest_share": t * 1e3,
+            "ms_mean_share": float(np.mean([x["ms_per_pass"] for x in rows])),
+            "projected_value": N / t, "projected_efficiency": t_full / (n * t),
+            "slowest_rank": slow["rank"], "slowest_phases_ms": slow["phases_ms"],
+            "shares_ms": [round(x["ms_per_pass"], 4) for x in rows]}
+    return out
+
+
 def wdist_max(x, dist, dev):
     from waafle_amd import dist as wdist
     return wdist.max_over_ranks(x, dist, dev)
@@ -510,6 +549,11 @@ def main():
                 "workload": "every rank its own {} contigs ([r n, (r + 1) n) of one {}-contig "
                             "stream), same flags, same timing".format(n_cfg, world * n_cfg)}
         del wbatch
+    projection = None
+    if world == 1 and args.shares:
+        projection = share_projection(so, h, chk, batch, params,
+                                      [int(x) for x in args.shares.split(",") if x],
+                                      args.steps, args.warmup, dev, elapsed / args.steps)
     pairs = float(pe.sum())
     k2_counts = k2_algorithmic(pe, batch)
     if dist:          # whole-job counts
@@ -605,6 +649,7 @@ def main():
                    "parallelism": "dp{} (contig ranges [r n/N, (r+1) n/N), no data-path "
                                   "collective)".format(world)},
         "weak": weak,
+        "strong_share_projection": projection,
         "k2_pair_evals_per_sec": None,
         "k2_pair_evals_note": "reference-equivalent count: sum of P_pot(P_pot-1)/2 over "
                               "explain_two calls (orgscorer.py:606-608 score(c1,c2) calls), "

@@ -188,3 +188,24 @@ def test_ungrouped_blastout_cli_one_and_two_ranks(tmp_path):
         b = engine.score(batch, tax, params, gpus=2, devices=[0, 0])
         for f in ("call", "crit", "rank", "clade1", "clade2", "iterations", "annot_hit"):
             assert np.array_equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_bench_one_gpu_share_projection(tmp_path):
+    """bench.py at N = 1 times every strong-scaling share of the workload alone on the GPU
+    (`strong_share_projection`): N shares per N covering the contigs, projected value = the
+    contigs / the slowest share's pass, efficiency = t(whole) / (N x slowest share)."""
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
+           "--contigs", "20000", "--k2-contigs", "0", "--cpu-sample", "0", "--e2e=", "--pcie", "0",
+           "--shares", "2,4"]
+    run = subprocess.run(cmd, capture_output=True, text=True, timeout=420, cwd=REPO)
+    assert run.returncode == 0, run.stderr[-3000:]
+    d = json.loads([l for l in run.stdout.splitlines() if l.startswith("{")][0])
+    p = d["strong_share_projection"]
+    assert abs(p["t_whole_ms"] - d["ms_per_step"]) <= 1e-6 * d["ms_per_step"]
+    for n in (2, 4):
+        q = p["per_n"][str(n)]
+        assert len(q["shares_ms"]) == n and q["contigs_per_gpu"] in (20000 // n, 20000 // n + 1)
+        t = max(q["shares_ms"])
+        assert q["ms_slowest_share"] == pytest.approx(t, rel=1e-3)
+        assert q["projected_value"] == pytest.approx(20000 / (t * 1e-3), rel=1e-3)
+        assert q["projected_efficiency"] == pytest.approx(d["ms_per_step"] / (n * t), rel=1e-3)

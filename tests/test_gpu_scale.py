@@ -207,6 +207,33 @@ def test_cfg4_full_size(cfg4_full):
     assert_same(slice_results(a, batch, c0, c0 + 200), want, sub)
 
 
+def test_cfg3_full_size():
+    """BASELINE config 3 at full size (100,000 contigs x 12 genes x 1,000 clades, 25 M hits,
+    the full taxonomy roll-up): no contig errors, deterministic, equal in the staged form
+    (which evaluates every segment mean) and from four cost-balanced shards, and equal to the
+    oracle on a 300-contig sample (contigs are independent)."""
+    batch, tax = synth.generate_batch("cfg3")
+    assert batch.n_contigs == 100_000
+    s = engine.GpuScorer(0)
+    s.set_taxonomy(tax)
+    a = s.score(batch, PARAMS)
+    assert not a.status.any()
+    assert (a.call == 2).sum() > 0 and (a.call == 1).sum() > 0 and (a.iterations > 2).sum() > 0
+    assert_same(s.score(batch, PARAMS), a, batch)
+    bounds = engine.shard_bounds(engine.contig_cost(batch), 4)
+    parts = [s.score(batch.slice(x, y), PARAMS) for x, y in bounds]
+    s.close()
+    assert len(parts) == 4
+    assert_same(engine.Results.concat(parts, [int(batch.hit_off[x]) for x, _ in bounds]), a, batch)
+    staged = score(batch, tax, mode="staged")
+    assert not staged.status.any()
+    assert_same(staged, a, batch)
+    k = 3                                            # 300 contigs of chunk 3
+    sub, want = oracle_chunk_sample("cfg3", k, 300, tax)
+    c0 = k * synth.chunk_size("cfg3")
+    assert_same(slice_results(a, batch, c0, c0 + 300), want, sub)
+
+
 def test_cfg5_shard_and_embedded_fixture(tmp_path):
     """The cfg5 per-GPU share at 8 GPUs (6,250 stress contigs, ~31 M hits, 5,000 clades):
     equal to its two halves and to the all-segment-table staged form; the reference-generated

@@ -17,6 +17,7 @@ SOURCES = [os.path.join(CSRC, "wf_staged.hip"), os.path.join(CSRC, "wf_fast.hip"
            os.path.join(CSRC, "wf_api.cpp")]
 DEPS = SOURCES + [os.path.join(CSRC, "wf_internal.h"), os.path.join(CSRC, "wf_device.h"),
                   os.path.join(CSRC, "wf_sparse.h"), os.path.join(CSRC, "wf_lanes.h"),
+                  os.path.join(CSRC, "wf_stamps.h"),
                   os.path.join(REPO, "include", "waafle_hip.h")]
 
 # -ffp-contract=off: no a*b+c fusion anywhere, so float64 results match numpy bit-for-bit.

@@ -13,10 +13,6 @@
 #include "waafle_hip.h"
 #include "wf_lanes.h"
 
-#ifndef WF_DPP_DEVICE
-#define WF_DPP_DEVICE 0     // 1: cross-lane ops of the shared device code by DPP (A/B variant)
-#endif
-
 namespace wf {
 
 namespace {
@@ -24,42 +20,7 @@ namespace {
 
 constexpr uint64_t kKeyPad = ~0ull;
 
-// Diagnostic build only (-DWF_STAMPS): thread 0 accumulates shader-clock deltas per phase,
-// always taken right after a workgroup barrier.  Never compiled into the product build.
-#ifdef WF_STAMPS
-__device__ unsigned long long g_stamps[32];
-__shared__ unsigned long long g_tlast;   // thread 0's last stamp (workgroup-local)
-#define STAMP_INIT() do { if (threadIdx.x == 0) g_tlast = __builtin_amdgcn_s_memtime(); } while (0)
-#define STAMP(i)                                                                    \
-  do {                                                                              \
-    if (threadIdx.x == 0) {                                                         \
-      unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
-      atomicAdd(&g_stamps[i], now_ - g_tlast);                                      \
-      g_tlast = now_;                                                               \
-    }                                                                               \
-  } while (0)
-#define STAMP_SYNC() __syncthreads()
-// wave-0 lap timer inside a phase (no barrier): cycles since the last LAP_MARK/LAP
-#define LAP_MARK() unsigned long long lap_ = __builtin_amdgcn_s_memtime()
-#define LAP(i)                                                                      \
-  do {                                                                              \
-    unsigned long long n_ = __builtin_amdgcn_s_memtime();                           \
-    if (threadIdx.x == 0) atomicAdd(&g_stamps[i], n_ - lap_);                       \
-    lap_ = n_;                                                                      \
-  } while (0)
-#define LAP_WAIT_LDS() __builtin_amdgcn_s_waitcnt(0xc07f)
-#define LAP_WAIT_V(v) asm volatile("" ::"v"(v))
-#define STAT(i, v) do { if (threadIdx.x == 0) atomicAdd(&g_stamps[i], (unsigned long long)(v)); } while (0)
-#else
-#define STAMP_INIT() do {} while (0)
-#define STAMP(i) do {} while (0)
-#define STAMP_SYNC() do {} while (0)
-#define LAP_MARK() do {} while (0)
-#define LAP(i) do {} while (0)
-#define LAP_WAIT_LDS() do {} while (0)
-#define LAP_WAIT_V(v) do {} while (0)
-#define STAT(i, v) do {} while (0)
-#endif
+#include "wf_stamps.h"
 constexpr int kLocVirtual = 0xFFFF;     // locus field of the virtual "Unknown" key
 
 struct Ctl {
@@ -116,17 +77,12 @@ __device__ __forceinline__ const T& kernarg_fresh(const T& arg) {
 template <int NT>
 __device__ __forceinline__ int block_scan(int v, int* total, Ctl& ctl) {
   const int lane = lane_id(), w = wave_id();
-#if WF_DPP_DEVICE
-  int wt;
-  int x = wave_excl_scan_dpp(v, &wt) + v;             // inclusive, within the wave
-#else
   int x = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     int y = __shfl_up(x, d, 64);
     if (lane >= d) x += y;
   }
-#endif
   if (lane == 63) ctl.red_i[w] = x;
   __syncthreads();
   int base = 0, tot = 0;
@@ -145,17 +101,12 @@ __device__ __forceinline__ int block_scan(int v, int* total, Ctl& ctl) {
 template <int NT>
 __device__ __forceinline__ void block_scan2(int v1, int v2, int* p1, int* p2, int* t1, int* t2, Ctl& ctl) {
   const int lane = lane_id(), w = wave_id();
-#if WF_DPP_DEVICE
-  int w1, w2;
-  int x = wave_excl_scan_dpp(v1, &w1) + v1, y = wave_excl_scan_dpp(v2, &w2) + v2;   // inclusive
-#else
   int x = v1, y = v2;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     int a = __shfl_up(x, d, 64), b = __shfl_up(y, d, 64);
     if (lane >= d) { x += a; y += b; }
   }
-#endif
   if (lane == 63) { ctl.red_i[w] = x; ctl.red_j[w] = y; }
   __syncthreads();
   int b1 = 0, b2 = 0, s1 = 0, s2 = 0;
@@ -181,20 +132,12 @@ __device__ __forceinline__ bool better(double r2, long long k2, double r, long l
 
 template <int NT>
 __device__ __forceinline__ void block_argmax(double& r, long long& k, Ctl& ctl) {
-#if WF_DPP_DEVICE
-  each_stride([&](auto J) {
-    const double r2 = xor_lanes<decltype(J)::value>(r);
-    const long long k2 = xor_lanes<decltype(J)::value>(k);
-    if (better(r2, k2, r, k)) { r = r2; k = k2; }
-  });
-#else
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     double r2 = __shfl_xor(r, off, 64);
     long long k2 = __shfl_xor(k, off, 64);
     if (better(r2, k2, r, k)) { r = r2; k = k2; }
   }
-#endif
   if (lane_id() == 0) { ctl.red_r[wave_id()] = r; ctl.red_k[wave_id()] = k; }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -267,15 +210,11 @@ __device__ __forceinline__ int block_lca(const KArgs& K, const int* list, int m,
   if (wave_id() == 0) {
     int acc = -1;
     for (int i = lane_id(); i < m; i += 64) acc = lca2(K, acc, list[i]);
-#if WF_DPP_DEVICE
-    each_stride([&](auto J) { acc = lca2(K, acc, xor_lanes<decltype(J)::value>(acc)); });
-#else
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       int o = __shfl_xor(acc, off, 64);
       acc = lca2(K, acc, o);
     }
-#endif
     if (lane_id() == 0) ctl.lca_out = acc;
   }
   __syncthreads();
@@ -924,14 +863,6 @@ __device__ __forceinline__ double wave_seg_mean(LT lt, int nl, int len, int lo, 
       if (lo > x) nb = lo;
       else if (hi > x) nb = hi;
     }
-#if WF_DPP_DEVICE
-    each_stride([&](auto J) {
-      const double v2 = xor_lanes<decltype(J)::value>(v);
-      const int n2 = xor_lanes<decltype(J)::value>(nb);
-      v = v2 > v ? v2 : v;
-      nb = n2 < nb ? n2 : nb;
-    });
-#else
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       const double v2 = __shfl_xor(v, off, 64);
@@ -939,7 +870,6 @@ __device__ __forceinline__ double wave_seg_mean(LT lt, int nl, int len, int lo, 
       v = v2 > v ? v2 : v;
       nb = n2 < nb ? n2 : nb;
     }
-#endif
     if (v > 0.0) {
       if (lane == 0) { W.r_lo[nr] = x; W.r_hi[nr] = nb; W.r_v[nr] = v; }
       ++nr;
@@ -991,11 +921,7 @@ __device__ __forceinline__ double wave_seg_mean(LT lt, int nl, int len, int lo, 
     mean = (0.0 + stk.s0) / (double)len;
   }
   wave_sync();                                      // W is reused by the next segment
-#if WF_DPP_DEVICE
-  return lane_bcast(mean, 0);
-#else
   return __shfl(mean, 0, 64);
-#endif
 }
 
 constexpr int kRegAtt = 4;   // attachments of a segment held in registers

@@ -31,59 +31,6 @@
 #include "wf_device.h"
 #include "wf_lanes.h"
 
-// WF_SKIP (diagnostic variants only, never the product build): 1 skips the segment means,
-// 2 the sort, 4 explain_one, 8 everything after the attachments, 16 explain_two (FULL),
-// 32 the roll-up (FULL) -- per-phase cost by
-// difference of kernel times (no contig is handed on, the results are not meaningful).
-#ifndef WF_SKIP
-#define WF_SKIP 0
-#endif
-#ifndef WF_LANE_MEANS6
-#define WF_LANE_MEANS6 0
-#endif
-// 1: every hit batch of a round finds its loci before the first takes its slots (the loci
-// searches of the batches overlap); 0: batch by batch.  Same-box A/B at cfg4 (r4c): 0 is
-// 0.15 ms faster per pass (the batched form's registers spill), so 0 is the default.
-// resident waves per SIMD of the roll-up launches: 4 (128 VGPRs, some spilled) beat 3 (168,
-// none) by 0.35 ms of roll-up per cfg4 pass on one box (r4f: their few contigs per wave
-// want occupancy more than registers)
-// hand-over: only candidate-pair members' rows evaluated whole (1), or every potential
-// clade's (0)
-#ifndef WF_E2_MEMBERS
-#define WF_E2_MEMBERS 1
-#endif
-// ... and pass-4 segments surely above every threshold left unevaluated (1)
-#ifndef WF_E2_LB
-#define WF_E2_LB 1
-#endif
-// unmasked loci settled by lower bounds where the hand-over is the compact table (1)
-#ifndef WF_UM_LB
-#define WF_UM_LB 1
-#endif
-#ifndef WF_ROLL_WAVES
-#define WF_ROLL_WAVES 4
-#endif
-// level 0: 1 moves ranges and scores into sorted order with the keys (as the roll-up
-// launches do); 0 (default) sorts the keys alone.  Same box, alternating (r4w): level-0
-// launch 9.19 / 9.25 ms keys alone against 9.25 / 9.26 moved.
-#ifndef WF_L0_PERMUTE
-#define WF_L0_PERMUTE 0
-#endif
-// roll-up launches: 1 keeps attachments in descending-score order (rank_slice, SegAttT's
-// early exits); 0 (default): sorted-order data as level 0.  Same-box A/B at cfg4 (r4j):
-// 16.04 / 16.09 ms with, 16.05 without -- the extra sort eats what the early exits save.
-#ifndef WF_ROLL_DESC
-#define WF_ROLL_DESC 0
-#endif
-// roll-up levels: multi-attachment segment means one numpy leaf per lane (flat_leaf_means);
-// 0: one segment per lane (lane_seg_mean)
-#ifndef WF_FLAT_LEAVES
-#define WF_FLAT_LEAVES 1
-#endif
-#ifndef WF_ATTACH_BATCHED
-#define WF_ATTACH_BATCHED 0
-#endif
-
 namespace wf {
 
 namespace {
@@ -99,35 +46,12 @@ constexpr int kMultiAtt0 = 32;       // ... so at most 32 attachments (2 * 32 - 
 constexpr int kRunsL0 = 32;          // the level-0 form: 16 attachments (a 10 KB slice:
 constexpr int kMultiAttL0 = 16;      // 16 waves per CU, see WaveSmem)
 constexpr int kXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
-#ifndef WF_XCD_MAP
-#define WF_XCD_MAP 1
-#endif
-// Diagnostic build only (-DWF_STAMPS): per-phase shader-clock laps of the first form on
-// every 16th contig, plus counters (scripts/wave_stamps.py reads them).  Never in the
-// product build.
-#ifndef WF_STAMPS_ROLL
-#define WF_STAMPS_ROLL 0             // stamps of the roll-up launches instead of level 0
-#endif
-#ifdef WF_STAMPS
-__device__ unsigned long long g_wstamps[48];
-#define WLAP_MARK() unsigned long long wlap_ = __builtin_amdgcn_s_memtime(); const bool wsamp_ = !FULL && (WF_STAMPS_ROLL ? ROLL : !ROLL) && (c & 15) == 0
-#define WLAP(i)                                                                     \
-  do {                                                                              \
-    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
-    if (wsamp_ && lane == 0) atomicAdd(&g_wstamps[i], n_ - wlap_);                  \
-    wlap_ = n_;                                                                     \
-  } while (0)
-#define WSTAT(i, v) do { if (wsamp_ && lane == 0) atomicAdd(&g_wstamps[i], (unsigned long long)(v)); } while (0)
-#else
-#define WLAP_MARK() do {} while (0)
-#define WLAP(i) do {} while (0)
-#define WSTAT(i, v) do {} while (0)
-#endif
+// resident waves per SIMD of the roll-up launches: 4 (128 VGPRs, some spilled) beat 3 (168,
+// none) by 0.35 ms of roll-up per cfg4 pass on one box (r4f: their few contigs per wave
+// want occupancy more than registers; again r5u: 3 waves +0.45 ms)
+constexpr int kRollWaves = 4;
 constexpr int kPot0 = 64;            // potential clades of an in-slice explain_two ...
-#ifndef WF_KS0
-#define WF_KS0 640
-#endif
-constexpr int kS0 = WF_KS0;          // ... and their score rows (potential clades x loci;
+constexpr int kS0 = 640;          // ... and their score rows (potential clades x loci;
                                      // 640 = 64 x 10 and a 20 KB slice: 8 waves per CU)
 
 // One wave's LDS slice.  `scr` is reused phase by phase (offsets in the accessors):
@@ -179,10 +103,8 @@ struct WaveSmem {
   __device__ uint8_t* best_syn() { return reinterpret_cast<uint8_t*>(ign() + 192); }    // [64]
 };
 
-#if WF_KS0 == 640
 static_assert(sizeof(WaveSmem<224, false>) <= 160 * 1024 / 16, "level-0 slice: 16 waves per CU");
 static_assert(sizeof(WaveSmem<256, true>) <= 160 * 1024 / 8, "FULL slice: 8 waves per CU");
-#endif
 
 __device__ __forceinline__ int leaves_for(const SArgs& S, int len) {
   return (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
@@ -248,9 +170,7 @@ __device__ __forceinline__ void wave_sort(T (&x)[R]) {
 // key -> slot hop: the loads of a segment's attachments issue together).  Nothing reads
 // the insertion order after the first sort (F.hit / F.sm: annotation pass 2, before it).
 //
-// PERMUTE = false (the roll-up launches): keys only.  Their slot fields are then data
-// positions in descending-score order (rank_slice), so within each segment the sorted
-// attachments come best first (SegAttT's kDesc early exits).
+// PERMUTE = false (level 0): keys only, attachments reached through the keys' slot fields.
 template <int R, bool PERMUTE = true, class SM>
 __device__ __forceinline__ void sort_slice(SM& F, int n_att) {
   const int lane = lane_id();
@@ -297,47 +217,6 @@ __device__ __forceinline__ void sort_slice(SM& F, int n_att) {
   wave_sync();
 }
 
-// The roll-up launches' data order: attachments moved to positions of descending score
-// (one 32-bit bitonic sort: the complemented top 23 score bits (desc_tb) over the insertion
-// slot), and each key's slot field set to its attachment's new position.  Keys stay
-// unsorted (the level's sort_slice<R, false> sorts them); F.hit / F.sm are not used past
-// this point.
-template <int R, class SM>
-__device__ __forceinline__ void rank_slice(SM& F, int n_att) {
-  const int lane = lane_id();
-  uint32_t y[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int t = R * lane + r;
-    y[r] = t < n_att ? ((((1u << 23) - 1u - (uint32_t)desc_tb(F.sc[t])) << 9) | (uint32_t)t) : ~0u;
-  }
-  wave_sort<R>(y);
-  uint32_t kk[R], lh[R];
-  double sv[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int t = R * lane + r;
-    kk[r] = 0u; lh[r] = 0u; sv[r] = 0.0;
-    if (t < n_att) {
-      const int slot = (int)(y[r] & kSlotMask);
-      kk[r] = F.key[slot];
-      lh[r] = F.lohi[slot];
-      sv[r] = F.sc[slot];
-    }
-  }
-  wave_sync();
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int t = R * lane + r;
-    if (t < n_att) {
-      F.key[t] = (kk[r] & ~kSlotMask) | (uint32_t)t;
-      F.lohi[t] = lh[r];
-      F.sc[t] = sv[r];
-    }
-  }
-  wave_sync();
-}
-
 // Segment s: (clade, locus) and its sorted attachment range [seg_first(s), seg_first(s+1)).
 template <class SM>
 __device__ __forceinline__ int2 cg_of(SM& F, int s) {
@@ -365,19 +244,6 @@ struct SliceSrc {
 // Level 0 without the data move: sorted position t -> its key's slot field -> range, score.
 struct SliceSrcKey {
   [[maybe_unused]] static constexpr bool kDesc = false;
-  const uint32_t* key;
-  const uint32_t* lohi;
-  const double* sc;
-  __device__ __forceinline__ int idx(int t) const { return (int)(key[t] & kSlotMask); }
-  __device__ __forceinline__ void att(int a, int& l, int& h, double& v) const {
-    const uint32_t w = lohi[a];
-    l = lo16(w); h = hi16(w); v = sc[a];
-  }
-};
-// The roll-up launches' attachments (rank_slice): sorted position t -> its key's slot field
-// -> range, score; a segment's attachments come in descending score order.
-struct SliceSrcDesc {
-  [[maybe_unused]] static constexpr bool kDesc = true;
   const uint32_t* key;
   const uint32_t* lohi;
   const double* sc;
@@ -559,13 +425,8 @@ __device__ __forceinline__ int wave_run_score(SM& F, const double* v, int t, int
 // Contig whose rows are the potential clades first, then the others).  Returns kDecDone
 // (written), kDecStop, kDecRaise, or -1 when the state does not fit (staged path).
 // eval_two inlined into wave_two: out of line, every call spilled the caller's live VGPRs
-// to scratch (cfg4: the FULL form 8.56 -> 8.35 ms inlined); WF_EVAL_OUTLINE: the old form
-#ifdef WF_EVAL_OUTLINE
-#define WF_EVAL_ATTR __noinline__
-#else
-#define WF_EVAL_ATTR __forceinline__
-#endif
-__device__ WF_EVAL_ATTR OptEval eval_two_call(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
+// to scratch (cfg4: the FULL form 8.56 -> 8.35 ms inlined)
+__device__ __forceinline__ OptEval eval_two_call(const KArgs& K, const Contig& C, int Pcount, int pa, int pb,
                                               const uint8_t* best, uint8_t* out) {
   return eval_two(K, C, Pcount, pa, pb, best, out);
 }
@@ -796,7 +657,7 @@ template <int CAP, bool FULL, bool ROLL = false>
 // offset 0.  ROLL (first form only): roll-up level start_level > 0 of the contigs in `list`
 // (the wave levels, S.anc set) -- its own instantiation, so profiles tell the level-0 pass
 // from the roll-up passes and level 0 carries none of their code.
-__global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
+__global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? kRollWaves : 4)) void k_wave(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves, int32_t* pend,
                                              const int32_t* list, int n_list, const int64_t* n_dev, int rollup,
                                              int start_level_arg) {
   static_assert(!(FULL && ROLL), "the roll-up passes are first-form launches");
@@ -810,7 +671,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
   // fields of 8 neighbours (1-8 B each, one array per field) share cache lines that 8 L2s
   // write back partially.  Instead XCD x's j-th workgroup takes contig (8 k + x) * B + j at
   // step k (B = grid / 8): each XCD walks runs of B consecutive contigs.
-  const bool xmap = WF_XCD_MAP && gridDim.x % kXcds == 0;
+  const bool xmap = gridDim.x % kXcds == 0;
   const int xb = (int)gridDim.x / kXcds, xj = (int)blockIdx.x / kXcds, xx = (int)blockIdx.x % kXcds;
   for (int it = 0;; ++it) {
     int ci;
@@ -916,59 +777,26 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
     int n_att = 0;
     long long nl_sum = 0;
     // kHB batches of 64 hits per round: every field of all of them is loaded up front (one
-    // global round trip per round instead of one per batch).  Each batch's loci are found
-    // first, for all batches at once (independent LDS reads in flight together; the loci
-    // are ascending and disjoint); then the batches take their slots in order, each picking
-    // its fields from the round's registers by a uniform select
+    // global round trip per round instead of one per batch); the batches take their slots in
+    // order, each picking its fields from the round's registers by a uniform select.  (Finding
+    // every batch's loci before the first takes its slots spilled: 0.15 ms slower, r4c.)
     for (int64_t hq = h0; hq < h1; hq += 64 * kHB) {
       if (hq != h0) load_round(hq);
-      int r_n[kHB];
-      uint64_t r_am[kHB];
-      if (WF_ATTACH_BATCHED && ordered) {
-#pragma unroll
-        for (int b = 0; b < kHB; ++b) {
-          int n = 0;
-          uint64_t am = 0;
-          if (hq + 64 * b + lane < h1 && r_scv[b] >= P.min_scov) {
-            const int qlo = r_qlo[b], qhi = r_qhi[b];
-            int g = 0;                               // first locus ending at or after qlo
-#pragma unroll
-            for (int k = 32; k > 0; k >>= 1) {
-              const int i = min(g + k, Gs) - 1;
-              if (g + k <= Gs && F.lo[i] + F.len[i] - 1 < qlo) g += k;
-            }
-            for (; g < Gs; ++g) {
-              const int lo = F.lo[g], len = F.len[g];
-              if (lo > qhi) break;
-              if (attaches(P, qlo, qhi, r_hs[b], lo, len, F.st[g])) {
-                ++n;
-                nl_sum += len < kNpyBuf ? F.nl1[g] : leaves_for(S, len);
-                am |= 1ull << g;
-              }
-            }
-          }
-          r_n[b] = n;
-          r_am[b] = am;
-          if (ROLL && n > 0) r_cl[b] = S.anc[r_cl[b]];   // parent^(jump + level), :431-445
-        }
-      }
     for (int bq = 0; bq < kHB && hq + 64 * bq < h1; ++bq) {
       const int64_t hb = hq + 64 * bq;
       const int64_t h = hb + lane;
       int qlo = r_qlo[0], qhi = r_qhi[0], hs = r_hs[0], clade = r_cl[0];
       double scv = r_scv[0], sc = r_sc[0];
       uint32_t m = r_m[0];
-      const bool pre = WF_ATTACH_BATCHED && ordered;   // (found above)
-      int n = pre ? r_n[0] : 0;
-      uint64_t am = pre ? r_am[0] : 0ull;
+      int n = 0;
+      uint64_t am = 0ull;
 #pragma unroll
       for (int b = 1; b < kHB; ++b)
         if (bq == b) {
           qlo = r_qlo[b]; qhi = r_qhi[b]; hs = r_hs[b]; clade = r_cl[b];
           scv = r_scv[b]; sc = r_sc[b]; m = r_m[b];
-          if (pre) { n = r_n[b]; am = r_am[b]; }
         }
-      if (!pre && ordered && h < h1 && scv >= P.min_scov) {
+      if (ordered && h < h1 && scv >= P.min_scov) {
         int g = 0;                                   // first locus ending at or after qlo
 #pragma unroll
         for (int k = 32; k > 0; k >>= 1) {
@@ -1057,17 +885,15 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
     pair_evals = lane_bcast((uint64_t)pair_evals, 0);
     bool seed = false;                                 // raised at level 0: staged level 1 seed
     bool dumped = false;                               // segment table handed to k_dump_sparse
-    // roll-up launches: attachments at descending-score positions (rank_slice), addressed
-    // through their keys' slot fields from here on; level 0 sorts them into key order
-    constexpr bool kDescOrder = ROLL && WF_ROLL_DESC;
-    // level 0 (WF_L0_PERMUTE 0): keys sorted alone, attachments reached through the keys'
-    // slot fields (its few multi-attachment segments do not repay moving the data)
-    constexpr bool kKeyOrder = !kDescOrder && !FULL && !ROLL && !WF_L0_PERMUTE;
-    using Src = typename std::conditional<kDescOrder, SliceSrcDesc,
-                                          typename std::conditional<kKeyOrder, SliceSrcKey, SliceSrc>::type>::type;
-    if (kDescOrder && !staged && n_att > 0) rank_slice<(CAP + 63) / 64>(F, n_att);
-    auto slot_at = [&](int t) -> int { return (kDescOrder || kKeyOrder) ? (int)(F.key[t] & kSlotMask) : t; };
-    for (int level = start_level; !staged && G > 0 && h1 > h0 && !(WF_SKIP & 8); ++level) {   // else: never evaluated (:959)
+    // level 0: keys sorted alone, attachments reached through the keys' slot fields (its few
+    // multi-attachment segments do not repay moving the data: r4w, 9.19 / 9.25 ms against
+    // 9.25 / 9.26 moved); the roll-up launches move ranges and scores with the keys.  (Keeping
+    // the roll-up attachments in descending-score order for early exits saved what its extra
+    // sort cost, r4j, and was removed.)
+    constexpr bool kKeyOrder = !FULL && !ROLL;
+    using Src = typename std::conditional<kKeyOrder, SliceSrcKey, SliceSrc>::type;
+    auto slot_at = [&](int t) -> int { return kKeyOrder ? (int)(F.key[t] & kSlotMask) : t; };
+    for (int level = start_level; !staged && G > 0 && h1 > h0; ++level) {   // else: never evaluated (:959)
       const int iteration = level + 1;
       if (level > start_level) {                     // roll up (:431-445): re-key to the parent clade
         for (int t = lane; t < n_att; t += 64) {
@@ -1077,7 +903,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         }
         wave_sync();
       }
-      if (!(WF_SKIP & 2)) sort_slice<(CAP + 63) / 64, !kDescOrder && !kKeyOrder>(F, n_att);   // one network: code size
+      sort_slice<(CAP + 63) / 64, !kKeyOrder>(F, n_att);   // one network: code size
       WLAP(3);
       // ---- segments = runs of equal (clade, locus) ----
       int ns = 0;
@@ -1109,7 +935,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
       // candidates, 6 every segment not yet evaluated.
       double* v = F.v();
       bool fail = false;
-      const bool prune = P.k1 > 0.0 && !(WF_SKIP & 1);
+      const bool prune = P.k1 > 0.0;
       const bool prune2 = FULL && prune && P.k2 > 0.0 && (!P.sister_on || P.sister_thr > 0.0);
       // first form, hand-over to k_dump_sparse after explain_one found no option: only what
       // its explain_two can read is evaluated (passes 4 and 5 as in the FULL form); the rest
@@ -1167,22 +993,13 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           const int run = max(0, hi16(x) - lo16(x));
           return fmin(sc, sc * ((double)run / (double)len) * (1.0 + 2e-12));
         }
-        if (kDescOrder) {                            // best first: past its top bits, nothing higher
-          const long long tb0 = desc_tb(F.sc[slot_at(kb)]);
-          for (int q = kb; q < ke; ++q) {
-            const double x = F.sc[slot_at(q)];
-            if (desc_tb(x) < tb0) break;
-            ub = fmax(ub, x);
-          }
-          return ub;
-        }
         for (int q = kb; q < ke; ++q) ub = fmax(ub, F.sc[slot_at(q)]);
         return ub;
       };
       auto best_score = [&](int t) -> double {       // (callers: v[t] < 0)
         return FULL ? scan_best(t) : -1.0 - v[t];
       };
-      // Hand-over (WF_E2_LB): a pass-4 candidate whose mean is surely >= every threshold the
+      // Hand-over (lower bounds): a pass-4 candidate whose mean is surely >= every threshold the
       // table's non-member readers compare it with (k2, the sister threshold, kmin) -- some
       // attachment's run alone gives the envelope a mean >= score x share, numpy's rounding
       // inside the 2e-12 slack -- is not evaluated in pass 4 (rc bit 0x80); its clade's mask
@@ -1202,12 +1019,12 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         return lb;
       };
       auto lb_sure = [&](int t) -> bool { return lb_mean(t) >= lb_thr; };
-      // Unmasked loci settled by lower bounds (WF_UM_LB): a known clade's segment whose bound
+      // Unmasked loci settled by lower bounds: a known clade's segment whose bound
       // reaches kmin unmasks its locus (:420-427) without its mean.  Only where the contig's
       // hand-over is sure to be the compact table (whose explain_two takes um from the header;
       // a whole table would rebuild um from the values it holds) or everything gets evaluated
       // (pass 6), and explain_one reads only the means of the clades it ranks.
-      const bool lb_um = !FULL && WF_UM_LB && prune2d && S.wave_two && S.dump_cap > 0 && G <= kE2MaxG &&
+      const bool lb_um = !FULL && prune2d && S.wave_two && S.dump_cap > 0 && G <= kE2MaxG &&
                          ns <= kE2Seg && P.weak == 0 && P.kmin > 0.0;
       auto lb_um_bits = [&](uint64_t open_) -> uint64_t {
         uint64_t b = 0;
@@ -1318,7 +1135,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
                 in = v[t] < 0.0 && ((um >> cg.y) & 1ull) && (int)rc[t] == gu;
               } else if (pass == 4) {
                 in = v[t] < 0.0 && best_score(t) >= bound2;
-                if (!FULL && WF_E2_LB && in && lb_sure(t)) {
+                if (!FULL && in && lb_sure(t)) {
                   in = false;
                   rc[t] |= 0x80;                       // (run sizes < 0x80: pass 4's post replaces them)
                 }
@@ -1351,9 +1168,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           bool one_run = false;                          // one envelope run [lo, hi) of value vv
           int lo = 0, hi = 0;
           double vv = 0.0;
-          if (WF_SKIP & 1) {
-            if (s < ns) v[s] = 0.75;
-          } else if (s < ns) {
+          if (s < ns) {
             const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att, na = ke - kb;
             g = cg_of(F, s).y;
             len = F.len[g];
@@ -1394,7 +1209,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           if (one_run) v[s] = one_run_mean(PackedLut{F.lut + F.lbase[g]}, nl, len, lo, hi, vv);
           WLAP(pass == 0 ? 7 : (pass == 6 ? 11 : 14));
           uint64_t mlist = __ballot(multi);
-          constexpr bool kFlat = ROLL && WF_FLAT_LEAVES;   // (its only multi path: the others compile out)
+          constexpr bool kFlat = ROLL;                   // (its only multi path: the others compile out)
           if constexpr (kFlat) {
             // roll-up levels, where a segment gathers the attachments of many clades: one
             // numpy leaf per lane over all of the chunk's multi-attachment segments
@@ -1406,7 +1221,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
               if (multi) v[s] = m;
             }
             mlist = 0;
-          } else if ((FULL || ROLL || (WF_LANE_MEANS6 && pass == 6)) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
+          } else if ((FULL || ROLL) && (__popcll(mlist) >= 3 || __ballot(big) != 0ull)) {
             // several multi-attachment segments: one lane each, not the whole wave per segment
             if (multi) {
               const int kb = seg_first(F, s), ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
@@ -1492,7 +1307,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
           // potential and to build their masks -- and count as sisters through pass 5's sister
           // candidates like any other clade.  Lane i: potential clade i's run (<= 64 of them,
           // else pass 6 below).
-          const bool members = !FULL && WF_E2_MEMBERS;
+          const bool members = !FULL;
           int ph = -1, pcnt = 0, np0 = 0;
           uint64_t pm = 0;
           for (int t0 = 0; t0 < ns; t0 += 64) {
@@ -1559,7 +1374,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
         }
         if (!e1_now) break;
         WLAP(32);                                      // (stamps: sure bits, pass choice)
-        if (__ballot(fail) != 0ull || (WF_SKIP & 4)) { staged = __ballot(fail) != 0ull; outcome = 2; break; }
+        if (__ballot(fail) != 0ull) { staged = __ballot(fail) != 0ull; outcome = 2; break; }
         // ---- explain_one (k_one's arithmetic, orgscorer.py:407-429, 447-461, 585-597) ----
         const int Gu = __popcll(um);
         if (Gu == 0) {                                 // level 0: skipped contig (:959)
@@ -1802,8 +1617,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
       const int Gu = __popcll(um);
       wave_sync();
       int dec = -1;
-      if constexpr (FULL) dec = (WF_SKIP & 16) ? kDecStop : wave_two(S, F, c, h0, l0, G, ns, um, Gu, iteration, pair_evals);
-      if ((WF_SKIP & 32) && dec == kDecRaise) dec = kDecStop;
+      if constexpr (FULL) dec = wave_two(S, F, c, h0, l0, G, ns, um, Gu, iteration, pair_evals);
       if (dec < 0) {
         staged = true;
         break;
@@ -1826,7 +1640,6 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? WF_ROLL_WAVES : 4)) void k_w
       }
       break;
     }
-    if (WF_SKIP & 15) staged = false;                  // variants: time this kernel alone
     if (lane == 0) {
       ccnt[c] = staged ? n_att : 0;
       cleaves[c] = staged ? nl_sum : 0;
@@ -1870,23 +1683,12 @@ hipError_t launch_cap(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t*
 
 }  // namespace
 
-#ifdef WF_STAMPS
-extern "C" int wf_stamps_read_fast(unsigned long long* out, int n) {
-  if (n > 48) n = 48;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
-}
-extern "C" int wf_stamps_reset_fast(void) {
-  unsigned long long z[48] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_wstamps), z, sizeof z) == hipSuccess ? 0 : -2;
-}
-#endif
+WF_STAMP_READER(fast, g_wstamps, 48)
 
 hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                        hipStream_t s) {
   const int N = sa.k.n_contigs;
-#ifndef WF_NO_CAP224
   if (max_hits <= 224) return launch_cap<224, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s);
-#endif
   return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s)
                          : launch_cap<512, false>(sa, ccnt, cleaves, pend, nullptr, N, nullptr, cus, 0, s);
 }
@@ -1894,9 +1696,7 @@ hipError_t launch_fast(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t
 hipError_t launch_fast_list(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
                             const int64_t* n_dev, int max_hits, int cus, hipStream_t s) {
   const int N = sa.k.n_contigs;
-#ifndef WF_NO_CAP224
   if (max_hits <= 224) return launch_cap<224, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s);
-#endif
   return max_hits <= 256 ? launch_cap<256, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s)
                          : launch_cap<512, false>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s);
 }
@@ -1904,9 +1704,7 @@ hipError_t launch_fast_list(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, in
 hipError_t launch_level(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, const int32_t* list,
                         const int64_t* n_dev, int level, int max_hits, int cus, hipStream_t s) {
   const int N = sa.k.n_contigs;
-#ifndef WF_NO_CAP224
   if (max_hits <= 224) return launch_cap<224, false, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
-#endif
   return max_hits <= 256 ? launch_cap<256, false, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level)
                          : launch_cap<512, false, true>(sa, ccnt, cleaves, pend, list, N, n_dev, cus, 0, s, level);
 }

@@ -33,11 +33,11 @@
 // tables, whose members outgrow the scratch, or with > 63 loci goes on to the dense
 // decision (k_decide_big) instead.
 constexpr int kSpCls = 128;      // mask-class hash slots (at most 3/4 used)
-constexpr int kSpPairs = 256;    // passing class pairs
+constexpr int kSpPairs = 128;    // passing class pairs
 constexpr int kSpMemG = 2048;    // member clades per contig (HBM scratch)
 constexpr int kSpParG = 4096;    // parent hash slots (HBM scratch), >= 2 * members
 constexpr int kSpDense = 16384;  // dense member rows (members x loci doubles, HBM scratch)
-constexpr int kSpWin = 256;      // segments staged per step
+constexpr int kSpWin = 256;      // segments staged per step (128: 0.04 ms slower, s6a)
 constexpr int kSpMaxG = 63;      // loci per contig (mask bits; ~0 marks an empty class slot)
 constexpr int kSpP1 = 8;         // pass 1: 64-segment chunks per step (one round trip each)
 
@@ -56,11 +56,14 @@ struct SpParent {                // 32 B: parent id (~0: empty), clades >= thres
 constexpr int kSpLPar = 64;
 static_assert(kSpLPar * 32 == kSpCls * (8 + 4 + 4), "lpar overlays the class table");
 // per-wave scratch: members (in the order found) | their positions grouped by class | parents
-// | the members' dense rows
+// | the members' dense rows | the virtual "Unknown" row | the melded-member bit sets (the
+// last two kept out of LDS: k_big_sparse's LDS sets its residency, 13 waves per CU at 12 KB)
 constexpr int64_t kSpOffGidx = (int64_t)kSpMemG * sizeof(SpMember);
 constexpr int64_t kSpOffPar = kSpOffGidx + (int64_t)kSpMemG * sizeof(int);
 constexpr int64_t kSpOffDense = kSpOffPar + (int64_t)kSpParG * sizeof(SpParent);
-constexpr int64_t kSpSlot = kSpOffDense + (int64_t)kSpDense * sizeof(double);
+constexpr int64_t kSpOffUrow = kSpOffDense + (int64_t)kSpDense * sizeof(double);
+constexpr int64_t kSpOffBm = kSpOffUrow + 64 * sizeof(double);
+constexpr int64_t kSpSlot = kSpOffBm + 2 * (kSpMemG / 32) * sizeof(unsigned);
 
 struct SpShared {
   // (wcg and wv are contiguous: after pass 4 they hold the members' dense rows, kSpLdsRows)
@@ -81,10 +84,8 @@ struct SpShared {
   int pair[kSpPairs];                        // passing class pairs: a | b << 16 (a <= b)
   int pref[kSpPairs + 1];                    // candidate-pair prefix
   double row[64];                            // one dense row (explain_one's best)
-  double urow[64];                           // --weak-loci assign-unknown: 1 - maxes
   int len[64];                               // locus lengths (ambiguous fraction)
   uint8_t syn[64];                           // best option's synteny
-  unsigned bm1[kSpMemG / 32], bm2[kSpMemG / 32];   // members melded as clade 1 / 2
   int n_used, n_pairs, n_in, all_ok, all_same, cnt, over;
 };
 
@@ -170,11 +171,11 @@ template <class F>
 __device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, int se, F f) {
   const int lane = threadIdx.x & 63;
   int carry = -1;
-  int2 cg[5];
-  double v[5];
+  int2 cg[kSpWin / 64 + 1];
+  double v[kSpWin / 64 + 1];
   auto fetch = [&](int base) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < kSpWin / 64 + 1; ++j) {
       const int t = base + 64 * j + lane;
       cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
       v[j] = t < se ? S.seg_mean[t] : 0.0;
@@ -184,7 +185,7 @@ __device__ __forceinline__ void sp_rows(const SArgs& S, SpShared& sh, int so, in
   for (int base = so; base < se; base += kSpWin) {
     __syncthreads();                                 // the previous window is consumed
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < kSpWin / 64 + 1; ++j) {
       sh.wcg[64 * j + lane] = cg[j];
       sh.wv[64 * j + lane] = v[j];
     }
@@ -210,11 +211,11 @@ template <class Pre, class F>
 __device__ __forceinline__ void sp_rows_pf(const SArgs& S, SpShared& sh, int so, int se, Pre pre, F f) {
   const int lane = threadIdx.x & 63;
   int carry = -1;
-  int2 cg[5];
-  double v[5];
+  int2 cg[kSpWin / 64 + 1];
+  double v[kSpWin / 64 + 1];
   auto fetch = [&](int base) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < kSpWin / 64 + 1; ++j) {
       const int t = base + 64 * j + lane;
       cg[j] = t < se ? S.seg_cg[t] : make_int2(-2, 0);
       v[j] = t < se ? S.seg_mean[t] : 0.0;
@@ -224,7 +225,7 @@ __device__ __forceinline__ void sp_rows_pf(const SArgs& S, SpShared& sh, int so,
   for (int base = so; base < se; base += kSpWin) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
+    for (int j = 0; j < kSpWin / 64 + 1; ++j) {
       sh.wcg[64 * j + lane] = cg[j];
       sh.wv[64 * j + lane] = v[j];
     }
@@ -451,6 +452,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   int* gidx = reinterpret_cast<int*>(ws + kSpOffGidx);
   SpParent* par = reinterpret_cast<SpParent*>(ws + kSpOffPar);
   double* drows = reinterpret_cast<double*>(ws + kSpOffDense);
+  double* urow = reinterpret_cast<double*>(ws + kSpOffUrow);   // --weak-loci assign-unknown: 1 - maxes
+  unsigned* bm1 = reinterpret_cast<unsigned*>(ws + kSpOffBm);  // members melded as clade 1 / 2
+  unsigned* bm2 = bm1 + kSpMemG / 32;
   BLAP_MARK(c);
   BSTAT(15, 1);
   BSTAT(12, se - so);
@@ -504,7 +508,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   // --weak-loci assign-unknown: the virtual "Unknown" row 1 - maxes (:416-418) and its bits
   const bool vu = P.weak == 2;
   const double uval = 1.0 - mxv;
-  if (vu && lane < G) sh.urow[lane] = uval;
+  if (vu && lane < G) urow[lane] = uval;
+  if (vu) __threadfence_block();                    // (read by other lanes after pass 2's barriers)
   const uint64_t u_k1 = vu ? __ballot(lane < G && uval >= P.k1) : 0ull;
   const uint64_t u_k2 = vu ? __ballot(lane < G && uval >= P.k2) : 0ull;
   const uint64_t u_hs = vu ? __ballot(lane < G && uval >= P.sister_thr) : 0ull;
@@ -539,13 +544,9 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       h = (h + 1) & (kSpCls - 1);
     }
   };
-#ifdef WF_STAMPS
-  unsigned long long p2_row = 0, p2_ins = 0;        // (stamps: pass 2's row summaries / class inserts)
-#endif
+  WF_STAMPS_ONLY(unsigned long long p2_row = 0, p2_ins = 0);   // (stamps: pass 2's row summaries / class inserts)
   sp_rows(S, sh, so, se, [&](bool st, int t, int w, int cl) {
-#ifdef WF_STAMPS
-    const unsigned long long q0 = __builtin_amdgcn_s_memtime();
-#endif
+    WF_STAMPS_ONLY(const unsigned long long q0 = __builtin_amdgcn_s_memtime());
     // past 3/4 of the class table the contig goes to the dense decision unless it has an
     // explain_one option: stop inserting (a full table made every new class probe all of it)
     const bool cls_full = sh.n_used * 4 > kSpCls * 3;
@@ -562,20 +563,11 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     }
     Pp += __popcll(__ballot(pot));
     upi += __popcll(__ballot(pot && cl < K.unknown));
-#ifdef WF_STAMPS
-    const unsigned long long q1 = __builtin_amdgcn_s_memtime();
-#endif
+    WF_STAMPS_ONLY(const unsigned long long q1 = __builtin_amdgcn_s_memtime());
     if (pot && !cls_full) ins_class(cmask);
-#ifdef WF_STAMPS
-    const unsigned long long q2 = __builtin_amdgcn_s_memtime();
-    p2_row += q1 - q0;
-    p2_ins += q2 - q1;
-#endif
+    WF_STAMPS_ONLY(const unsigned long long q2 = __builtin_amdgcn_s_memtime(); p2_row += q1 - q0; p2_ins += q2 - q1);
   });
-#ifdef WF_STAMPS
-  BSTAT(10, p2_row);
-  BSTAT(11, p2_ins);
-#endif
+  WF_STAMPS_ONLY(BSTAT(10, p2_row); BSTAT(11, p2_ins));
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const double r2 = __shfl_xor(br, off, 64);
@@ -591,7 +583,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
     auto next = [&]() -> double {
       const int g = __builtin_ctzll(m);
       m &= m - 1;
-      return sh.urow[g];
+      return urow[g];
     };
     u_rank = (0.0 + np_sum_seq(Gu, next)) / (double)Gu;
     if (better(u_rank, K.unknown, br, bk)) { br = u_rank; bk = K.unknown; brs = -1; }
@@ -634,7 +626,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       return true;
     }
     // the best clade's row: crit (min over kept loci) and set_synteny_one (:495-509)
-    sh.row[lane] = brs < 0 && lane < G ? sh.urow[lane] : 0.0;
+    sh.row[lane] = brs < 0 && lane < G ? urow[lane] : 0.0;
     __syncthreads();
     if (brs >= 0) {
       const int t = brs + lane;
@@ -785,7 +777,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
         const SpMember m = mem[q];
         double* row = drows + (int64_t)q * G;
         if (m.rs < 0) {
-          for (int g = 0; g < G; ++g) row[g] = sh.urow[g];
+          for (int g = 0; g < G; ++g) row[g] = urow[g];
         } else {
           for (int g = 0; g < G; ++g) row[g] = 0.0;
           for (int t = m.rs; t < se; ++t) {
@@ -797,7 +789,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       }
     const double* rows = dense ? drows : nullptr;     // (after pass 4: an LDS copy when it fits)
     auto acc = [&](int q, const SpMember& m) -> SpRowAcc {
-      return SpRowAcc{rows ? rows + (int64_t)q * G : nullptr, SpCursor{m.rs, m.cl, se, m.rs < 0 ? sh.urow : nullptr}};
+      return SpRowAcc{rows ? rows + (int64_t)q * G : nullptr, SpCursor{m.rs, m.cl, se, m.rs < 0 ? urow : nullptr}};
     };
     __threadfence_block();
     __syncthreads();
@@ -881,7 +873,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       best_crit = sp_pair_crit(S, acc(pu, A), acc(pv, B), keep);
       sh.n_in = 0; sh.all_ok = 1; sh.all_same = 1;
     }
-    for (int i = lane; i < kSpMemG / 32; i += 64) { sh.bm1[i] = 0; sh.bm2[i] = 0; }
+    for (int i = lane; i < kSpMemG / 32; i += 64) { bm1[i] = 0; bm2[i] = 0; }
+    __threadfence_block();
     __syncthreads();
     BLAP(7);
     // ---- pass 2 over the candidates: options within --range get the LGT filters --------
@@ -894,9 +887,10 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       if (!e.ok) atomicAnd(&sh.all_ok, 0);
       if (!e.same) atomicAnd(&sh.all_same, 0);
       const int q1 = e.c1p ? v : u, q2 = e.c2p ? v : u;
-      atomicOr(&sh.bm1[q1 >> 5], 1u << (q1 & 31));
-      atomicOr(&sh.bm2[q2 >> 5], 1u << (q2 & 31));
+      atomicOr(&bm1[q1 >> 5], 1u << (q1 & 31));
+      atomicOr(&bm2[q2 >> 5], 1u << (q2 & 31));
     });
+    __threadfence_block();
     __syncthreads();
     BLAP(8);
     // ---- meld_two (:640-669) ----------------------------------------------------------------
@@ -916,8 +910,8 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
       // the melded clades' LCAs (utils.py:401-411)
       int a1 = -1, a2 = -1;
       for (int q = lane; q < M; q += 64) {
-        if (in_bm(sh.bm1, q)) { a1 = lca2(K, a1, mem[q].cl); ++m1; }
-        if (in_bm(sh.bm2, q)) { a2 = lca2(K, a2, mem[q].cl); ++m2; }
+        if (in_bm(bm1, q)) { a1 = lca2(K, a1, mem[q].cl); ++m1; }
+        if (in_bm(bm2, q)) { a2 = lca2(K, a2, mem[q].cl); ++m2; }
       }
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) {
@@ -945,7 +939,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
         int o1 = 0, o2 = 0;
         for (int base = 0; base < M; base += 64) {
           const int q = base + lane;
-          const bool in1 = in_bm(sh.bm1, q), in2 = in_bm(sh.bm2, q);
+          const bool in1 = in_bm(bm1, q), in2 = in_bm(bm2, q);
           const uint64_t w1 = __ballot(in1), w2 = __ballot(in2);
           if (in1) K.meld[mbase + o1 + __popcll(w1 & below)] = mem[q].cl;
           if (in2) K.meld[mbase + m1 + o2 + __popcll(w2 & below)] = mem[q].cl;
@@ -1412,7 +1406,7 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
 // S_arg stays the first parameter: the loop body re-reads the argument block through
 // kernarg_fresh (wf_device.h) per contig -- held across the loop, its fields overflowed the
 // SGPR file (309 SGPRs spilled to VGPR lanes: a v_readlane per use, the kernel's SALU excess).
-__global__ __launch_bounds__(64, 3) void k_big_sparse(const SArgs S_arg, int level, int64_t n_keys) {
+__global__ __launch_bounds__(64, 4) void k_big_sparse(const SArgs S_arg, int level, int64_t n_keys) {
   __shared__ SpShared sh;
   char* ws = S_arg.sp_ws + (int64_t)blockIdx.x * kSpSlot;
   const int count = (int)S_arg.counters[2];

@@ -100,9 +100,6 @@ __global__ void k_init(const KArgs K) {
 // paints sites in (orgscorer.py:359-382).  Pass 0 only counts (attachments, a leaf bound
 // and the largest contig); pass 1 writes them at the contig's offset and does the
 // annotation transfer (orgscorer.py:383-392) for the contig's loci in LDS.
-#ifndef WF_ATT_NT_FORCE64
-#define WF_ATT_NT_FORCE64 0
-#endif
 constexpr int kAttNT = 64;       // one wave per contig: many contigs in flight ...
 constexpr int kAttNTBig = 512;   // ... or 8 when the batch's contigs have thousands of hits (the
 constexpr int kAttBigHits = 2048;   // cfg5 stress shape: one wave stepped ~80 dependent chunks)
@@ -1507,52 +1504,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int lev
   }
 }
 
-// Diagnostic build only (-DWF_STAMPS): shader-clock laps of sp_two (the compact hand-over's
-// explain_two) on every 8th contig it decides (scripts/wave_stamps.py reads them).
-#ifdef WF_STAMPS
-__device__ unsigned long long g_sstamps[16];
-#define SLAP_MARK(c) unsigned long long slap_ = __builtin_amdgcn_s_memtime(); const bool ssamp_ = ((c) & 7) == 0
-#define SLAP(i)                                                                     \
-  do {                                                                              \
-    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
-    if (ssamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_sstamps[i], n_ - slap_);    \
-    slap_ = n_;                                                                     \
-  } while (0)
-#define SSTAT(i, v) do { if (ssamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_sstamps[i], (unsigned long long)(v)); } while (0)
-// ... and of sp_level (k_big_sparse, k_dump_sparse<0>) on every 8th contig
-__device__ unsigned long long g_bstamps[24];
-#define BLAP_MARK(c) unsigned long long blap_ = __builtin_amdgcn_s_memtime(); const bool bsamp_ = ((c) & 7) == 0
-#define BLAP(i)                                                                     \
-  do {                                                                              \
-    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
-    if (bsamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_bstamps[i], n_ - blap_);    \
-    blap_ = n_;                                                                     \
-  } while (0)
-#define BSTAT(i, v) do { if (bsamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_bstamps[i], (unsigned long long)(v)); } while (0)
-#else
-#define BLAP_MARK(c) do {} while (0)
-#define BLAP(i) do {} while (0)
-#define BSTAT(i, v) do {} while (0)
-#define SLAP_MARK(c) do {} while (0)
-#define SLAP(i) do {} while (0)
-#define SSTAT(i, v) do {} while (0)
-#endif
 #include "wf_sparse.h"
-#ifdef WF_STAMPS
-extern "C" int wf_stamps_read_sparse(unsigned long long* out, int n) {
-  if (n > 16) n = 16;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
-}
-extern "C" int wf_stamps_reset_sparse(void) {
-  unsigned long long z[24] = {0};
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_bstamps), z, sizeof z) != hipSuccess) return -2;
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_sstamps), z, 16 * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
-}
-extern "C" int wf_stamps_read_big(unsigned long long* out, int n) {
-  if (n > 24) n = 24;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
-}
-#endif
+WF_STAMP_READER(sparse, g_sstamps, 16)
+WF_STAMP_READER(big, g_bstamps, 24)
 
 int bits_for(int64_t v) {   // bits to hold values 0..v
   int b = 1;
@@ -1588,20 +1542,11 @@ struct Buf {
 }  // namespace
 
 
-// roll-up launches of the first wave form: contigs handed out by a work-queue counter (1) or
-// in static XCD order (0)
-#ifndef WF_WAVE_QUEUE
-#define WF_WAVE_QUEUE 1
-#endif
-// ... and the level-0 launch over the triage's list
-#ifndef WF_L0_QUEUE
-#define WF_L0_QUEUE 1
-#endif
-// levels whose largest contig has 4,097..8,192 attachments: the per-contig LDS radix sort
-// (k_sort_radix, 1) or the device radix sort of the whole level (0)
-#ifndef WF_RADIX_LDS
-#define WF_RADIX_LDS 1
-#endif
+// The roll-up launches of the first wave form and its level-0 launch over the triage's list
+// take their contigs from a work-queue counter (a static XCD order left a few waves finishing
+// last: roll-up 4.98 -> 4.35, list 2.36 -> 2.00 ms, r5j / r5k).  Levels whose largest contig
+// has 4,097..8,192 attachments sort per contig in LDS (k_sort_radix), not with the device
+// radix sort of the whole level.
 
 struct StagedState {
   int device = 0;
@@ -2035,11 +1980,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     // The first form hands the contigs it leaves at explain_two (or at an unproven
     // assign-unknown row) over with their level-0 segment tables, every mean evaluated:
     // k_dump_sparse decides them from the table (pend 3 -> 0, 2 or 1)
-#ifdef WF_NO_DUMP
-    const bool dump = false;
-#else
     const bool dump = st->sparse_big != 0 && !st->rollup;
-#endif
     // Wave levels (WF_OPT_WAVE_TWO): the first form also decides explain_two and carries the
     // roll-up levels, one launch per level over the contigs the level before raised
     const bool levels = dump && st->wave_two;
@@ -2071,7 +2012,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         da.fail_ctr = rcnt + kMaxIter + 2;
       }
     }
-    if (WF_WAVE_QUEUE && (levels || st->triage)) {
+    if (levels || st->triage) {
       // work queues: [0] the level-0 list, [L] level L's launch
       ST_TRY(st->wq.ensure(s, (kMaxIter + 2) * sizeof(unsigned long long)));
       ST_TRY(hipMemsetAsync(st->wq.p, 0, (kMaxIter + 2) * sizeof(unsigned long long), s));
@@ -2092,7 +2033,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       ST_TRY(select_list(st, s, PendItT(st->pend.as<int32_t>(), PendIs{kPendTriage}), st->tri_list.as<int32_t>(),
                          st->tri_cnt.as<int64_t>(), N));
       SArgs ta = da;                                   // (the list's contigs vary in cost as the roll-up lists')
-      ta.wq = WF_WAVE_QUEUE && WF_L0_QUEUE ? st->wq.as<unsigned long long>() : nullptr;
+      ta.wq = st->wq.as<unsigned long long>();
       ST_TRY(launch_fast_list(ta, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                               st->tri_list.as<int32_t>(), st->tri_cnt.as<int64_t>(), max_hits, st->cus, s));
     } else {
@@ -2137,7 +2078,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
             la.dump_ctr_next = dctr + ((L + 1) & 1);
             la.roll_next = roll[(L + 1) & 1];
             la.roll_next_n = rcnt + L + 1;
-            la.wq = WF_WAVE_QUEUE ? st->wq.as<unsigned long long>() + L : nullptr;
+            la.wq = st->wq.as<unsigned long long>() + L;
             ST_TRY(launch_level(la, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                                 roll[L & 1], reinterpret_cast<const int64_t*>(rcnt + L), L, max_hits, st->cus, s));
             la.wq = nullptr;                             // (a queue for sp_two: r5t, 0.35 ms slower)
@@ -2170,10 +2111,8 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     ST_TRY(select_list(st, s, FitIt(hipcub::CountingInputIterator<int>(0),
                                     PendFits{st->pend.as<int32_t>(), st->cnt.as<int64_t>(), max_hits <= 256 ? 256 : 512}),
                        st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, N));
-#ifndef WF_NO_FULL
     ST_TRY(launch_full(sa, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(),
                        st->act0.as<int32_t>(), st->red.as<int64_t>() + 3, max_hits, st->cus, st->rollup, s));
-#endif
   } else {
     hipLaunchKernelGGL((k_att_contig<0, kAttNT>), dim3(agrid), dim3(kAttNT), 0, s, sa, st->cnt.as<int64_t>(),
                        st->cnt_leaves.as<int64_t>(),
@@ -2251,7 +2190,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
   if (max_att <= kSortMax && sa.key_tb + sa.key_lb + kSortIdxBits <= 64) {
     sa.sort_cap = 2;
     while (sa.sort_cap < max_att) sa.sort_cap <<= 1;
-  } else if (WF_RADIX_LDS && max_att <= kRadixMax && sa.key_tb + sa.key_lb <= 32) {
+  } else if (max_att <= kRadixMax && sa.key_tb + sa.key_lb <= 32) {
     sa.sort_cap = (int)((max_att + 511) & ~int64_t(511));   // the LDS radix sort (k_sort_radix)
   }
   if (A >= st->att_limit || TLB >= (int64_t(1) << 31) - 1) {
@@ -2322,7 +2261,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     ST_TRY(hipMemsetAsync(st->annot_best.p, 0, (size_t)n_annot * 8, s));
     ST_TRY(hipMemsetAsync(k.annot, 0xFF, (size_t)n_annot * 4, s));     // -1: no winner
   }
-  if (max_hits >= kAttBigHits && !WF_ATT_NT_FORCE64)
+  if (max_hits >= kAttBigHits)
     hipLaunchKernelGGL((k_att_contig<1, kAttNTBig>), dim3(std::min<unsigned>(agrid, (unsigned)n_first)), dim3(kAttNTBig), 0,
                        s, sa, nullptr, nullptr, nullptr, level0 ? st->act0.as<int32_t>() : nullptr, n_first);
   else
@@ -2540,15 +2479,5 @@ int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int m
   return rc;
 }
 
-#ifdef WF_STAMPS
-extern "C" int wf_stamps_read_staged(unsigned long long* out, int n) {
-  if (n > 32) n = 32;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess
-             ? 0 : -2;
-}
-extern "C" int wf_stamps_reset_staged(void) {
-  unsigned long long z[32] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof z) == hipSuccess ? 0 : -2;
-}
-#endif
+WF_STAMP_READER(staged, g_stamps, 32)
 }  // namespace wf

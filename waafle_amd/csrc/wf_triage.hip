@@ -30,31 +30,11 @@
 #include "wf_device.h"
 #include "wf_lanes.h"
 
-#ifndef WF_TRIAGE_WAVES
-#define WF_TRIAGE_WAVES 8              // resident waves per SIMD (64 VGPRs, ~12 spilled; a 4.8 KB slice).
-                                       // Same box (r5c): 3.66 ms per cfg4 pass against 3.85 at 6
-                                       // waves per SIMD (75 VGPRs, none spilled)
-#endif
 
 namespace wf {
 
 namespace {
 
-// Diagnostic build only (-DWF_STAMPS): per-phase shader-clock laps of every 16th contig the
-// triage takes (scripts/wave_stamps.py prints them).  Never in the product build.
-#ifdef WF_STAMPS
-__device__ unsigned long long g_tstamps[16];
-#define TLAP_MARK() unsigned long long tlap_ = __builtin_amdgcn_s_memtime(); const bool tsamp_ = (c & 15) == 0
-#define TLAP(i)                                                                     \
-  do {                                                                              \
-    const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
-    if (tsamp_ && lane == 0) atomicAdd(&g_tstamps[i], n_ - tlap_);                  \
-    tlap_ = n_;                                                                     \
-  } while (0)
-#else
-#define TLAP_MARK() do {} while (0)
-#define TLAP(i) do {} while (0)
-#endif
 
 constexpr int kTrHB = 4;               // hit batches of 64: contigs of up to 256 hits
 constexpr int kTrLoc = 64;             // loci (64-bit locus masks)
@@ -63,14 +43,11 @@ constexpr int kTrSeg = 64;             // full clades x loci evaluated (one lane
 constexpr int kTrSpan = 26;            // loci one hit may attach to, from its first candidate
 constexpr uint32_t kTrEmpty = 0xFFFFFFFFu;
 constexpr int kTrXcds = 8;             // MI355X: 8 XCDs of 32 CUs, each with its own L2
+constexpr int kTrWaves = 8;            // resident waves per SIMD (64 VGPRs, ~12 spilled; a 4.8 KB slice).
+                                       // Same box (r5c): 3.66 ms per cfg4 pass against 3.85 at 6
+                                       // waves per SIMD (75 VGPRs, none spilled)
 constexpr int kTrBig = 512;            // more hits than any wave slice: k_count
 constexpr int kCntR = 4;               // k_count: hit batches per round of loads
-#ifndef WF_TRI_BF
-#define WF_TRI_BF 1                    // branch-free binary search and rank accumulation
-#endif
-#ifndef WF_COUNT_WIDE
-#define WF_COUNT_WIDE 0                // 512-thread k_count for contigs of thousands of hits
-#endif
 
 struct TriSmem {
   int lo[kTrLoc], hi[kTrLoc];          // locus site ranges (min, max of start/end)
@@ -89,7 +66,7 @@ struct TriSmem {
   int8_t tfull[kTrTab];                // table slot -> full clade index (-1: not full)
   int8_t st[kTrLoc];
 };
-static_assert(sizeof(TriSmem) <= 160 * 1024 / (4 * WF_TRIAGE_WAVES), "triage slice: WF_TRIAGE_WAVES per SIMD");
+static_assert(sizeof(TriSmem) <= 160 * 1024 / (4 * kTrWaves), "triage slice: kTrWaves per SIMD");
 
 __device__ __forceinline__ uint32_t tr_hash(uint32_t clade) { return (clade * 0x9E3779B1u) >> 25; }   // 7 bits
 
@@ -104,7 +81,7 @@ __device__ __forceinline__ uint32_t tr_lohi(int qlo, int qhi, int llo, int len) 
   return (uint32_t)start | ((uint32_t)stop << 16);
 }
 
-__global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves,
+__global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves,
                                                                int32_t* pend) {
   __shared__ TriSmem F;
   const int lane = threadIdx.x;
@@ -189,12 +166,8 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
         int g = 0;
 #pragma unroll
         for (int k = 32; k > 0; k >>= 1) {
-#if WF_TRI_BF
           const int gk = g + k;                      // (a select, not a branch per step)
           g = (gk <= G && F.hi[min(gk, G) - 1] < qlo) ? gk : g;
-#else
-          if (g + k <= G && F.hi[g + k - 1] < qlo) g += k;
-#endif
         }
         const int g0 = g;
         uint32_t rel = 0u;
@@ -361,7 +334,6 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
       const int m8 = G < 8 ? 0 : G - (G & 7);
       double r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0, r4 = 0.0, r5 = 0.0, r6 = 0.0, r7 = 0.0;
       double mn = __builtin_inf();
-#if WF_TRI_BF
       for (int u = 0; u < m8; u += 8) {                // (u % 8 -> accumulator, in order: straight-line)
         const double x0 = lane_bcast(mean, base + u), x1 = lane_bcast(mean, base + u + 1);
         const double x2 = lane_bcast(mean, base + u + 2), x3 = lane_bcast(mean, base + u + 3);
@@ -371,22 +343,6 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
         mn = x0 < mn ? x0 : mn; mn = x1 < mn ? x1 : mn; mn = x2 < mn ? x2 : mn; mn = x3 < mn ? x3 : mn;
         mn = x4 < mn ? x4 : mn; mn = x5 < mn ? x5 : mn; mn = x6 < mn ? x6 : mn; mn = x7 < mn ? x7 : mn;
       }
-#else
-      for (int u = 0; u < m8; ++u) {
-        const double x = lane_bcast(mean, base + u);
-        mn = x < mn ? x : mn;
-        switch (u & 7) {
-          case 0: r0 += x; break;
-          case 1: r1 += x; break;
-          case 2: r2 += x; break;
-          case 3: r3 += x; break;
-          case 4: r4 += x; break;
-          case 5: r5 += x; break;
-          case 6: r6 += x; break;
-          default: r7 += x; break;
-        }
-      }
-#endif
       double res = m8 > 0 ? leaf_tree(r0, r1, r2, r3, r4, r5, r6, r7) : 0.0;
       for (int u = m8; u < G; ++u) {
         const double x = lane_bcast(mean, base + u);
@@ -451,9 +407,7 @@ __global__ __launch_bounds__(64, WF_TRIAGE_WAVES) void k_triage(const SArgs S_ar
     }
     wave_sync();                                       // the slice is reused by the next contig
     TLAP(8);                                           // (stamps: explain_one, meld_one, record)
-#ifdef WF_STAMPS
-    if (tsamp_ && lane == 0) atomicAdd(&g_tstamps[15], 1ull);
-#endif
+    WF_STAMPS_ONLY(if (tsamp_ && lane == 0) atomicAdd(&g_tstamps[15], 1ull));
   }
 }
 
@@ -530,105 +484,10 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
   if (lane == 0 && n_staged && S.fail_ctr) atomicAdd(S.fail_ctr, n_staged);   // (one add per wave)
 }
 
-#if WF_COUNT_WIDE
-template <int NT>
-__global__ __launch_bounds__(NT) void k_count_wide(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend) {
-  constexpr int kW = NT / 64;                      // (NT 512: contigs of thousands of hits, 8 waves each)
-  __shared__ int s_lo[kTrLoc], s_hi[kTrLoc];
-  __shared__ int8_t s_st[kTrLoc];
-  __shared__ int s_ok;
-  __shared__ long long s_red[2][kW];
-  const KArgs& K = S.k;
-  const DevParams& P = K.p;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  unsigned long long n_staged = 0;
-  for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
-    const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
-    if (h1 - h0 <= kTrBig) continue;                 // (k_triage handed it on: pend kPendTriage)
-    const int64_t l0 = K.loc_off[c];
-    const int G = (int)(K.loc_off[c + 1] - l0);
-    if (w == 0) {
-      int clo = 0, chi = -1, cst = 0;
-      if (lane < G && G <= kTrLoc) {
-        const int a = K.lstart[l0 + lane], e = K.lend[l0 + lane];
-        clo = min(a, e);
-        chi = max(a, e);
-        cst = K.lstrand[l0 + lane];
-      }
-      const int cprev = __shfl_up(chi, 1, 64);
-      const bool ok = G > 0 && G <= kTrLoc && P.min_overlap > 0.0 &&
-                      __ballot(lane < G && lane >= 1 && clo <= cprev) == 0ull;
-      if (lane == 0) s_ok = ok ? 1 : 0;
-      if (ok && lane < G) { s_lo[lane] = clo; s_hi[lane] = chi; s_st[lane] = (int8_t)cst; }
-    }
-    __syncthreads();
-    if (!s_ok) {                                     // (uniform) left to the wave form
-      __syncthreads();
-      continue;
-    }
-    long long n_att = 0, nl = 0;
-    for (int64_t hb = h0; hb < h1; hb += NT * kCntR) {   // kCntR batches' loads issued together
-      double r_scv[kCntR];
-      int r_qlo[kCntR], r_qhi[kCntR], r_hs[kCntR];
-#pragma unroll
-      for (int r = 0; r < kCntR; ++r) {
-        const int64_t h = hb + NT * r + tid;
-        r_scv[r] = -1.0; r_qlo[r] = 0; r_qhi[r] = 0; r_hs[r] = 0;
-        if (h < h1) { r_scv[r] = K.scov[h]; r_qlo[r] = K.qlo[h]; r_qhi[r] = K.qhi[h]; if (P.stranded) r_hs[r] = K.hstrand[h]; }
-      }
-#pragma unroll
-      for (int r = 0; r < kCntR; ++r) {
-        if (hb + NT * r + tid >= h1 || !(r_scv[r] >= P.min_scov)) continue;
-        const int qlo = r_qlo[r], qhi = r_qhi[r], hs = r_hs[r];
-        int g = 0;
-#pragma unroll
-        for (int k = 32; k > 0; k >>= 1)
-          if (g + k <= G && s_hi[g + k - 1] < qlo) g += k;
-        for (; g < G; ++g) {
-          const int lo = s_lo[g];
-          if (lo > qhi) break;
-          const int len = s_hi[g] - lo + 1;
-          if (attaches(P, qlo, qhi, hs, lo, len, s_st[g])) {
-            ++n_att;
-            nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
-                  (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
-          }
-        }
-      }
-    }
-    n_att = wave_sum_dpp(n_att);
-    nl = wave_sum_dpp(nl);
-    if (kW > 1) {
-      if (lane == 0) { s_red[0][w] = n_att; s_red[1][w] = nl; }
-      __syncthreads();
-      if (tid == 0)
-        for (int x = 1; x < kW; ++x) { n_att += s_red[0][x]; nl += s_red[1][x]; }
-    }
-    if (tid == 0) {
-      ccnt[c] = n_att;
-      cleaves[c] = nl;
-      pend[c] = 1;                                   // staged from level 0
-    }
-    ++n_staged;
-    __syncthreads();                                 // (the loci and s_ok are the next contig's)
-  }
-  if (tid == 0 && n_staged && S.fail_ctr) atomicAdd(S.fail_ctr, n_staged);   // (one add per workgroup)
-}
-
-#endif
 
 }  // namespace
 
-#ifdef WF_STAMPS
-extern "C" int wf_stamps_read_triage(unsigned long long* out, int n) {
-  if (n > 16) n = 16;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -2;
-}
-extern "C" int wf_stamps_reset_triage(void) {
-  unsigned long long z[16] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_tstamps), z, sizeof z) == hipSuccess ? 0 : -2;
-}
-#endif
+WF_STAMP_READER(triage, g_tstamps, 16)
 
 int triage_per_cu() {
   static const int per_cu = [] {
@@ -647,12 +506,6 @@ hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * triage_per_cu()));
   hipLaunchKernelGGL(k_triage, dim3(grid), dim3(64), 0, s, sa, ccnt, cleaves, pend);
   if (max_hits > kTrBig)
-#if WF_COUNT_WIDE
-    if (max_hits >= 2048)                             // thousands of hits per contig: 8 waves each
-      hipLaunchKernelGGL(k_count_wide<512>, dim3((unsigned)std::min<int64_t>(N, (int64_t)cus * 4)), dim3(512), 0, s,
-                         sa, ccnt, cleaves, pend);
-    else
-#endif
     hipLaunchKernelGGL(k_count, dim3((unsigned)std::min<int64_t>(N, (int64_t)cus * 32)), dim3(64), 0, s, sa, ccnt,
                        cleaves, pend);
   return hipGetLastError();
