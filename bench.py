@@ -253,9 +253,10 @@ def cli_end_to_end(config, workers):
 
 class DeviceBatch:
     """A batch's arrays and result records in HBM (torch tensors) with the wf_batch /
-    wf_result structs pointing at them."""
+    wf_result structs pointing at them.  `min_scov`: the packed hit_key (wf_batch.hit_key,
+    built on the host with the arrays, as the CLI packs it at parse time) for that value."""
 
-    def __init__(self, batch, dev):
+    def __init__(self, batch, dev, min_scov=None):
         import torch
         from waafle_amd import lib as L
         N, NH, NL = batch.n_contigs, batch.n_hits, batch.n_loci
@@ -266,6 +267,9 @@ class DeviceBatch:
             if arr.dtype == np.uint32:
                 arr = arr.view(np.int32)
             self.d[f] = torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+        if min_scov is not None:
+            from waafle_amd import engine
+            self.d["hit_key"] = torch.from_numpy(engine.hit_keys(batch, min_scov).view(np.int32)).to(dev)
         e = lambda n, t: torch.empty(max(n, 1), dtype=t, device=dev)
         self.out = {
             "call": e(N, torch.int8), "crit": e(N, torch.float64), "rank": e(N, torch.float64),
@@ -279,6 +283,7 @@ class DeviceBatch:
                             max_hits=batch.max_hits, max_loci=batch.max_loci,
                             device_resident=1, _pad=0,
                             **{f: C.c_void_p(self.d[f].data_ptr()) for f in self.d})
+        self.keys_packed = min_scov is not None
         self.rs = L.WfResult(**{f: C.c_void_p(self.out[f].data_ptr())
                                 for f, _ in L.WfResult._fields_})
 
@@ -319,7 +324,7 @@ def timed_passes(so, h, chk, db, params, steps, warmup, dist, dev, cdev=None):
 def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=None, traffic_json=None):
     """The explain_two stress leg (BASELINE configs[4]) on this rank's cfg5 share."""
     import torch
-    db = DeviceBatch(kbatch, dev)
+    db = DeviceBatch(kbatch, dev, params.min_scov)
     elapsed, tm = timed_passes(so, h, chk, db, params, steps, 1, dist, dev, cdev)
     pe = db.host("pair_evals")
     calls = db.host("call")
@@ -407,7 +412,7 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
     return out
 
 
-def share_projection(so, h, chk, batch, params, ns, steps, warmup, dev, t_full):
+def share_projection(so, h, chk, batch, params, ns, steps, warmup, dev, t_full, min_scov=None):
     """The strong-scaling shares of this workload timed one at a time on this GPU: for each N,
     every rank's contig range [r n / N, (r + 1) n / N) (exactly what bench.py --gpus N gives
     rank r) as its own device-resident batch, W + K passes as the main line.  The path has no
@@ -424,7 +429,7 @@ def share_projection(so, h, chk, batch, params, ns, steps, warmup, dev, t_full):
         rows = []
         for r in range(n):
             a, b = r * N // n, (r + 1) * N // n
-            db = DeviceBatch(batch.slice(a, b), dev)
+            db = DeviceBatch(batch.slice(a, b), dev, min_scov)
             el, tm = timed_passes(so, h, chk, db, params, steps, warmup, None, dev)
             del db
             torch.cuda.empty_cache()
@@ -531,14 +536,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
     chk(so.wf_set_stream(h, C.c_void_p(stream.cuda_stream)))
 
-    db = DeviceBatch(batch, dev)
+    db = DeviceBatch(batch, dev, params.min_scov)
     elapsed, tm = timed_passes(so, h, chk, db, params, args.steps, args.warmup, dist, dev, cdev)
     calls, pe, iters = db.host("call"), db.host("pair_evals"), db.host("iterations")
     del db
     torch.cuda.empty_cache()
     weak = None
     if wbatch is not None:
-        wdb = DeviceBatch(wbatch, dev)
+        wdb = DeviceBatch(wbatch, dev, params.min_scov)
         w_el, _ = timed_passes(so, h, chk, wdb, params, args.steps, args.warmup, dist, dev, cdev)
         del wdb
         torch.cuda.empty_cache()
@@ -553,7 +558,7 @@ def main():
     if world == 1 and args.shares:
         projection = share_projection(so, h, chk, batch, params,
                                       [int(x) for x in args.shares.split(",") if x],
-                                      args.steps, args.warmup, dev, elapsed / args.steps)
+                                      args.steps, args.warmup, dev, elapsed / args.steps, params.min_scov)
     pairs = float(pe.sum())
     k2_counts = k2_algorithmic(pe, batch)
     if dist:          # whole-job counts

@@ -24,8 +24,9 @@
 extern "C" {
 #endif
 
-#define WF_ABI_VERSION 5   /* 4: WF_OPT_SPARSE_BIG 0/1 retired, WF_PHASE_ROLLUP, WF_OPT_WAVE_TWO / _DUMP_CAP;
-                                 5: WF_OPT_TRIAGE, WF_PHASE_TRIAGE */
+#define WF_ABI_VERSION 6   /* 4: WF_OPT_SPARSE_BIG 0/1 retired, WF_PHASE_ROLLUP, WF_OPT_WAVE_TWO / _DUMP_CAP;
+                                 5: WF_OPT_TRIAGE, WF_PHASE_TRIAGE;
+                                 6: wf_batch.hit_key (packed hit record), wf_pack_hit_keys */
 
 enum wf_status {
   WF_OK = 0,
@@ -146,6 +147,14 @@ typedef struct wf_batch {
   const int32_t* loc_start;   /* [n_loci] GFF start */
   const int32_t* loc_end;     /* [n_loci] GFF end */
   const int8_t*  loc_strand;  /* [n_loci] 0 '+', 1 '-', 2 anything else */
+  /* Optional (NULL: the library packs it on the device, one extra pass over the hits): the
+     hit's filter fields packed in one word, wf_pack_hit_keys' layout -- bits 0-23 hit_taxon,
+     bit 24 hit_scov >= params.min_scov (the attach_hits filter, orgscorer.py:363-364: it
+     must be packed with the min_scov of the wf_score call it is passed to), bit 25
+     hit_strand '-', bits 26-31 hit_sysmask & 63 (systems 0-5).  The level-0 triage, the
+     kernel of most contigs, then reads 20 bytes per hit (qlo, qhi, key, score) instead of
+     32.  The other arrays stay required (the other kernels read them). */
+  const uint32_t* hit_key;    /* [n_hits] */
 } wf_batch;
 
 /* Per-contig results (caller-allocated, same residency as the batch). */
@@ -313,6 +322,12 @@ int wf_set_mode(wf_ctx* ctx, int mode);               /* WF_MODE_LEVEL0 (default
 int wf_set_option(wf_ctx* ctx, int option, int64_t value);   /* wf_option */
 int wf_set_taxonomy(wf_ctx* ctx, const wf_taxonomy* tax);
 int wf_score(wf_ctx* ctx, const wf_batch* batch, const wf_params* params, wf_result* out);
+/* wf_batch.hit_key from the separate arrays (host memory, any thread, no context):
+   out[i] = taxon[i] | (scov[i] >= min_scov) << 24 | (strand[i] == 1) << 25
+            | (sysmask[i] & 63) << 26.
+   WF_E_BADINPUT for a taxon id outside [0, 2^24) or a strand other than 0 / 1. */
+int wf_pack_hit_keys(int64_t n_hits, const int32_t* taxon, const int8_t* strand, const double* scov,
+                     const uint32_t* sysmask, double min_scov, uint32_t* out);
 int wf_synchronize(wf_ctx* ctx);
 int wf_timing_enable(wf_ctx* ctx, int on);             /* also resets the counters */
 int wf_timing_read(wf_ctx* ctx, wf_timing* out);       /* synchronises first */

@@ -298,3 +298,31 @@ def test_pruned_forms_agree_with_staged(lgt_heavy, flags):
     assert (got["staged"].call == 2).sum() > 100           # (the shortcuts' inputs are there)
     assert_same(got["level0"], got["staged"], batch)
     assert_same(got["notriage"], got["staged"], batch)
+
+
+@pytest.mark.parametrize("flags", [[], ["--min-scov", "0.9"], ["--stranded"]],
+                         ids=["default", "min-scov_0p9", "stranded"])
+def test_packed_hit_key_equals_library_packed_and_is_checked(flags):
+    """wf_batch.hit_key (ABI 6): the engine's packed words (numpy, parse time) and the
+    library's own packing (hit_key NULL: k_pack_keys before the triage) give the same
+    records; a host batch whose key disagrees with its arrays (packed for another
+    --min-scov) is refused with WF_E_BADINPUT before any launch."""
+    data = synth.generate(n=2000, genes=8, clades=200, seed=91)
+    batch, tax = synth.to_batch(data)
+    params = cli.param_dict(cli.parse_flags(flags))
+    s = engine.GpuScorer(0)
+    s.set_taxonomy(tax)
+    got = s.score(batch, params)
+    res = engine.Results.empty(batch.n_contigs, batch.n_hits, batch.n_loci, len(batch.systems))
+    bs, rs = engine.batch_struct(batch), res.struct()          # hit_key NULL
+    ps = engine.params_struct(params)
+    import ctypes as C
+    assert s.lib.wf_score(s.h, C.byref(bs), C.byref(ps), C.byref(rs)) == lib.WF_OK
+    assert_same(res, got, batch)
+    stale = engine.hit_keys(batch, float(params["min_scov"]) + 0.07).copy()
+    bs = engine.batch_struct(batch)
+    bs.hit_key = lib.ptr(stale)
+    if (stale != engine.hit_keys(batch, float(params["min_scov"]))).any():
+        assert s.lib.wf_score(s.h, C.byref(bs), C.byref(ps), C.byref(rs)) == lib.WF_E_BADINPUT
+        assert b"hit_key" in s.lib.wf_last_error(s.h)
+    s.close()

@@ -36,7 +36,7 @@ struct wf_ctx {
   int64_t lds_bytes = 24 * 1024;   // decision arena per workgroup (wf_set_lds_bytes)
   // staging for host-resident batches
   DevBuf b_hit_off, b_qlo, b_qhi, b_taxon, b_hstrand, b_score, b_scov, b_sysmask;
-  DevBuf b_loc_off, b_lstart, b_lend, b_lstrand;
+  DevBuf b_loc_off, b_lstart, b_lend, b_lstrand, b_hkey;
   DevBuf r_call, r_crit, r_rank, r_c1, r_c2, r_dir, r_iters, r_syn, r_nm1, r_nm2, r_meld,
       r_annot, r_pairs, r_status, r_need;
   // timing
@@ -219,7 +219,7 @@ void wf_free(wf_ctx* ctx) {
                     &ctx->jn_lhits, &ctx->jn_c1, &ctx->jn_c2, &ctx->jn_cj, &ctx->jn_ratio,
                     &ctx->jn_tmp, &ctx->jn_pfirst, &ctx->jn_pmask, &ctx->jn_ovf,
                     &ctx->b_hit_off, &ctx->b_qlo, &ctx->b_qhi, &ctx->b_taxon, &ctx->b_hstrand,
-                    &ctx->b_score, &ctx->b_scov, &ctx->b_sysmask, &ctx->b_loc_off,
+                    &ctx->b_score, &ctx->b_scov, &ctx->b_sysmask, &ctx->b_hkey, &ctx->b_loc_off,
                     &ctx->b_lstart, &ctx->b_lend, &ctx->b_lstrand, &ctx->r_call, &ctx->r_crit,
                     &ctx->r_rank, &ctx->r_c1, &ctx->r_c2, &ctx->r_dir, &ctx->r_iters,
                     &ctx->r_syn, &ctx->r_nm1, &ctx->r_nm2, &ctx->r_meld, &ctx->r_annot,
@@ -374,6 +374,15 @@ static int check_batch(wf_ctx* ctx, const wf_batch* b, const wf_params* p, const
     for (int64_t i = 0; i < b->n_hits; ++i)
       if (b->hit_taxon[i] < 0 || b->hit_taxon[i] >= ctx->tax_n)
         return fail(ctx, WF_E_BADINPUT, "hit %lld taxon id out of range", (long long)i);
+    if (b->hit_key)                // the packed words must say what the arrays say
+      for (int64_t i = 0; i < b->n_hits; ++i) {
+        const uint32_t k = b->hit_key[i];
+        const uint32_t want = (uint32_t)b->hit_taxon[i] | (uint32_t)(b->hit_scov[i] >= p->min_scov) << 24 |
+                              (uint32_t)(b->hit_strand[i] == 1) << 25 | (b->hit_sysmask[i] & 63u) << 26;
+        if (k != want)
+          return fail(ctx, WF_E_BADINPUT, "hit %lld: hit_key 0x%08x, its arrays (min_scov %g) give 0x%08x",
+                      (long long)i, k, p->min_scov, want);
+      }
   }
   return WF_OK;
 }
@@ -423,7 +432,7 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
     K.hit_off = b->hit_off; K.qlo = b->hit_qlo; K.qhi = b->hit_qhi; K.taxon = b->hit_taxon;
     K.hstrand = b->hit_strand; K.score = b->hit_score; K.scov = b->hit_scov;
     K.sysmask = b->hit_sysmask; K.loc_off = b->loc_off; K.lstart = b->loc_start;
-    K.lend = b->loc_end; K.lstrand = b->loc_strand;
+    K.lend = b->loc_end; K.lstrand = b->loc_strand; K.hkey = b->hit_key;
     K.call = r->call; K.crit = r->crit; K.rank = r->rank; K.c1 = r->clade1; K.c2 = r->clade2;
     K.dir = r->direction; K.iters = r->iterations; K.syn = r->synteny; K.nm1 = r->n_meld1;
     K.nm2 = r->n_meld2; K.meld = r->meld; K.annot = r->annot_hit; K.pair_evals = r->pair_evals;
@@ -445,6 +454,8 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
       (rc = upload(ctx, ctx->b_lend, b->loc_end, NL, &K.lend)) ||
       (rc = upload(ctx, ctx->b_lstrand, b->loc_strand, NL, &K.lstrand)))
     return rc;
+  K.hkey = nullptr;
+  if (b->hit_key && (rc = upload(ctx, ctx->b_hkey, b->hit_key, NH, &K.hkey))) return rc;
   if ((rc = alloc_out(ctx, ctx->r_call, N, &K.call)) ||
       (rc = alloc_out(ctx, ctx->r_crit, N, &K.crit)) ||
       (rc = alloc_out(ctx, ctx->r_rank, N, &K.rank)) ||
@@ -478,6 +489,17 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
   for (int32_t c = 0; c < b->n_contigs; ++c)
     if (r->status[c] != 0)
       return fail(ctx, r->status[c], "contig %d failed with status %d", c, r->status[c]);
+  return WF_OK;
+}
+
+int wf_pack_hit_keys(int64_t n_hits, const int32_t* taxon, const int8_t* strand, const double* scov,
+                     const uint32_t* sysmask, double min_scov, uint32_t* out) {
+  if (n_hits < 0 || (n_hits > 0 && (!taxon || !strand || !scov || !sysmask || !out))) return WF_E_BADINPUT;
+  for (int64_t i = 0; i < n_hits; ++i) {
+    if (taxon[i] < 0 || taxon[i] >= (1 << 24) || (strand[i] != 0 && strand[i] != 1)) return WF_E_BADINPUT;
+    out[i] = (uint32_t)taxon[i] | (uint32_t)(scov[i] >= min_scov) << 24 | (uint32_t)(strand[i] == 1) << 25 |
+             (sysmask[i] & 63u) << 26;
+  }
   return WF_OK;
 }
 

@@ -34,6 +34,7 @@ struct KArgs {
   const int64_t* hit_off; const int32_t* qlo; const int32_t* qhi; const int32_t* taxon;
   const int8_t* hstrand; const double* score; const double* scov; const uint32_t* sysmask;
   const int64_t* loc_off; const int32_t* lstart; const int32_t* lend; const int8_t* lstrand;
+  const uint32_t* hkey;          // wf_batch.hit_key (caller's, or packed by k_pack_keys)
   // taxonomy
   const int32_t* parent; const int32_t* depth; const int32_t* sibp; const int64_t* leaves;
   const int32_t* lin;            // [names * kLin] ancestor at each depth (-1 below the name);
@@ -178,6 +179,7 @@ struct StagedState;
 // Level-0 triage (wf_triage.hip): pend[c] = 0 for the contigs it finished (explain_one from
 // the full clades), kPendTriage for the rest, which the first wave form then runs (list).
 constexpr int kPendTriage = 9;
+hipError_t pack_keys(const KArgs& k, int64_t n_hits, uint32_t* key, int cus, hipStream_t s);
 hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                          hipStream_t s);
 // the first wave form over `list` (length *n_dev, on the device) at level 0

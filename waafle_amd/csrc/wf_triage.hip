@@ -81,8 +81,22 @@ __device__ __forceinline__ uint32_t tr_lohi(int qlo, int qhi, int llo, int len) 
   return (uint32_t)start | ((uint32_t)stop << 16);
 }
 
+// The packed hit word (wf_batch.hit_key): taxon | scov >= min_scov << 24 | strand '-' << 25 |
+// systems 0-5 << 26.  After the table pass the low 24 bits hold the clade's table slot + 1.
+constexpr uint32_t kKeyTaxon = (1u << 24) - 1u, kKeyScov = 1u << 24, kKeyMinus = 1u << 25;
+constexpr int kKeySys = 26;
+
+// wf_batch.hit_key when the caller passes none (include/waafle_hip.h)
+__global__ void k_pack_keys(const KArgs K, int64_t n_hits, uint32_t* key) {
+  for (int64_t h = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; h < n_hits; h += (int64_t)gridDim.x * blockDim.x)
+    key[h] = (uint32_t)K.taxon[h] | (K.scov[h] >= K.p.min_scov ? kKeyScov : 0u) | (K.hstrand[h] == 1 ? kKeyMinus : 0u) |
+             (K.n_sys > 0 ? (K.sysmask[h] & 63u) << kKeySys : 0u);
+}
+
+// SYSKEY: the annotation systems come from the key (n_systems <= 6); else from hit_sysmask.
+template <bool SYSKEY>
 __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int64_t* ccnt, int64_t* cleaves,
-                                                               int32_t* pend) {
+                                                         int32_t* pend) {
   __shared__ TriSmem F;
   const int lane = threadIdx.x;
   const int N = S_arg.k.n_contigs;
@@ -104,24 +118,26 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     const int64_t nh = h1 - h0;
     const int64_t hend = min(h1, h0 + 64 * kTrHB);
-    // every field of the contig's hits, issued before the loci
-    int r_qlo[kTrHB], r_qhi[kTrHB], r_cl[kTrHB], r_hs[kTrHB];
-    double r_sc[kTrHB], r_scv[kTrHB];
-    uint32_t r_m[kTrHB];
+    // every field of the contig's hits, issued before the loci: 20 bytes a hit (range, the
+    // packed key, score)
+    int r_qlo[kTrHB], r_qhi[kTrHB];
+    uint32_t r_k[kTrHB];
+    double r_sc[kTrHB];
+    uint32_t r_m[SYSKEY ? 1 : kTrHB];
 #pragma unroll
     for (int b = 0; b < kTrHB; ++b) {
       const int64_t h = h0 + 64 * b + lane;
-      r_qlo[b] = 0; r_qhi[b] = 0; r_cl[b] = 0; r_hs[b] = 0; r_sc[b] = 0.0; r_scv[b] = 0.0; r_m[b] = 0u;
+      r_qlo[b] = 0; r_qhi[b] = 0; r_k[b] = 0u; r_sc[b] = 0.0;
+      if (!SYSKEY) r_m[b] = 0u;
       if (h < hend) {
-        r_scv[b] = K.scov[h];
         r_qlo[b] = K.qlo[h];
         r_qhi[b] = K.qhi[h];
-        if (P.stranded) r_hs[b] = K.hstrand[h];        // (the strand only matters --stranded)
-        r_cl[b] = K.taxon[h];
+        r_k[b] = K.hkey[h];
         r_sc[b] = K.score[h];
-        if (nsys > 0) r_m[b] = K.sysmask[h];
+        if (!SYSKEY && nsys > 0) r_m[b] = K.sysmask[h];
       }
     }
+    auto sysm = [&](int b) -> uint32_t { return SYSKEY ? r_k[b] >> kKeySys : r_m[b]; };
     const int64_t l0 = K.loc_off[c];
     const int G = (int)(K.loc_off[c + 1] - l0);
     int my_lo = 0, my_hi = -1, my_st = 0;
@@ -161,7 +177,7 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
 #pragma unroll
     for (int b = 0; b < kTrHB; ++b) {
       uint32_t am = 0u;
-      if (h0 + 64 * b + lane < hend && r_scv[b] >= P.min_scov) {
+      if (h0 + 64 * b + lane < hend && (r_k[b] & kKeyScov)) {
         const int qlo = r_qlo[b], qhi = r_qhi[b];
         int g = 0;
 #pragma unroll
@@ -174,14 +190,16 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
         for (; g < G; ++g) {
           const int lo = F.lo[g];
           if (lo > qhi) break;
-          if (attaches(P, qlo, qhi, r_hs[b], lo, F.hi[g] - lo + 1, F.st[g])) {
+          if (attaches(P, qlo, qhi, (r_k[b] & kKeyMinus) ? 1 : 0, lo, F.hi[g] - lo + 1, F.st[g])) {
             if (g - g0 < kTrSpan) rel |= 1u << (g - g0);
             else bad = true;
           }
         }
         if (rel) {
           am = (uint32_t)g0 | (rel << 6);
-          for (int j = 0; j < P.jump; ++j) r_cl[b] = K.parent[r_cl[b]];   // orgscorer.py:955-957
+          int cl = (int)(r_k[b] & kKeyTaxon);
+          for (int j = 0; j < P.jump; ++j) cl = K.parent[cl];           // orgscorer.py:955-957
+          r_k[b] = (r_k[b] & ~kKeyTaxon) | (uint32_t)cl;
         }
       }
       r_am[b] = am;
@@ -191,7 +209,7 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
 #pragma unroll
     for (int b = 0; b < kTrHB; ++b) {
       if ((r_am[b] & 0x7Fu) == 0x40u) {               // g0 == 0 and locus 0 attached
-        const uint32_t cl = (uint32_t)r_cl[b];
+        const uint32_t cl = r_k[b] & kKeyTaxon;
         uint32_t slot = tr_hash(cl);
         for (int probes = 0;; ++probes) {
           if (probes == kTrTab) { bad = true; break; }
@@ -208,8 +226,8 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
     }
     wave_sync();
     TLAP(2);                                           // (stamps: candidate inserts)
-    // ---- every attachment ORs its loci into its clade's mask (r_cl becomes the clade's table
-    // slot, -1 outside the table); annotation pass 1 (:383-392) ----
+    // ---- every attachment ORs its loci into its clade's mask (the key's taxon bits become the
+    // clade's table slot + 1, 0 outside the table); annotation pass 1 (:383-392) ----
 #pragma unroll
     for (int b = 0; b < kTrHB; ++b) {
       const uint32_t am = r_am[b];
@@ -217,7 +235,7 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
       if (am != 0u) {
         const int g0 = (int)(am & 63u);
         const uint64_t lm = (uint64_t)(am >> 6) << g0;
-        const uint32_t cl = (uint32_t)r_cl[b];
+        const uint32_t cl = r_k[b] & kKeyTaxon;
         uint32_t slot = tr_hash(cl);
         for (int probes = 0; probes < kTrTab; ++probes) {
           const uint32_t k = F.tkey[slot];
@@ -225,14 +243,15 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
           if (k == kTrEmpty) break;
           slot = (slot + 1) & (kTrTab - 1);
         }
-        if (ann_on && r_m[b] != 0u && r_sc[b] >= P.annot_ref)
+        const uint32_t m = sysm(b);
+        if (ann_on && m != 0u && r_sc[b] >= P.annot_ref)
           for (uint64_t bits = lm; bits; bits &= bits - 1) {
             const int g = __builtin_ctzll(bits);
             for (int s = 0; s < nsys; ++s)
-              if ((r_m[b] >> s) & 1u) atomicMax(&F.abest[g * nsys + s], dbits(r_sc[b]));
+              if ((m >> s) & 1u) atomicMax(&F.abest[g * nsys + s], dbits(r_sc[b]));
           }
       }
-      r_cl[b] = found;
+      r_k[b] = (r_k[b] & ~kKeyTaxon) | (uint32_t)(found + 1);
     }
     wave_sync();
     TLAP(3);                                           // (stamps: masks, annotation pass 1)
@@ -263,7 +282,8 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
       int fi = -1;
       if (am != 0u) {
         const int g0 = (int)(am & 63u);
-        fi = r_cl[b] >= 0 ? (int)F.tfull[r_cl[b]] : -1;
+        const int slot = (int)(r_k[b] & kKeyTaxon) - 1;
+        fi = slot >= 0 ? (int)F.tfull[slot] : -1;
         if (fi >= 0)
           for (uint32_t rel = am >> 6; rel; rel &= rel - 1) {
             const int g = g0 + __builtin_ctz(rel);
@@ -278,12 +298,13 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
             if (lo < hi) atomicMax(&F.spart[q], dbits(r_sc[b]));
             if (lo <= 0 && hi >= len && r_sc[b] > 0.0) atomicMax(&F.sfw[q], dbits(r_sc[b]));
           }
-        if (ann_on && r_m[b] != 0u && r_sc[b] >= P.annot_ref) {
+        const uint32_t m = sysm(b);
+        if (ann_on && m != 0u && r_sc[b] >= P.annot_ref) {
           const int h = (int)(h0 + 64 * b + lane);
           for (uint64_t bits = (uint64_t)(am >> 6) << g0; bits; bits &= bits - 1) {
             const int g = __builtin_ctzll(bits);
             for (int s = 0; s < nsys; ++s)
-              if (((r_m[b] >> s) & 1u) && F.abest[g * nsys + s] == dbits(r_sc[b])) atomicMax(&F.ahit[g * nsys + s], h);
+              if (((m >> s) & 1u) && F.abest[g * nsys + s] == dbits(r_sc[b])) atomicMax(&F.ahit[g * nsys + s], h);
           }
         }
       }
@@ -443,18 +464,18 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
     wave_sync();
     long long n_att = 0, nl = 0;
     for (int64_t hb = h0; hb < h1; hb += 64 * kCntR) {   // kCntR batches' loads issued together
-      double r_scv[kCntR];
-      int r_qlo[kCntR], r_qhi[kCntR], r_hs[kCntR];
+      uint32_t r_k[kCntR];
+      int r_qlo[kCntR], r_qhi[kCntR];
 #pragma unroll
       for (int r = 0; r < kCntR; ++r) {
         const int64_t h = hb + 64 * r + lane;
-        r_scv[r] = -1.0; r_qlo[r] = 0; r_qhi[r] = 0; r_hs[r] = 0;
-        if (h < h1) { r_scv[r] = K.scov[h]; r_qlo[r] = K.qlo[h]; r_qhi[r] = K.qhi[h]; if (P.stranded) r_hs[r] = K.hstrand[h]; }
+        r_k[r] = 0u; r_qlo[r] = 0; r_qhi[r] = 0;
+        if (h < h1) { r_k[r] = K.hkey[h]; r_qlo[r] = K.qlo[h]; r_qhi[r] = K.qhi[h]; }
       }
 #pragma unroll
       for (int r = 0; r < kCntR; ++r) {
-        if (hb + 64 * r + lane >= h1 || !(r_scv[r] >= P.min_scov)) continue;
-        const int qlo = r_qlo[r], qhi = r_qhi[r], hs = r_hs[r];
+        if (hb + 64 * r + lane >= h1 || !(r_k[r] & kKeyScov)) continue;
+        const int qlo = r_qlo[r], qhi = r_qhi[r], hs = (r_k[r] & kKeyMinus) ? 1 : 0;
         int g = 0;
 #pragma unroll
         for (int k = 32; k > 0; k >>= 1)
@@ -489,10 +510,11 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
 
 WF_STAMP_READER(triage, g_tstamps, 16)
 
+template <bool SYSKEY>
 int triage_per_cu() {
   static const int per_cu = [] {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_triage), 64, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, reinterpret_cast<const void*>(&k_triage<SYSKEY>), 64, 0) !=
             hipSuccess || b < 1)
       b = 1;
     return b;
@@ -500,11 +522,23 @@ int triage_per_cu() {
   return per_cu;
 }
 
+hipError_t pack_keys(const KArgs& k, int64_t n_hits, uint32_t* key, int cus, hipStream_t s) {
+  if (n_hits > 0)
+    hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)std::min<int64_t>((n_hits + 255) / 256, (int64_t)cus * 16)),
+                       dim3(256), 0, s, k, n_hits, key);
+  return hipGetLastError();
+}
+
 hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                          hipStream_t s) {
   const int N = sa.k.n_contigs;
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * triage_per_cu()));
-  hipLaunchKernelGGL(k_triage, dim3(grid), dim3(64), 0, s, sa, ccnt, cleaves, pend);
+  if (sa.k.n_sys <= 6) {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * triage_per_cu<true>()));
+    hipLaunchKernelGGL(k_triage<true>, dim3(grid), dim3(64), 0, s, sa, ccnt, cleaves, pend);
+  } else {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(N, (int64_t)cus * triage_per_cu<false>()));
+    hipLaunchKernelGGL(k_triage<false>, dim3(grid), dim3(64), 0, s, sa, ccnt, cleaves, pend);
+  }
   if (max_hits > kTrBig)
     hipLaunchKernelGGL(k_count, dim3((unsigned)std::min<int64_t>(N, (int64_t)cus * 32)), dim3(64), 0, s, sa, ccnt,
                        cleaves, pend);

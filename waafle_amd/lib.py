@@ -6,6 +6,8 @@ loaded, `load()` raises.  Build it with `python -m waafle_amd.build`.
 import ctypes as C
 import os
 
+import numpy as np
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libwaafle_hip.so")
 
@@ -18,7 +20,7 @@ MODE_WAVES = 3
 OPT_SPARSE_BIG, OPT_ATT_LIMIT, OPT_WAVE_TWO, OPT_DUMP_CAP, OPT_TRIAGE = 1, 2, 3, 4, 5   # wf_set_option
 PHASES = ("waves", "attach", "segments", "decide", "big", "handover", "rollup", "triage")   # wf_phase 0..7
 N_PHASES = 8
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _P = C.c_void_p
 
@@ -45,7 +47,8 @@ class WfBatch(C.Structure):
                 ("device_resident", C.c_int32), ("_pad", C.c_int32),
                 ("hit_off", _P), ("hit_qlo", _P), ("hit_qhi", _P), ("hit_taxon", _P),
                 ("hit_strand", _P), ("hit_score", _P), ("hit_scov", _P), ("hit_sysmask", _P),
-                ("loc_off", _P), ("loc_start", _P), ("loc_end", _P), ("loc_strand", _P)]
+                ("loc_off", _P), ("loc_start", _P), ("loc_end", _P), ("loc_strand", _P),
+                ("hit_key", _P)]
 
 
 class WfResult(C.Structure):
@@ -117,6 +120,7 @@ SIGNATURES = {
     "wf_set_taxonomy": (C.c_int, [C.c_void_p, C.POINTER(WfTaxonomy)]),
     "wf_score": (C.c_int, [C.c_void_p, C.POINTER(WfBatch), C.POINTER(WfParams),
                            C.POINTER(WfResult)]),
+    "wf_pack_hit_keys": (C.c_int, [C.c_int64, _P, _P, _P, _P, C.c_double, _P]),
     "wf_synchronize": (C.c_int, [C.c_void_p]),
     "wf_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
     "wf_timing_read": (C.c_int, [C.c_void_p, C.POINTER(WfTiming)]),
@@ -167,6 +171,16 @@ def device_count():
     n = C.c_int(0)
     lib.wf_device_count(C.byref(n))
     return n.value
+
+
+def pack_hit_keys(taxon, strand, scov, sysmask, min_scov):
+    """wf_batch.hit_key (include/waafle_hip.h, wf_pack_hit_keys' layout) in numpy: taxon |
+    (scov >= min_scov) << 24 | (strand == 1) << 25 | (sysmask & 63) << 26."""
+    key = np.asarray(taxon).astype(np.uint32)
+    key |= (np.asarray(scov) >= min_scov).astype(np.uint32) << np.uint32(24)
+    key |= (np.asarray(strand) == 1).astype(np.uint32) << np.uint32(25)
+    key |= (np.asarray(sysmask).astype(np.uint32) & np.uint32(63)) << np.uint32(26)
+    return key
 
 
 def ptr(a):
