@@ -1578,6 +1578,7 @@ struct StagedState {
   int64_t phase_n[8] = {0};
   Buf act0, act1, base0, base1, big_list, big2_list, two_list, one_list, big_ws, tmp, pend, act_l0;
   Buf sp_ws;                        // k_big_sparse scratch (kSpSlot per wave)
+  Buf hkey;                         // wf_batch.hit_key when the caller passed none
   Buf dump_cg, dump_mean, dump_first, dump_list, dump_ctr, dump_um;   // hand-over (k_dump_sparse)
   bool level0 = true;               // wave kernels (wf_fast.hip) before the staged kernels
   bool rollup = false;              // ... carrying the roll-up levels too
@@ -2022,6 +2023,11 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       // clades; the first wave form runs the rest from its list (count on the device)
       ST_TRY(st->tri_list.ensure(s, (size_t)N * 4));
       ST_TRY(st->tri_cnt.ensure(s, 8));
+      if (!da.k.hkey) {                                  // no wf_batch.hit_key: packed here
+        ST_TRY(st->hkey.ensure(s, (size_t)std::max<int64_t>(NH, 1) * 4));
+        ST_TRY(pack_keys(da.k, NH, st->hkey.as<uint32_t>(), st->cus, s));
+        da.k.hkey = st->hkey.as<uint32_t>();
+      }
       const int t_tri0 = t_mark(st, s);                 // (the triage span: its launch alone)
       ST_TRY(launch_triage(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,
                            st->cus, s));
