@@ -931,12 +931,8 @@ constexpr int kRegAtt = 4;   // attachments of a segment held in registers
 // max(0, max{score_a : lo_a <= x < hi_a}).
 // Where a segment's attachments come from: the fused kernel's sorted LDS keys (attachment
 // index in the low 24 bits) or the staged path's sorted (key, attachment index) pairs.
-// Attachment sources for SegAttT.  kDesc: the attachments of a segment come in descending
-// order of their scores' top 23 bits (desc_tb; ties in any order), which lets SegAttT stop a
-// scan once those bits fall below the cover it found (see SegAttT::classify).
-__device__ __forceinline__ long long desc_tb(double v) { return __double_as_longlong(v) >> 40; }
+// Attachment sources for SegAttT: sorted position t -> attachment index -> (range, score).
 struct KeySrc {
-  static constexpr bool kDesc = false;
   const uint64_t* keys;
   const int *alo, *ahi;
   const double* asc;
@@ -946,7 +942,6 @@ struct KeySrc {
   }
 };
 struct SortedSrc {                       // attachments gathered into sorted order
-  static constexpr bool kDesc = false;
   const int2* lohi;
   const double* sc;
   __device__ __forceinline__ int idx(int t) const { return t; }
@@ -956,7 +951,6 @@ struct SortedSrc {                       // attachments gathered into sorted ord
   }
 };
 struct ValSrc {
-  static constexpr bool kDesc = false;
   const int* vals;
   const int *alo, *ahi;
   const double* asc;
@@ -999,15 +993,9 @@ struct SegAttT {
       for (int i = 0; i < NREG; ++i)
         if (x >= lo[i] && x < hi[i]) v = sc[i] > v ? sc[i] : v;
     } else {
-      long long vtb = -1;                  // (kDesc: top bits of the first cover's score)
       for (int t = kb; t < ke; ++t) {
         int l, h; double s;
         get(C, t, l, h, s);
-        if (Src::kDesc) {
-          const long long tb = desc_tb(s);
-          if (vtb >= 0 && tb < vtb) break;   // every later score is below the cover's
-          if (x >= l && x < h && vtb < 0) vtb = tb;
-        }
         if (x >= l && x < h) v = s > v ? s : v;
       }
     }
@@ -1033,21 +1021,12 @@ struct SegAttT {
   __device__ __forceinline__ int classify(const Src& C, int st, int m, double& F, int& plo,
                                           int& phi, double& ps) const {
     const int be = st + (m << 3);
-    int na = REG ? NREG : ke - kb;
+    const int na = REG ? NREG : ke - kb;
     F = 0.0;
-    long long ftb = -1;
 #pragma unroll
     for (int i = 0; i < na; ++i) {
       int l, h; double v;
       att<REG>(C, i, l, h, v);
-      if (!REG && Src::kDesc) {
-        // descending scores: past the first whole-body cover, once the scores drop below
-        // its (top bits) nothing later covers higher or exceeds F, so the partial-overlap
-        // scan below stops there too
-        const long long tb = desc_tb(v);
-        if (ftb >= 0 && tb < ftb) { na = i; break; }
-        if (l < h && l <= st && be <= h && ftb < 0) ftb = tb;
-      }
       if (l < h && l <= st && be <= h) F = v > F ? v : F;
     }
     int npos = 0;
@@ -1138,19 +1117,10 @@ struct SegAttT {
     for (int x = st; x < be;) {
       double v = 0.0;
       int nx = be;
-      long long vtb = -1;
 #pragma unroll
       for (int i = 0; i < na; ++i) {
         int l, h; double s;
         att<REG>(C, i, l, h, s);
-        if (!REG && Src::kDesc) {
-          // descending scores: the attachments past the first cover of x, once below its
-          // score, neither raise the envelope on [x, nx) nor start a higher run inside it
-          // (a run split at a lower attachment's end would add the same values in order)
-          const long long tb = desc_tb(s);
-          if (vtb >= 0 && tb < vtb) break;
-          if (l < h && l <= x && x < h && vtb < 0) vtb = tb;
-        }
         if (l < h) {
           if (l <= x && x < h) { v = s > v ? s : v; nx = min(nx, h); }
           else if (l > x) nx = min(nx, l);

@@ -231,7 +231,6 @@ __device__ __forceinline__ int hi16(uint32_t w) { return (int)(w >> 16); }
 // The slice's attachments for SegAttT (wf_device.h): sorted position t -> range, score (at
 // t since sort_slice).
 struct SliceSrc {
-  static constexpr bool kDesc = false;
   const uint32_t* key;
   const uint32_t* lohi;
   const double* sc;
@@ -243,7 +242,6 @@ struct SliceSrc {
 };
 // Level 0 without the data move: sorted position t -> its key's slot field -> range, score.
 struct SliceSrcKey {
-  [[maybe_unused]] static constexpr bool kDesc = false;
   const uint32_t* key;
   const uint32_t* lohi;
   const double* sc;
@@ -663,6 +661,10 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? kRollWaves : 4)) void k_wave
   static_assert(!(FULL && ROLL), "the roll-up passes are first-form launches");
   const int start_level = ROLL ? start_level_arg : 0;   // (ROLL: always >= 1)
   if (n_dev) n_list = (int)*n_dev;                   // the list's length, counted on the device
+  // a queue hands out n_list contigs in all: waves past that many take none and leave before
+  // touching its counter (a short roll-up list over ~4 k waves spent ~50 us in their claims;
+  // the static order below deals contigs to every block, so it has no such exit)
+  if (S_arg.wq && (int)blockIdx.x >= n_list) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WaveSmem<CAP, FULL>& F = *reinterpret_cast<WaveSmem<CAP, FULL>*>(smem);
   const int lane = threadIdx.x;
@@ -1215,7 +1217,30 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? kRollWaves : 4)) void k_wave
             // numpy leaf per lane over all of the chunk's multi-attachment segments
             if (mlist != 0ull) {
               int kb = 0, ke = 0;
-              if (multi) { kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att; }
+              if (multi) {
+                kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
+                // The envelope needs only the attachments scoring above the best whole-locus
+                // one (Fw, which covers every site) and [0, len) at Fw itself: compacted in
+                // place (a roll-up launch's sorted attachments are its data, read by nothing
+                // once their segment's mean is taken), so each leaf lane scans those few
+                // instead of every attachment the segment gathered.  The same envelope, the
+                // same site values, the same bits.
+                double Fw = 0.0;
+                for (int t = kb; t < ke; ++t) {
+                  const uint32_t x = F.lohi[t];
+                  const double sc = F.sc[t];
+                  if (lo16(x) <= 0 && hi16(x) >= len && sc > Fw) Fw = sc;
+                }
+                int o = kb;                              // (o <= t: writes trail the reads)
+                for (int t = kb; t < ke; ++t) {
+                  const uint32_t x = F.lohi[t];
+                  const double sc = F.sc[t];
+                  if (lo16(x) < hi16(x) && sc > Fw) { F.lohi[o] = x; F.sc[o] = sc; ++o; }
+                }
+                if (Fw > 0.0) { F.lohi[o] = (uint32_t)len << 16; F.sc[o] = Fw; ++o; }   // (o < ke: the
+                ke = o;                                  // whole-locus attachment was not kept)
+              }
+              wave_sync();
               const double m = flat_leaf_means(Src{F.key, F.lohi, F.sc}, F.lut + F.lbase[multi ? g : 0], mlist,
                                                kb, ke, nl, len, F.runs());
               if (multi) v[s] = m;
