@@ -86,11 +86,11 @@ def parse_args():
                     help="N = 1: time every rank's strong-scaling share of the workload at these "
                          "N on this one GPU (`strong_share_projection`); '' disables")
     ap.add_argument("--traffic-json", default=None)
-    ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r05", "cfg4_valu.json"),
+    ap.add_argument("--valu-pmc-json", default=os.path.join(PROFILES, "r06", "cfg4_valu.json"),
                     help="PMC VALU counts of the main pass (scripts/pmc_main.py, optional)")
-    ap.add_argument("--k2-traffic-json", default=os.path.join(PROFILES, "r05", "traffic_cfg5.json"),
+    ap.add_argument("--k2-traffic-json", default=os.path.join(PROFILES, "r06", "traffic_cfg5.json"),
                     help="FETCH/WRITE of the k2 leg's kernels (scripts/pmc_k2_r5.sh)")
-    ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r05", "k2_pmc.json"),
+    ap.add_argument("--k2-pmc-json", default=os.path.join(PROFILES, "r06", "k2_pmc.json"),
                     help="PMC VALU counts of the k2 leg's kernels (rocprofv3 --pmc, optional)")
     return ap.parse_args()
 
@@ -610,7 +610,7 @@ def main():
             return None, "{} file of another libwaafle_hip.so build".format(kind)
         return j, None
     traffic, tsrc = None, None
-    tj, why_t = pmc_file(args.traffic_json or os.path.join(PROFILES, "r05", "traffic_{}.json".format(args.config)),
+    tj, why_t = pmc_file(args.traffic_json or os.path.join(PROFILES, "r06", "traffic_{}.json".format(args.config)),
                          "traffic")
     if tj:
         # per launch, corrected as MI355X_MICROARCH.md's HBM / rocprofv3 section prescribes:

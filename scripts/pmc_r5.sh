@@ -6,7 +6,7 @@
 set -u
 O=gpurun_out/${OUT:-r5pmc}; mkdir -p $O
 export TMPDIR=/tmp
-B4="--k2-contigs 0 --cpu-sample 0 --e2e= --pcie 0 --steps 3 --warmup 1"
+B4="--k2-contigs 0 --cpu-sample 0 --e2e= --pcie 0 --shares= --steps 3 --warmup 1"
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 IC="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE"
 if [ "${TRAFFIC:-1}" = 1 ]; then

@@ -1217,30 +1217,7 @@ __global__ __launch_bounds__(64, FULL ? 2 : (ROLL ? kRollWaves : 4)) void k_wave
             // numpy leaf per lane over all of the chunk's multi-attachment segments
             if (mlist != 0ull) {
               int kb = 0, ke = 0;
-              if (multi) {
-                kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att;
-                // The envelope needs only the attachments scoring above the best whole-locus
-                // one (Fw, which covers every site) and [0, len) at Fw itself: compacted in
-                // place (a roll-up launch's sorted attachments are its data, read by nothing
-                // once their segment's mean is taken), so each leaf lane scans those few
-                // instead of every attachment the segment gathered.  The same envelope, the
-                // same site values, the same bits.
-                double Fw = 0.0;
-                for (int t = kb; t < ke; ++t) {
-                  const uint32_t x = F.lohi[t];
-                  const double sc = F.sc[t];
-                  if (lo16(x) <= 0 && hi16(x) >= len && sc > Fw) Fw = sc;
-                }
-                int o = kb;                              // (o <= t: writes trail the reads)
-                for (int t = kb; t < ke; ++t) {
-                  const uint32_t x = F.lohi[t];
-                  const double sc = F.sc[t];
-                  if (lo16(x) < hi16(x) && sc > Fw) { F.lohi[o] = x; F.sc[o] = sc; ++o; }
-                }
-                if (Fw > 0.0) { F.lohi[o] = (uint32_t)len << 16; F.sc[o] = Fw; ++o; }   // (o < ke: the
-                ke = o;                                  // whole-locus attachment was not kept)
-              }
-              wave_sync();
+              if (multi) { kb = seg_first(F, s); ke = s + 1 < ns ? seg_first(F, s + 1) : n_att; }
               const double m = flat_leaf_means(Src{F.key, F.lohi, F.sc}, F.lut + F.lbase[multi ? g : 0], mlist,
                                                kb, ke, nl, len, F.runs());
               if (multi) v[s] = m;
