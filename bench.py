@@ -73,7 +73,7 @@ def parse_args():
     ap.add_argument("--flags", default="",
                     help="waafle_orgscorer flags for the main workload, e.g. '--weak-loci assign-unknown'")
     ap.add_argument("--option", action="append", default=[],
-                    help="wf_set_option NAME=VALUE (sparse_big, att_limit, wave_two, dump_cap); repeatable")
+                    help="wf_set_option NAME=VALUE (sparse_big, att_limit, dump_cap, triage); repeatable")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: "
                          "control traffic on the CPU, e.g. with several ranks on one device)")

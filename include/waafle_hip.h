@@ -26,7 +26,8 @@ extern "C" {
 
 #define WF_ABI_VERSION 6   /* 4: WF_OPT_SPARSE_BIG 0/1 retired, WF_PHASE_ROLLUP, WF_OPT_WAVE_TWO / _DUMP_CAP;
                                  5: WF_OPT_TRIAGE, WF_PHASE_TRIAGE;
-                                 6: wf_batch.hit_key (packed hit record), wf_pack_hit_keys */
+                                 6: wf_batch.hit_key (packed hit record), wf_pack_hit_keys;
+                                    WF_OPT_WAVE_TWO 0 (the round-3 hand-over flow) retired */
 
 enum wf_status {
   WF_OK = 0,
@@ -48,7 +49,7 @@ enum wf_call { WF_CALL_UNCLASSIFIED = 0, WF_CALL_NO_LGT = 1, WF_CALL_LGT = 2 };
  * WF_MODE_LEVEL0 (default): per-contig wave kernels carry level 0 in LDS (explain_one in
  *   the wave; explain_two from the segment table it hands over, k_dump_sparse), and every
  *   roll-up level is one more launch of the same wave form over the contigs the level before
- *   raised (WF_OPT_WAVE_TWO 1).  Only contigs that exceed a wave's LDS slice (attachments,
+ *   raised.  Only contigs that exceed a wave's LDS slice (attachments,
  *   loci, leaf tables) or the hand-over tables continue in the second wave form and then
  *   the staged kernels.
  * WF_MODE_WAVES: the second (FULL) wave form carries explain_two and the roll-up levels in
@@ -70,10 +71,11 @@ enum wf_mode { WF_MODE_STAGED = 0, WF_MODE_LEVEL0 = 2, WF_MODE_WAVES = 3 };
  * WF_OPT_ATT_LIMIT: hit-locus attachments the staged kernels accept in one wf_score call
  *   (default and maximum 2^31 - 1; more -> WF_E_TOOBIG and the call's records are not
  *   valid: score the batch in parts).  The wave forms hold a contig's attachments in LDS.
- * WF_OPT_WAVE_TWO (WF_MODE_LEVEL0): 1 (default) the first wave form also decides explain_two
- *   (up to 64 potential clades, <= 63 loci) and carries the roll-up levels, one pass per level
- *   over the contigs still open; the rest goes to the segment-table decision (k_dump_sparse);
- *   0: every explain_two contig goes there and the roll-up levels run in the staged kernels.
+ * WF_OPT_WAVE_TWO (WF_MODE_LEVEL0): 1, the only value since ABI 6: the first wave form also
+ *   decides explain_two (up to 64 potential clades, <= 63 loci) and carries the roll-up
+ *   levels, one pass per level over the contigs still open; the rest goes to the
+ *   segment-table decision (k_dump_sparse).  0 (every explain_two contig there and the
+ *   roll-up levels in the staged kernels: the round-3 flow) is retired: WF_E_BADINPUT.
  * WF_OPT_DUMP_CAP: segment-table entries of the wave form's hand-over buffer (default
  *   max(32 * contigs, 65536)); contigs past it go to the staged kernels (a test setting).
  * WF_OPT_TRIAGE (WF_MODE_LEVEL0 / _WAVES): 1 (default) a level-0 triage kernel first decides

@@ -31,8 +31,6 @@ FORMS = {
     "level0": dict(mode="level0"),
     # the same without the level-0 triage (wf_triage.hip): the wave form runs every contig
     "notriage": dict(mode="level0", options={lib.OPT_TRIAGE: 0}),
-    # round-3 flow: every explain_two contig handed over whole, roll-up in the staged kernels
-    "handover": dict(mode="level0", options={lib.OPT_WAVE_TWO: 0}),
     # a hand-over buffer of 96 entries: the contigs past it take the staged kernels
     "dumpcap": dict(mode="level0", options={lib.OPT_DUMP_CAP: 96}),
     "waves": dict(mode="waves"),
@@ -315,7 +313,6 @@ def test_full_size_cfg2_properties():
                dict(mode="staged", options={lib.OPT_SPARSE_BIG: 2}),   # segment-table form
                dict(lds_bytes=65536),         # large arena: every contig in LDS
                dict(mode="staged"), dict(mode="level0"), dict(mode="waves"),
-               dict(options={lib.OPT_WAVE_TWO: 0}),      # round-3 hand-over flow
                dict(options={lib.OPT_DUMP_CAP: 4096}),   # hand-over buffer overflow
                dict()):
         small = engine.GpuScorer(0, **kw)

@@ -167,7 +167,7 @@ def test_option_validation():
     s = engine.GpuScorer(0)
     for opt, val in ((lib.OPT_ATT_LIMIT, 0), (lib.OPT_ATT_LIMIT, 1 << 31), (lib.OPT_SPARSE_BIG, 4),
                      (lib.OPT_SPARSE_BIG, 0), (lib.OPT_SPARSE_BIG, 1), (lib.OPT_TRIAGE, 2),
-                     (99, 1)):   # (SPARSE_BIG 0, 1: retired)
+                     (lib.OPT_WAVE_TWO, 0), (99, 1)):   # (SPARSE_BIG 0, 1 and WAVE_TWO 0: retired)
         assert s.lib.wf_set_option(s.h, opt, val) == lib.WF_E_BADINPUT
     s.close()
 
@@ -184,7 +184,7 @@ def test_cfg4_full_size(cfg4_full):
     records on a second pass, from four cost-balanced shards, with a 16 KB decision arena
     (round 2: WF_DEC_LDS=16384 produced WF_E_EMPTYMASK at this shape), with the dense
     workgroup decision's arena, with every staged decision in the segment-table form, and
-    with the round-3 hand-over flow; and the oracle's records on a 200-contig sample."""
+    without the triage; and the oracle's records on a 200-contig sample."""
     batch, tax = cfg4_full
     s = engine.GpuScorer(0)
     s.set_taxonomy(tax)
@@ -197,7 +197,7 @@ def test_cfg4_full_size(cfg4_full):
     s.close()
     assert_same(engine.Results.concat(parts, [int(batch.hit_off[x]) for x, _ in bounds]), a, batch)
     for kw in (dict(lds_bytes=16384), dict(options={lib.OPT_SPARSE_BIG: 2}),
-               dict(options={lib.OPT_WAVE_TWO: 0}), dict(options={lib.OPT_TRIAGE: 0})):
+               dict(options={lib.OPT_TRIAGE: 0})):
         c = score(batch, tax, **kw)
         assert not c.status.any(), kw
         assert_same(c, a, batch)

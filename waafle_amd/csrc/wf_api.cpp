@@ -48,7 +48,6 @@ struct wf_ctx {
   int mode = WF_MODE_LEVEL0;       // wf_set_mode
   int sparse_big = 3;              // wf_set_option(WF_OPT_SPARSE_BIG)
   int64_t att_limit = (int64_t(1) << 31) - 1;   // wf_set_option(WF_OPT_ATT_LIMIT)
-  int wave_two = 1;                // wf_set_option(WF_OPT_WAVE_TWO)
   int64_t dump_cap = 0;            // wf_set_option(WF_OPT_DUMP_CAP), 0: the default size
   int triage = 1;                  // wf_set_option(WF_OPT_TRIAGE)
   wf::StagedState* staged = nullptr;
@@ -269,9 +268,8 @@ int wf_set_option(wf_ctx* ctx, int option, int64_t value) {
         return fail(ctx, WF_E_BADINPUT, "WF_OPT_ATT_LIMIT %lld out of [1, 2^31 - 1]", (long long)value);
       ctx->att_limit = value;
       return WF_OK;
-    case WF_OPT_WAVE_TWO:
-      if (value < 0 || value > 1) return fail(ctx, WF_E_BADINPUT, "WF_OPT_WAVE_TWO is 0 or 1");
-      ctx->wave_two = (int)value;
+    case WF_OPT_WAVE_TWO:        // (0, the round-3 hand-over flow, retired in ABI 6)
+      if (value != 1) return fail(ctx, WF_E_BADINPUT, "WF_OPT_WAVE_TWO is 1 (0 is retired)");
       return WF_OK;
     case WF_OPT_DUMP_CAP:
       if (value < 0 || value > (int64_t(1) << 31) - 4096)
@@ -394,7 +392,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   if (!ctx->staged) ctx->staged = wf::staged_create(ctx->device);
   if (ctx->lds_set) wf::staged_set_lds(ctx->staged, ctx->lds_bytes);
   wf::staged_set_level0(ctx->staged, ctx->mode != WF_MODE_STAGED, ctx->mode == WF_MODE_WAVES);
-  wf::staged_set_options(ctx->staged, ctx->sparse_big, ctx->att_limit, ctx->wave_two, ctx->dump_cap,
+  wf::staged_set_options(ctx->staged, ctx->sparse_big, ctx->att_limit, ctx->dump_cap,
                          ctx->triage);
   std::pair<int, int> el{-1, -1};
   if (ctx->timing) {

@@ -202,7 +202,7 @@ void staged_set_lds(StagedState* st, int64_t bytes);
 // context options (include/waafle_hip.h wf_option): the segment-table decision for contigs
 // that outgrow the LDS arena, the attachments one call accepts (more: WF_E_TOOBIG), explain_two
 // and the roll-up levels in the first wave form, the hand-over buffer's size (0: default)
-void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap,
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int64_t dump_cap,
                         int triage);
 // per-phase timing (wf_phase): HIP events around each phase of each level, read back at the
 // end of every staged_score call into the accumulators (reset by staged_timing(st, on))

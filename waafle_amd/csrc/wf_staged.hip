@@ -1563,7 +1563,6 @@ struct StagedState {
   int sparse_res = -1;               // resident k_big_sparse waves per CU
   int two_res = -1;                  // resident k_dump_sparse<1> (compact tables) waves per CU
   int64_t att_limit = (int64_t(1) << 31) - 1;   // attachments per call (WF_OPT_ATT_LIMIT)
-  int wave_two = 1;                  // WF_OPT_WAVE_TWO: explain_two + roll-up levels in the wave form
   int64_t dump_cap = 0;              // WF_OPT_DUMP_CAP (0: max(32 N, 65536))
   int triage = 1;                    // WF_OPT_TRIAGE: level-0 triage before the first wave form
   Buf tri_list, tri_cnt;             // the contigs the triage hands on, and their count
@@ -1634,12 +1633,10 @@ void staged_set_lds(StagedState* st, int64_t bytes) {
   st->dec_lds_fixed = true;
 }
 
-void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int wave_two, int64_t dump_cap,
-                        int triage) {
+void staged_set_options(StagedState* st, int sparse_big, int64_t att_limit, int64_t dump_cap, int triage) {
   st->triage = triage;
   st->sparse_big = sparse_big;
   st->att_limit = att_limit;
-  st->wave_two = wave_two;
   st->dump_cap = dump_cap;
 }
 
@@ -1982,9 +1979,9 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     // assign-unknown row) over with their level-0 segment tables, every mean evaluated:
     // k_dump_sparse decides them from the table (pend 3 -> 0, 2 or 1)
     const bool dump = st->sparse_big != 0 && !st->rollup;
-    // Wave levels (WF_OPT_WAVE_TWO): the first form also decides explain_two and carries the
-    // roll-up levels, one launch per level over the contigs the level before raised
-    const bool levels = dump && st->wave_two;
+    // Wave levels: the first form also decides explain_two and carries the roll-up levels,
+    // one launch per level over the contigs the level before raised
+    const bool levels = dump;
     SArgs da = sa;
     unsigned long long* rcnt = nullptr;              // [kMaxIter + 2] per-level list counts, fail count
     if (dump) {
