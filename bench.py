@@ -101,17 +101,21 @@ def algorithmic_bytes(batch):
     return 24 * batch.n_hits + 12 * batch.n_loci + 16 * (N + 1) + 80 * N
 
 
-def k2_algorithmic(pair_evals, batch):
-    """SURVEY §8(d) counts for the isolated explain_two kernel, from the per-contig
-    reference-equivalent pair counts P_pot(P_pot-1)/2: B_k2 = sum P_pot*G*8 (the S rows
-    of the potential clades) and OPS_pair = sum pairs*G (this rank only)."""
+def k2_algorithmic(pair_evals, batch, ppot_sum=None):
+    """SURVEY §8(d) counts for the isolated explain_two kernel: B_k2 = sum over the explain_two
+    calls of P_pot*G*8 (the S rows of the potential clades; ppot_sum: the library's per-contig
+    sum of P_pot over its calls, one per roll-up level) and OPS_pair = sum pairs*G (this rank
+    only).  Without ppot_sum, P_pot is solved from the contig's summed pairs P_pot(P_pot-1)/2,
+    which undercounts contigs with explain_two at several levels."""
     sel = pair_evals > 0
     p = pair_evals[sel].astype(np.float64)
-    ppot = np.rint((1.0 + np.sqrt(1.0 + 8.0 * p)) / 2.0)
+    one = np.rint((1.0 + np.sqrt(1.0 + 8.0 * p)) / 2.0)   # (one call's P_pot from its pairs)
+    ppot = ppot_sum[sel].astype(np.float64) if ppot_sum is not None else one
     g = np.diff(batch.loc_off)[sel].astype(np.float64)
-    return {"contigs_explain_two": int(sel.sum()), "p_pot_max": int(ppot.max()) if p.size else 0,
+    return {"contigs_explain_two": int(sel.sum()), "p_pot_max": int(one.max()) if p.size else 0,
             "b_k2_bytes": float((ppot * g * 8.0).sum()), "ops_pair": float((p * g).sum()),
-            "pairs": float(p.sum())}
+            "pairs": float(p.sum()),
+            "b_k2_from": "ppot_sum (per call)" if ppot_sum is not None else "pairs (one call per contig)"}
 
 
 def file_sha(path):
@@ -256,7 +260,7 @@ class DeviceBatch:
     wf_result structs pointing at them.  `min_scov`: the packed hit_key (wf_batch.hit_key,
     built on the host with the arrays, as the CLI packs it at parse time) for that value."""
 
-    def __init__(self, batch, dev, min_scov=None):
+    def __init__(self, batch, dev, min_scov=None, ppot=False):
         import torch
         from waafle_amd import lib as L
         N, NH, NL = batch.n_contigs, batch.n_hits, batch.n_loci
@@ -279,12 +283,14 @@ class DeviceBatch:
             "n_meld2": e(N, torch.int32), "meld": e(2 * NH + 2 * N, torch.int32),
             "annot_hit": e(NL, torch.int32), "pair_evals": e(N, torch.int64),
             "status": e(N, torch.int32), "need_bytes": e(N, torch.int64)}
+        if ppot:                                     # wf_result.ppot_sum (the k2 leg's B_k2)
+            self.out["ppot_sum"] = e(N, torch.int64)
         self.bs = L.WfBatch(n_contigs=N, n_systems=1, n_hits=NH, n_loci=NL,
                             max_hits=batch.max_hits, max_loci=batch.max_loci,
                             device_resident=1, _pad=0,
                             **{f: C.c_void_p(self.d[f].data_ptr()) for f in self.d})
         self.keys_packed = min_scov is not None
-        self.rs = L.WfResult(**{f: C.c_void_p(self.out[f].data_ptr())
+        self.rs = L.WfResult(**{f: C.c_void_p(self.out[f].data_ptr()) if f in self.out else None
                                 for f, _ in L.WfResult._fields_})
 
     def host(self, f):
@@ -324,11 +330,11 @@ def timed_passes(so, h, chk, db, params, steps, warmup, dist, dev, cdev=None):
 def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=None, traffic_json=None):
     """The explain_two stress leg (BASELINE configs[4]) on this rank's cfg5 share."""
     import torch
-    db = DeviceBatch(kbatch, dev, params.min_scov)
+    db = DeviceBatch(kbatch, dev, params.min_scov, ppot=True)
     elapsed, tm = timed_passes(so, h, chk, db, params, steps, 1, dist, dev, cdev)
     pe = db.host("pair_evals")
     calls = db.host("call")
-    counts = k2_algorithmic(pe, kbatch)
+    counts = k2_algorithmic(pe, kbatch, db.host("ppot_sum"))
     del db
     torch.cuda.empty_cache()
     ph = tm.phases()
@@ -361,8 +367,11 @@ def k2_leg(so, h, chk, kbatch, params, steps, dist, dev, world, pmc_json, cdev=N
         "explain_two_phases_ms": {"decide": per("decide"), "big": per("big"),
                                   "handover": per("handover")},
         "other_phases_ms": {k: per(k) for k in ("waves", "attach", "segments")},
-        "b_k2_bytes": v[1], "b_k2_rule": "sum over explain_two contigs of P_pot * G * 8 "
-                                        "(SURVEY 8(d): the potential clades' score rows)",
+        "b_k2_bytes": v[1], "b_k2_rule": "sum over explain_two calls (every roll-up level) of "
+                                        "P_pot * G * 8 (SURVEY 8(d): the potential clades' score "
+                                        "rows; P_pot summed per contig by the library, "
+                                        "wf_result.ppot_sum)",
+        "b_k2_one_call_per_contig": k2_algorithmic(pe, kbatch)["b_k2_bytes"],
         "hbm": {"achieved_GBs": achieved, "peak_GBs": HBM_PEAK_GBS,
                 "frac": achieved / HBM_PEAK_GBS,
                 "rule": "sum of B_k2 over ranks / max explain_two time over ranks / "

@@ -178,6 +178,10 @@ typedef struct wf_result {
   int64_t* pair_evals;        /* [n] sum of P_pot*(P_pot-1)/2 over explain_two calls */
   int32_t* status;            /* [n] 0 or a WF_E_* code for this contig */
   int64_t* need_bytes;        /* [n] workspace bytes asked for when status == WF_E_NOMEM */
+  int64_t* ppot_sum;          /* [n] optional (NULL: not reported): sum of P_pot over the
+                                 explain_two calls that evaluate pairs (P_pot >= 2), one per
+                                 roll-up level -- the per-call sizes behind pair_evals, for
+                                 SURVEY 8(d)'s B_k2 = sum P_pot * G * 8 (ABI 6) */
 } wf_result;
 
 /* Pass timing accumulated while enabled: HIP events recorded on the context stream

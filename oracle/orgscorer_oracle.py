@@ -311,6 +311,7 @@ class ContigModel:
         self.best_two = None
         self.iterations = 0
         self.pair_evals = 0
+        self.ppot_sum = 0       # sum of len(pool) over the explain_two calls with pairs
 
     def add_loci(self, loci):
         """orgscorer.py:348-357 (names by start rank over ALL loci of the group)."""
@@ -461,6 +462,8 @@ def two_clade(C, tax):
     p = C.p
     pool = [c for c in _ordered(C.clades) if max(C.genes[c]) >= p.k2]
     C.pair_evals += len(pool) * (len(pool) - 1) // 2
+    if len(pool) >= 2:
+        C.ppot_sum += len(pool)
     opts = []
     for a in pool:
         for b in pool:
@@ -571,6 +574,7 @@ def evaluate_contig(C, tax, details=None):
     an ungrouped blastout is evaluated once per run and reports its last evaluation."""
     it = 1
     C.pair_evals = 0
+    C.ppot_sum = 0
     write_details(details, C, it)
     one = one_clade(C, tax)
     two = two_clade(C, tax) if not _ok(one) else None

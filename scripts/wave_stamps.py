@@ -97,9 +97,9 @@ def main():
     nt = max(1, t[15])
     out["triage"] = {"decided_sampled": t[15], "cycles_per_contig": sum(t[:9]) / nt,
                      "phases": {k: t[i] / nt for i, k in enumerate(TRIAGE_PHASES)}}
-    bg = (C.c_ulonglong * 24)()
+    bg = (C.c_ulonglong * 48)()
     so.wf_stamps_read_big.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    so.wf_stamps_read_big(bg, 24)
+    so.wf_stamps_read_big(bg, 48)
     b = [int(x) for x in bg]
     nb = max(1, b[15])
     out["sp_level"] = {"sampled": b[15], "cycles_per_contig": sum(b[:10]) / nb,
@@ -109,7 +109,11 @@ def main():
                                       "members": b[14] / nb},
                        "outcomes": {"declined: class table": b[16], "declined: class pairs": b[17],
                                     "explain_one": b[18]},
-                       "calls_by_level": {"0": b[19], "1": b[20], "2+": b[21]}}
+                       "calls_by_level": {"0": b[19], "1": b[20], "2+": b[21]},
+                       "levels_1_up": {"sampled": b[34],
+                                       "cycles_per_contig": sum(b[24:34]) / max(1, b[34]),
+                                       "phases": {k: b[24 + i] / max(1, b[34])
+                                                  for i, k in enumerate(SP_LEVEL_PHASES)}}}
     print(json.dumps(out))
     for p, d in out["phases"].items():
         print("{:24s} {:10.0f} cyc  {:5.1f}%".format(p, d["cycles_per_contig"], 100 * d["frac"]),

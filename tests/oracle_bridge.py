@@ -25,6 +25,7 @@ def oracle_results(contigs, batch, tax):
         mbase = 2 * int(batch.hit_off[c]) + 2 * c
         one, two = C.best_one, C.best_two
         res.pair_evals[c] = C.pair_evals
+        res.ppot_sum[c] = C.ppot_sum
         res.iterations[c] = C.iterations
         if one is not None and one.ok:
             res.call[c] = CALL_NO_LGT

@@ -29,7 +29,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(lib.WfParams) == 6 * 8 + 11 * 4 + 4
     assert lib.WfBatch.hit_off.offset == 40 and ctypes.sizeof(lib.WfBatch) == 40 + 13 * 8
     assert lib.WfBatch.hit_key.offset == 40 + 12 * 8
-    assert ctypes.sizeof(lib.WfResult) == 15 * 8
+    assert ctypes.sizeof(lib.WfResult) == 16 * 8 and lib.WfResult.ppot_sum.offset == 15 * 8
     assert lib.WfTaxonomy.parent.offset == 8 and lib.WfTaxonomy.root.offset == 40
 
 

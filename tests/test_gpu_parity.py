@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 CASES = gc.case_names()
 FIELDS = ("call", "crit", "rank", "clade1", "clade2", "direction", "synteny", "n_meld1",
-          "n_meld2", "annot_hit", "pair_evals", "iterations", "status")
+          "n_meld2", "annot_hit", "pair_evals", "ppot_sum", "iterations", "status")
 
 
 FORMS = {

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 PARAMS = cli.param_dict(cli.parse_flags([]))
 SCALARS = ("call", "crit", "rank", "clade1", "direction", "iterations", "n_meld1", "n_meld2",
-           "pair_evals", "status")
+           "pair_evals", "ppot_sum", "status")
 
 
 def meld_keys(res, batch):

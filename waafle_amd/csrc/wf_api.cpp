@@ -38,7 +38,7 @@ struct wf_ctx {
   DevBuf b_hit_off, b_qlo, b_qhi, b_taxon, b_hstrand, b_score, b_scov, b_sysmask;
   DevBuf b_loc_off, b_lstart, b_lend, b_lstrand, b_hkey;
   DevBuf r_call, r_crit, r_rank, r_c1, r_c2, r_dir, r_iters, r_syn, r_nm1, r_nm2, r_meld,
-      r_annot, r_pairs, r_status, r_need;
+      r_annot, r_pairs, r_status, r_need, r_ppot;
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -222,7 +222,7 @@ void wf_free(wf_ctx* ctx) {
                     &ctx->b_lstart, &ctx->b_lend, &ctx->b_lstrand, &ctx->r_call, &ctx->r_crit,
                     &ctx->r_rank, &ctx->r_c1, &ctx->r_c2, &ctx->r_dir, &ctx->r_iters,
                     &ctx->r_syn, &ctx->r_nm1, &ctx->r_nm2, &ctx->r_meld, &ctx->r_annot,
-                    &ctx->r_pairs, &ctx->r_status, &ctx->r_need};
+                    &ctx->r_pairs, &ctx->r_status, &ctx->r_need, &ctx->r_ppot};
   for (DevBuf* b : bufs) release(*b);
   if (ctx->staged) wf::staged_destroy(ctx->staged);
   for (hipEvent_t ev : ctx->ev_pool) (void)hipEventDestroy(ev);
@@ -404,6 +404,7 @@ static int run_kernels(wf_ctx* ctx, wf::KArgs& K, const wf_batch* b) {
   const int rc = wf::staged_score(ctx->staged, K, ctx->tax_n, b->max_loci, b->max_hits, b->n_hits, b->n_loci, ctx->stream,
                                   &err, ctx->details_on ? &ctx->det : nullptr);
   if (rc) return fail(ctx, rc == -1 ? WF_E_BADINPUT : (rc == WF_E_TOOBIG ? WF_E_TOOBIG : WF_E_HIP), "%s", err.c_str());
+  HIP_TRY(ctx, wf::finish_ppot(K, ctx->stream));
   if (el.first >= 0) HIP_TRY(ctx, hipEventRecord(ctx->ev_pool[el.second], ctx->stream));
   ++ctx->launches;
   return WF_OK;
@@ -434,7 +435,7 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
     K.call = r->call; K.crit = r->crit; K.rank = r->rank; K.c1 = r->clade1; K.c2 = r->clade2;
     K.dir = r->direction; K.iters = r->iterations; K.syn = r->synteny; K.nm1 = r->n_meld1;
     K.nm2 = r->n_meld2; K.meld = r->meld; K.annot = r->annot_hit; K.pair_evals = r->pair_evals;
-    K.status = r->status; K.need = r->need_bytes;
+    K.status = r->status; K.need = r->need_bytes; K.ppot = r->ppot_sum;
     return run_kernels(ctx, K, b);
   }
 
@@ -469,6 +470,8 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
       (rc = alloc_out(ctx, ctx->r_status, N, &K.status)) ||
       (rc = alloc_out(ctx, ctx->r_need, N, &K.need)))
     return rc;
+  K.ppot = nullptr;
+  if (r->ppot_sum && (rc = alloc_out(ctx, ctx->r_ppot, N, &K.ppot))) return rc;
   if ((rc = run_kernels(ctx, K, b))) return rc;
   if ((rc = download(ctx, r->status, K.status, N)) || (rc = download(ctx, r->need_bytes, K.need, N)))
     return rc;
@@ -483,6 +486,7 @@ int wf_score(wf_ctx* ctx, const wf_batch* b, const wf_params* p, wf_result* r) {
       (rc = download(ctx, r->annot_hit, K.annot, n_annot)) ||
       (rc = download(ctx, r->pair_evals, K.pair_evals, N)))
     return rc;
+  if (K.ppot && (rc = download(ctx, r->ppot_sum, K.ppot, N))) return rc;
   HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
   for (int32_t c = 0; c < b->n_contigs; ++c)
     if (r->status[c] != 0)

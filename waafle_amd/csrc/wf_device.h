@@ -23,6 +23,16 @@ constexpr uint64_t kKeyPad = ~0ull;
 #include "wf_stamps.h"
 constexpr int kLocVirtual = 0xFFFF;     // locus field of the virtual "Unknown" key
 
+// wf_result.ppot_sum: P_pot of an explain_two call that evaluates pairs (P_pot >= 2, the
+// calls behind pair_evals), once per (contig, iteration) -- a form that declines a contig
+// after counting, and the one that then decides it, count it once.  One thread calls it.
+__device__ __forceinline__ void note_ppot(const KArgs& K, int c, int iteration, int Pp) {
+  if (!K.ppot || Pp < 2) return;
+  const uint64_t old = (uint64_t)K.ppot[c];
+  if ((int)(old >> 40) != iteration)
+    K.ppot[c] = (int64_t)(((uint64_t)iteration << 40) | ((old & ((1ull << 40) - 1ull)) + (uint64_t)Pp));
+}
+
 struct Ctl {
   int A, A1, npow, S_n, P, Gu, Pp;
   int overflow, status, cnt, cnt2, p_unk, root_present, all_ignored;
@@ -1825,6 +1835,7 @@ __device__ __forceinline__ int decide_two(const KArgs& K, const Contig& C, Ctl& 
     for (int p = pb0; p < pe0; ++p)
       if (potential(p)) C.pot[pos++] = p;
     pair_evals += (int64_t)Pp * (Pp - 1) / 2;
+    if (threadIdx.x == 0) note_ppot(K, c, iteration, Pp);
     STAMP_SYNC();
     STAMP(16);
     const bool use_mask = Gu <= 64;

@@ -478,6 +478,7 @@ __device__ __noinline__ int wave_two(const SArgs& S, WaveSmem<CAP, true>& F, int
   }
   root = __ballot(root) != 0ull;
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
+  if (lane == 0) note_ppot(K, c, iteration, Pp);
   if (Pp > kPot0 || Pp * G > kS0 || Pn > CAP) return -1;
   // pass B: rows (potential clades first, clade order), S rows, sister data
   double* Sm = F.S();

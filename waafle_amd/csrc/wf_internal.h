@@ -45,6 +45,9 @@ struct KArgs {
   int8_t* call; double* crit; double* rank; int32_t* c1; int32_t* c2; int8_t* dir;
   int16_t* iters; uint8_t* syn; int32_t* nm1; int32_t* nm2; int32_t* meld; int32_t* annot;
   int64_t* pair_evals; int32_t* status; int64_t* need;
+  int64_t* ppot;                 // wf_result.ppot_sum (optional): bits 0-39 the sum, 40-47 the
+                                 // iteration last counted (a level counted once, whichever form
+                                 // decides it)
   // HBM decision slots for contigs whose state outgrows the LDS arena (k_decide_big)
   char* big_ws; int64_t slot_bytes;
 };
@@ -180,6 +183,7 @@ struct StagedState;
 // the full clades), kPendTriage for the rest, which the first wave form then runs (list).
 constexpr int kPendTriage = 9;
 hipError_t pack_keys(const KArgs& k, int64_t n_hits, uint32_t* key, int cus, hipStream_t s);
+hipError_t finish_ppot(const KArgs& k, hipStream_t s);   // strips the iteration tags of K.ppot
 hipError_t launch_triage(const SArgs& sa, int64_t* ccnt, int64_t* cleaves, int32_t* pend, int max_hits, int cus,
                          hipStream_t s);
 // the first wave form over `list` (length *n_dev, on the device) at level 0

@@ -459,6 +459,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
   BSTAT(15, 1);
   BSTAT(12, se - so);
   BSTAT(19 + min(level, 2), 1);
+  if (level > 0) BSTAT(34, 1);
 
   // ---- pass 1: per-locus maxes over known clades, root present (:407-411) -------------
   sh.mx[lane] = 0;
@@ -663,6 +664,7 @@ __device__ __forceinline__ bool sp_level(const SArgs& S, SpShared& sh, char* ws,
 
   // ---- explain_two (:599-619) --------------------------------------------------------
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
+  if (lane == 0) note_ppot(K, c, iteration, Pp);
   if (sh.n_used * 4 > kSpCls * 3) {                // too many classes for the table
     BSTAT(16, 1);
     return false;
@@ -1208,6 +1210,7 @@ __device__ __forceinline__ bool sp_two(const SArgs& S, E2Shared& sh, int c, int 
   SSTAT(10, Pp);
   const uint64_t my_pm = lane < Pp ? sh.pm[lane] : 0ull;   // (cand overwrites pm and cg)
   pair_evals += (int64_t)Pp * (Pp - 1) / 2;
+  if (lane == 0) note_ppot(K, c, iteration, Pp);
   // the candidate pairs, crit >= k2 <=> (m_i | m_j) == um, listed so that their ranks are
   // taken 64 at a time (one pair per lane): the Pp (Pp - 1) / 2 pairs are tested 64 at a
   // time too, pair p = j (j - 1) / 2 + i (i < j) on lane p mod 64, the two masks fetched

@@ -92,6 +92,7 @@ __global__ void k_init(const KArgs K) {
   K.crit[c] = 0.0; K.rank[c] = 0.0; K.c1[c] = -1; K.c2[c] = -1; K.dir[c] = 0;
   K.iters[c] = 0; K.nm1[c] = 0; K.nm2[c] = 0; K.pair_evals[c] = 0; K.status[c] = 0;
   K.need[c] = 0;
+  if (K.ppot) K.ppot[c] = 0;
 }
 
 // Hits -> attachments, one workgroup per contig (grid-stride).  The contig's loci are
@@ -1506,7 +1507,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_decide_big(const SArgs S, int lev
 
 #include "wf_sparse.h"
 WF_STAMP_READER(sparse, g_sstamps, 16)
-WF_STAMP_READER(big, g_bstamps, 24)
+WF_STAMP_READER(big, g_bstamps, 48)
 
 int bits_for(int64_t v) {   // bits to hold values 0..v
   int b = 1;
@@ -2467,6 +2468,17 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     n_keys = (int64_t)(st->host_counters[0] & ((1ull << 40) - 1));
   }
   return 0;
+}
+
+__global__ void k_ppot_strip(int64_t* ppot, int n) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < n) ppot[c] &= (int64_t(1) << 40) - 1;
+}
+
+hipError_t finish_ppot(const KArgs& k, hipStream_t s) {
+  if (!k.ppot || k.n_contigs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ppot_strip, dim3((unsigned)((k.n_contigs + 255) / 256)), dim3(256), 0, s, k.ppot, k.n_contigs);
+  return hipGetLastError();
 }
 
 int staged_score(StagedState* st, const KArgs& k, int n_tax, int max_loci, int max_hits, int64_t NH, int64_t NL,

@@ -75,12 +75,17 @@ __device__ unsigned long long g_sstamps[16];
   } while (0)
 #define SSTAT(i, v) do { if (ssamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_sstamps[i], (unsigned long long)(v)); } while (0)
 // ... and of sp_level (k_big_sparse, k_dump_sparse<0>) on every 8th contig
-__device__ unsigned long long g_bstamps[24];
+// (slots 0-23 every contig-level; 24-33 the phases again for roll-up levels >= 1 alone, 34
+// their sampled count; `level` is sp_level's)
+__device__ unsigned long long g_bstamps[48];
 #define BLAP_MARK(c) unsigned long long blap_ = __builtin_amdgcn_s_memtime(); const bool bsamp_ = ((c) & 7) == 0
 #define BLAP(i)                                                                     \
   do {                                                                              \
     const unsigned long long n_ = __builtin_amdgcn_s_memtime();                     \
-    if (bsamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_bstamps[i], n_ - blap_);    \
+    if (bsamp_ && (threadIdx.x & 63) == 0) {                                        \
+      atomicAdd(&g_bstamps[i], n_ - blap_);                                         \
+      if (level > 0) atomicAdd(&g_bstamps[24 + (i)], n_ - blap_);                   \
+    }                                                                               \
     blap_ = n_;                                                                     \
   } while (0)
 #define BSTAT(i, v) do { if (bsamp_ && (threadIdx.x & 63) == 0) atomicAdd(&g_bstamps[i], (unsigned long long)(v)); } while (0)

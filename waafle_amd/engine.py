@@ -57,6 +57,7 @@ class Results:
     pair_evals: np.ndarray
     status: np.ndarray
     need_bytes: np.ndarray
+    ppot_sum: np.ndarray = None    # sum of P_pot over the explain_two calls with pairs (B_k2)
 
     @classmethod
     def empty(cls, n, n_hits, n_loci, n_sys):
@@ -68,7 +69,7 @@ class Results:
                    meld=np.zeros(2 * n_hits + 2 * n, np.int32),
                    annot_hit=np.zeros(n_loci * n_sys, np.int32),
                    pair_evals=np.zeros(n, np.int64), status=np.zeros(n, np.int32),
-                   need_bytes=np.zeros(n, np.int64))
+                   need_bytes=np.zeros(n, np.int64), ppot_sum=np.zeros(n, np.int64))
 
     def struct(self):
         return L.WfResult(*[L.ptr(getattr(self, f)) for f, _ in L.WfResult._fields_])

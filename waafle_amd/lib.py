@@ -55,7 +55,7 @@ class WfResult(C.Structure):
     _fields_ = [("call", _P), ("crit", _P), ("rank", _P), ("clade1", _P), ("clade2", _P),
                 ("direction", _P), ("iterations", _P), ("synteny", _P), ("n_meld1", _P),
                 ("n_meld2", _P), ("meld", _P), ("annot_hit", _P), ("pair_evals", _P),
-                ("status", _P), ("need_bytes", _P)]
+                ("status", _P), ("need_bytes", _P), ("ppot_sum", _P)]
 
 
 class WfTiming(C.Structure):
