@@ -24,12 +24,14 @@ constexpr uint64_t kKeyPad = ~0ull;
 constexpr int kLocVirtual = 0xFFFF;     // locus field of the virtual "Unknown" key
 
 // wf_result.ppot_sum: P_pot of an explain_two call that evaluates pairs (P_pot >= 2, the
-// calls behind pair_evals), once per (contig, iteration) -- a form that declines a contig
-// after counting, and the one that then decides it, count it once.  One thread calls it.
+// calls behind pair_evals), once per (contig, iteration).  Every form takes a contig's levels
+// in increasing order, and a contig a form hands on is taken again from level 0 or from the
+// level it stopped at (same data, same P_pot): so an iteration at or below the last one
+// counted is a repeat.  One thread calls it.
 __device__ __forceinline__ void note_ppot(const KArgs& K, int c, int iteration, int Pp) {
   if (!K.ppot || Pp < 2) return;
   const uint64_t old = (uint64_t)K.ppot[c];
-  if ((int)(old >> 40) != iteration)
+  if (iteration > (int)(old >> 40))
     K.ppot[c] = (int64_t)(((uint64_t)iteration << 40) | ((old & ((1ull << 40) - 1ull)) + (uint64_t)Pp));
 }
 

@@ -46,8 +46,8 @@ struct KArgs {
   int16_t* iters; uint8_t* syn; int32_t* nm1; int32_t* nm2; int32_t* meld; int32_t* annot;
   int64_t* pair_evals; int32_t* status; int64_t* need;
   int64_t* ppot;                 // wf_result.ppot_sum (optional): bits 0-39 the sum, 40-47 the
-                                 // iteration last counted (a level counted once, whichever form
-                                 // decides it)
+                                 // highest iteration counted (a level counted once, whichever
+                                 // form decides it)
   // HBM decision slots for contigs whose state outgrows the LDS arena (k_decide_big)
   char* big_ws; int64_t slot_bytes;
 };
