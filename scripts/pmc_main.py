@@ -32,7 +32,11 @@ def main():
         acc[m.group(1) if m else r["Kernel_Name"][:40]][r["Counter_Name"]] += float(r["Counter_Value"])
     per = {k: {c: x / passes for c, x in v.items()} for k, v in acc.items()}
     total = sum(v.get("SQ_INSTS_VALU", 0.0) for v in per.values())
-    dom = per.get(dominant, {})
+    dom = collections.defaultdict(float)            # every instantiation of the dominant kernel
+    for k, v in per.items():
+        if k == dominant or k.startswith(dominant + "<"):
+            for c, x in v.items():
+                dom[c] += x
     res = {"config": config, "contigs": contigs, "passes": passes,
            "valu_insts_per_pass": total,
            "salu_insts_per_pass": sum(v.get("SQ_INSTS_SALU", 0.0) for v in per.values()),

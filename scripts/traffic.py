@@ -52,7 +52,8 @@ def per_pass(d, counter, passes, dominant, by_kernel):
             continue     # pass = our kernels + device sorts/scans (runtime fills/copies not counted)
         acc[r["Dispatch_Id"]] += float(r["Counter_Value"])
         by_kernel[kname(r["Kernel_Name"])][counter] += float(r["Counter_Value"]) / passes
-        if kname(r["Kernel_Name"]) == dominant:
+        k = kname(r["Kernel_Name"])
+        if k == dominant or k.startswith(dominant + "<"):     # (every instantiation of it)
             dom += float(r["Counter_Value"])
     assert acc, "no {} rows".format(counter)
     return sum(acc.values()) / passes, len(acc), dom / passes
