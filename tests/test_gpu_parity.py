@@ -31,8 +31,9 @@ FORMS = {
     "level0": dict(mode="level0"),
     # the same without the level-0 triage (wf_triage.hip): the wave form runs every contig
     "notriage": dict(mode="level0", options={lib.OPT_TRIAGE: 0}),
-    # a hand-over buffer of 96 entries: the contigs past it take the staged kernels
-    "dumpcap": dict(mode="level0", options={lib.OPT_DUMP_CAP: 96}),
+    # a hand-over buffer of 96 entries: the contigs past it take the staged kernels; the
+    # caller's packed hit_key (numpy) instead of the library's (k_pack_keys)
+    "dumpcap": dict(mode="level0", options={lib.OPT_DUMP_CAP: 96}, host_keys=True),
     "waves": dict(mode="waves"),
     "staged": dict(mode="staged"),
     # every staged decision from the segment table (k_big_sparse, wf_sparse.h)

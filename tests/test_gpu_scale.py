@@ -303,7 +303,7 @@ def test_pruned_forms_agree_with_staged(lgt_heavy, flags):
 @pytest.mark.parametrize("flags", [[], ["--min-scov", "0.9"], ["--stranded"]],
                          ids=["default", "min-scov_0p9", "stranded"])
 def test_packed_hit_key_equals_library_packed_and_is_checked(flags):
-    """wf_batch.hit_key (ABI 6): the engine's packed words (numpy, parse time) and the
+    """wf_batch.hit_key (ABI 6): the caller's packed words (numpy, lib.pack_hit_keys) and the
     library's own packing (hit_key NULL: k_pack_keys before the triage) give the same
     records; a host batch whose key disagrees with its arrays (packed for another
     --min-scov) is refused with WF_E_BADINPUT before any launch."""
@@ -312,9 +312,9 @@ def test_packed_hit_key_equals_library_packed_and_is_checked(flags):
     params = cli.param_dict(cli.parse_flags(flags))
     s = engine.GpuScorer(0)
     s.set_taxonomy(tax)
-    got = s.score(batch, params)
+    got = s.score(batch, params)                               # hit_key NULL
     res = engine.Results.empty(batch.n_contigs, batch.n_hits, batch.n_loci, len(batch.systems))
-    bs, rs = engine.batch_struct(batch), res.struct()          # hit_key NULL
+    bs, rs = engine.batch_struct(batch, float(params["min_scov"])), res.struct()
     ps = engine.params_struct(params)
     import ctypes as C
     assert s.lib.wf_score(s.h, C.byref(bs), C.byref(ps), C.byref(rs)) == lib.WF_OK

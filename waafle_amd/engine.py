@@ -127,9 +127,12 @@ def rebase_error(err, first):
 
 class GpuScorer:
     """One libwaafle_hip context on one device.  `options`: {wf_option: value}
-    (lib.OPT_*), e.g. {lib.OPT_ATT_LIMIT: n} to make wf_score split smaller batches."""
+    (lib.OPT_*), e.g. {lib.OPT_ATT_LIMIT: n} to make wf_score split smaller batches.
+    `host_keys`: pass the numpy-packed wf_batch.hit_key with the host arrays (a test form:
+    the library packs it on the device faster than it checks a host one)."""
 
-    def __init__(self, device=0, lds_bytes=None, mode=None, options=None):
+    def __init__(self, device=0, lds_bytes=None, mode=None, options=None, host_keys=False):
+        self.host_keys = host_keys
         self.lib = L.load()
         h = C.c_void_p()
         rc = self.lib.wf_init(int(device), C.byref(h))
@@ -177,7 +180,11 @@ class GpuScorer:
 
     def _score_once(self, batch, params):
         res = Results.empty(batch.n_contigs, batch.n_hits, batch.n_loci, len(batch.systems))
-        bs, ps, rs = batch_struct(batch, float(params["min_scov"])), params_struct(params), res.struct()
+        # host arrays: no hit_key by default (the library packs it on the device in well under
+        # a millisecond; a host key costs 4 B/hit more H2D and the library's host check of it
+        # -- scope (ii) 0.25 -> 0.40 s at cfg4).  Device-resident callers pass it (bench.py).
+        ms = float(params["min_scov"]) if self.host_keys else None
+        bs, ps, rs = batch_struct(batch, ms), params_struct(params), res.struct()
         rc = self.lib.wf_score(self.h, C.byref(bs), C.byref(ps), C.byref(rs))
         if rc != L.WF_OK:
             bad = np.nonzero(res.status)[0]
