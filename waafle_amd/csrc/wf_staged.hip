@@ -412,24 +412,123 @@ constexpr int kRadixBins = 1 << kRadixBits;
 // buffers, the per-wave digit counts -- 80 KB at cap 6,144 (two workgroups per CU), 104 KB at 8,192
 inline size_t radix_lds(int cap) { return (size_t)cap * 2 * (4 + 2) + (size_t)(kRadixNT / 64) * kRadixBins * 4 + 64; }
 
+// The sort's LDS (dynamic, radix_lds(cap) bytes): the ping-pong key and index buffers and
+// the per-wave digit counts
+struct RadixLds {
+  uint32_t* kb0;
+  uint16_t* ib0;
+  int* cnt;                                            // [wave][bin]
+  int cap;
+  __device__ RadixLds(char* smem, int cap_)
+      : kb0(reinterpret_cast<uint32_t*>(smem)), ib0(reinterpret_cast<uint16_t*>(smem + 8 * (size_t)cap_)),
+        cnt(reinterpret_cast<int*>(smem + 12 * (size_t)cap_)), cap(cap_) {}
+  __device__ uint32_t* kb(int x) const { return kb0 + x * cap; }   // buffer x of the pair
+  __device__ uint16_t* ib(int x) const { return ib0 + x * cap; }
+};
+
+// One contig's n > 0 attachments [a0, a0 + n) sorted by key in LDS (the whole workgroup);
+// returns the buffer holding the sorted keys and their contig-local indices.
+__device__ __forceinline__ int radix_sort_contig(const SArgs& S, int64_t a0, int n, const RadixLds& R, int* s_red) {
+  constexpr int kW = kRadixNT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int kbits = S.key_tb + S.key_lb;              // (<= 32: checked on the host)
+  int* const cnt = R.cnt;
+  // (the attachments' clade and locus loads of four strides issued together)
+  for (int i0 = 0; i0 < n; i0 += 4 * kRadixNT) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + r * kRadixNT + tid;
+      kk[r] = i < n ? (uint32_t)make_key(S, 0, (int)(a0 + i)) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + r * kRadixNT + tid;
+      if (i < n) {
+        R.kb(0)[i] = kk[r];
+        R.ib(0)[i] = (uint16_t)i;
+      }
+    }
+  }
+  // wave w's slice [lo, hi) of the elements
+  const int per = (n + kW - 1) / kW;
+  const int lo = min(n, w * per), hi = min(n, lo + per);
+  int cur = 0;
+  for (int shift = 0; shift < kbits; shift += kRadixBits) {
+    for (int i = tid; i < kW * kRadixBins; i += kRadixNT) cnt[i] = 0;
+    __syncthreads();
+    // the lanes of this chunk with the same digit (d), from 8 ballots
+    auto group = [&](int i, int& d) -> uint64_t {
+      const bool live = i < hi;
+      d = live ? (int)((R.kb(cur)[i] >> shift) & (kRadixBins - 1)) : 0;
+      uint64_t m = __ballot(live);
+#pragma unroll
+      for (int b = 0; b < kRadixBits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1);
+        m &= ((d >> b) & 1) ? bal : ~bal;
+      }
+      return live ? m : 0ull;
+    };
+    for (int i0 = lo; i0 < hi; i0 += 64) {           // per-wave digit counts
+      int d;
+      const uint64_t m = group(i0 + lane, d);
+      if (m && (m & below) == 0ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's first lane)
+    }
+    __syncthreads();
+    // offsets: digit-major, wave-minor (thread d walks the waves of digit d, then a scan of
+    // the digit totals across the block)
+    int tot = 0;
+    if (tid < kRadixBins)
+      for (int x = 0; x < kW; ++x) {
+        const int v = cnt[x * kRadixBins + tid];
+        cnt[x * kRadixBins + tid] = tot;
+        tot += v;
+      }
+    // exclusive scan of the 256 digit totals (threads 0..255 = waves 0..3)
+    int incl = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) s_red[w] = incl;
+    __syncthreads();
+    if (tid < kRadixBins) {
+      int pre = incl - tot;
+      for (int x = 0; x < w; ++x) pre += s_red[x];
+      for (int x = 0; x < kW; ++x) cnt[x * kRadixBins + tid] += pre;
+    }
+    __syncthreads();
+    // scatter, each wave its chunks in order (stable)
+    for (int i0 = lo; i0 < hi; i0 += 64) {
+      int d;
+      const uint64_t m = group(i0 + lane, d);
+      if (m) {
+        const int pos = cnt[w * kRadixBins + d] + __popcll(m & below);
+        R.kb(cur ^ 1)[pos] = R.kb(cur)[i0 + lane];
+        R.ib(cur ^ 1)[pos] = R.ib(cur)[i0 + lane];
+      }
+      wave_sync();                                   // (reads of the counts before the update)
+      if (m && (m >> lane) == 1ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's last lane)
+      wave_sync();
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  return cur;
+}
+
 __global__ __launch_bounds__(kRadixNT) void k_sort_radix(const SArgs S, int n_act, int level, uint64_t* keys,
                                                        int32_t* vals) {
   int64_t n_keys_ = 0;
   lvl_counts(S, n_act, n_keys_);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int cap = S.sort_cap;                          // (the level's largest contig, rounded up)
-  uint32_t* const kb0 = reinterpret_cast<uint32_t*>(smem);
-  uint16_t* const ib0 = reinterpret_cast<uint16_t*>(smem + 8 * (size_t)cap);
-  // buffer x of the ping-pong pair (keys, indices)
-  auto kb = [&](int x) { return kb0 + x * cap; };
-  auto ib = [&](int x) { return ib0 + x * cap; };
-  int* cnt = reinterpret_cast<int*>(smem + 12 * (size_t)cap);    // [wave][bin]
+  const RadixLds R(smem, S.sort_cap);                  // (the level's largest contig, rounded up)
   __shared__ int s_red[kRadixNT / 64];
   constexpr int kW = kRadixNT / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint64_t below = (1ull << lane) - 1ull;
-  const int kbits = S.key_tb + S.key_lb;              // (<= 32: checked on the host)
-  const uint64_t rank_shift = (uint64_t)kbits;
+  const uint64_t rank_shift = (uint64_t)(S.key_tb + S.key_lb);
   for (int cr = blockIdx.x; cr < n_act; cr += gridDim.x) {
     const int c = S.act ? S.act[cr] : cr;
     const int64_t a0 = S.catt_off[c], a1 = S.catt_off[c + 1];
@@ -439,95 +538,14 @@ __global__ __launch_bounds__(kRadixNT) void k_sort_radix(const SArgs S, int n_ac
       if (tid == 0) S.seg_cnt[cr] = 0;
       continue;
     }
-    // (the attachments' clade and locus loads of four strides issued together)
-    for (int i0 = 0; i0 < n; i0 += 4 * kRadixNT) {
-      uint32_t kk[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + r * kRadixNT + tid;
-        kk[r] = i < n ? (uint32_t)make_key(S, 0, (int)(a0 + i)) : 0u;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + r * kRadixNT + tid;
-        if (i < n) {
-          kb(0)[i] = kk[r];
-          ib(0)[i] = (uint16_t)i;
-        }
-      }
-    }
-    // wave w's slice [lo, hi) of the elements
-    const int per = (n + kW - 1) / kW;
-    const int lo = min(n, w * per), hi = min(n, lo + per);
-    int cur = 0;
-    for (int shift = 0; shift < kbits; shift += kRadixBits) {
-      for (int i = tid; i < kW * kRadixBins; i += kRadixNT) cnt[i] = 0;
-      __syncthreads();
-      // the lanes of this chunk with the same digit (d), from 8 ballots
-      auto group = [&](int i, int& d) -> uint64_t {
-        const bool live = i < hi;
-        d = live ? (int)((kb(cur)[i] >> shift) & (kRadixBins - 1)) : 0;
-        uint64_t m = __ballot(live);
-#pragma unroll
-        for (int b = 0; b < kRadixBits; ++b) {
-          const uint64_t bal = __ballot((d >> b) & 1);
-          m &= ((d >> b) & 1) ? bal : ~bal;
-        }
-        return live ? m : 0ull;
-      };
-      for (int i0 = lo; i0 < hi; i0 += 64) {           // per-wave digit counts
-        int d;
-        const uint64_t m = group(i0 + lane, d);
-        if (m && (m & below) == 0ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's first lane)
-      }
-      __syncthreads();
-      // offsets: digit-major, wave-minor (thread d walks the waves of digit d, then a scan of
-      // the digit totals across the block)
-      int tot = 0;
-      if (tid < kRadixBins)
-        for (int x = 0; x < kW; ++x) {
-          const int v = cnt[x * kRadixBins + tid];
-          cnt[x * kRadixBins + tid] = tot;
-          tot += v;
-        }
-      // exclusive scan of the 256 digit totals (threads 0..255 = waves 0..3)
-      int incl = tot;
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
-      }
-      if (lane == 63) s_red[w] = incl;
-      __syncthreads();
-      if (tid < kRadixBins) {
-        int pre = incl - tot;
-        for (int x = 0; x < w; ++x) pre += s_red[x];
-        for (int x = 0; x < kW; ++x) cnt[x * kRadixBins + tid] += pre;
-      }
-      __syncthreads();
-      // scatter, each wave its chunks in order (stable)
-      for (int i0 = lo; i0 < hi; i0 += 64) {
-        int d;
-        const uint64_t m = group(i0 + lane, d);
-        if (m) {
-          const int pos = cnt[w * kRadixBins + d] + __popcll(m & below);
-          kb(cur ^ 1)[pos] = kb(cur)[i0 + lane];
-          ib(cur ^ 1)[pos] = ib(cur)[i0 + lane];
-        }
-        wave_sync();                                   // (reads of the counts before the update)
-        if (m && (m >> lane) == 1ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's last lane)
-        wave_sync();
-      }
-      __syncthreads();
-      cur ^= 1;
-    }
+    const int cur = radix_sort_contig(S, a0, n, R, s_red);
     int ns = 0;                                      // distinct keys = segments
     const uint64_t crank_bits = (uint64_t)cr << rank_shift;
     for (int t = tid; t < n; t += kRadixNT) {
-      const uint32_t k = kb(cur)[t];
+      const uint32_t k = R.kb(cur)[t];
       keys[base + t] = crank_bits | (uint64_t)k;
-      vals[base + t] = (int)(a0 + (int64_t)ib(cur)[t]);
-      ns += (t == 0 || k != kb(cur)[t - 1]) ? 1 : 0;
+      vals[base + t] = (int)(a0 + (int64_t)R.ib(cur)[t]);
+      ns += (t == 0 || k != R.kb(cur)[t - 1]) ? 1 : 0;
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ns += __shfl_xor(ns, off, 64);
@@ -813,14 +831,97 @@ __global__ void k_seg_spans(const SArgs S, int64_t n_keys, int32_t* span_cnt, in
   span_cnt[s] = any ? cnt : -1;
 }
 
-template <bool THREAD_MEAN>
+struct RecAtt {
+  int2 x;                                            // site range [lo, hi)
+  double sc;
+};
+
+// One segment's mean or record (k_seg_rec's per-segment body): its na attachments are get(t),
+// t < na, in sorted order; a record's attachments are written through put(k, att) (the list
+// the wave / leaf kernels read at sorted positions kb...; in_place: get(t) already reads
+// position kb + t, so only moved entries are written).  One run: the exact mean into
+// seg_mean[s]; else seg_rec[s] and, for 5..64 attachments of a short locus, to_wave
+// (k_seg_wave).  Returns the segment's leaves for the leaf kernels (0: finished here or by
+// k_seg_wave).
+template <class Get, class Put>
+__device__ __forceinline__ int seg_record(const SArgs& S, int64_t s, int kb, int na, int len, Get get, Put put,
+                                          bool in_place, bool& to_wave) {
+  int nl = (len / kNpyBuf) * lut_count(S, kNpyBuf) + lut_count(S, len % kNpyBuf);
+  int lo = 0, hi = 0;
+  double v = 0.0;
+  bool one_run = false, listed = in_place;           // listed: the record's list is in place
+  const bool thread_ok = len < kNpyBuf && nl <= kThreadLeaves;
+  to_wave = false;
+  if (na == 1) {
+    if (thread_ok) {
+      const RecAtt t = get(0);
+      lo = t.x.x; hi = t.x.y; v = t.sc;
+      one_run = true;
+    }
+  } else if (na <= kPruneMax) {
+    double F = 0.0;                                  // best whole-locus attachment
+#pragma unroll 4
+    for (int t = 0; t < na; ++t) {
+      const RecAtt e = get(t);
+      if (e.x.x <= 0 && e.x.y >= len && e.sc > F) F = e.sc;
+    }
+    // attachments at or below F (or empty) change no site: the envelope is
+    // max(F, the others).  None left: one run of F.  Otherwise the survivors are
+    // compacted, with F as one whole-locus attachment after them, so the leaf
+    // kernel sees few attachments (usually <= kRegAtt: register path).
+    int kept = 0;
+#pragma unroll 4
+    for (int t = 0; t < na; ++t) {
+      const RecAtt e = get(t);
+      if (e.x.x < e.x.y && e.sc > F) {
+        if (!in_place || kept != t) put(kept, e);
+        ++kept;
+      }
+    }
+    if (kept == 0 && thread_ok) {
+      lo = 0; hi = len; v = F; one_run = true;
+    } else {
+      // F > 0 came from an attachment that was not kept (its score is F), so the list
+      // never grows; it may have shifted, so F is always re-appended
+      if (F > 0.0) {
+        put(kept, RecAtt{make_int2(0, len), F});
+        ++kept;
+      }
+      na = kept;
+      listed = true;
+    }
+  }
+  if (one_run) {
+    S.seg_mean[s] = one_run_mean(PtrLut{S.lut + S.lut_off[len]}, nl, len, lo, hi, v);
+    return 0;
+  }
+  if (!listed)
+    for (int t = 0; t < na; ++t) put(t, get(t));
+  S.seg_rec[s] = make_int4(kb, na, len, nl);
+  // many attachments (higher roll-up levels): one wave per segment (k_seg_wave)
+  to_wave = na > kRegAtt && na <= 64 && nl <= 64 && len < kNpyBuf;
+  return to_wave ? 0 : nl;
+}
+
+// the segments k_seg_rec / k_front_radix hand to k_seg_wave: one list append per wave
+__device__ __forceinline__ void wave_list_add(const SArgs& S, int64_t s, bool to_wave) {
+  const uint64_t bm = __ballot(to_wave);
+  if (bm) {
+    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(bm);
+    int base = 0;
+    if (lane == leader) base = (int)atomicAdd(&S.counters[7], (unsigned long long)__popcll(bm));
+    base = __shfl(base, leader, 64);
+    if (to_wave) S.wave_list[base + __popcll(bm & ((1ull << lane) - 1ull))] = (int)s;
+  }
+}
+
 __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
   int n_act_ = 0;
   lvl_counts(S, n_act_, n_keys);
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s > n_keys) return;
   int nl = 0;
-  bool one_run = false, to_wave = false;
+  bool to_wave = false;
   if (s < seg_count(S, n_keys)) {
     SegInfo si;
     if (S.seg_len) {                                 // k_seg_build wrote length and (clade, locus)
@@ -831,71 +932,180 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
       si = seg_info(S, (int)s);
       S.seg_cg[s] = make_int2((int)((S.keys[si.kb] >> S.key_lb) & ((1ull << S.key_tb) - 1)), si.g);
     }
-    nl = (si.len / kNpyBuf) * lut_count(S, kNpyBuf) + lut_count(S, si.len % kNpyBuf);
-    int lo = 0, hi = 0;
-    double v = 0.0;
-    int na = si.ke - si.kb;
-    const bool thread_ok = THREAD_MEAN && si.len < kNpyBuf && nl <= kThreadLeaves;
-    if (na == 1) {
-      if (thread_ok) {
-        const int2 x = S.satt_lohi[si.kb];
-        lo = x.x; hi = x.y; v = S.satt_sc[si.kb];
-        one_run = true;
-      }
-    } else if (THREAD_MEAN && na <= kPruneMax) {
-      double F = 0.0;                                // best whole-locus attachment
-#pragma unroll 4
-      for (int t = si.kb; t < si.ke; ++t) {
-        const int2 x = S.satt_lohi[t];
-        const double sc = S.satt_sc[t];
-        if (x.x <= 0 && x.y >= si.len && sc > F) F = sc;
-      }
-      // attachments at or below F (or empty) change no site: the envelope is
-      // max(F, the others).  None left: one run of F.  Otherwise the survivors are
-      // compacted in place, with F as one whole-locus attachment after them, so the leaf
-      // kernel sees few attachments (usually <= kRegAtt: register path).
-      int kept = 0;
-#pragma unroll 4
-      for (int t = si.kb; t < si.ke; ++t) {
-        const int2 x = S.satt_lohi[t];
-        const double sc = S.satt_sc[t];
-        if (x.x < x.y && sc > F) {
-          if (kept != t - si.kb) { S.satt_lohi[si.kb + kept] = x; S.satt_sc[si.kb + kept] = sc; }
-          ++kept;
-        }
-      }
-      if (kept == 0 && thread_ok) {
-        lo = 0; hi = si.len; v = F; one_run = true;
-      } else {
-        // F > 0 came from an attachment that was not kept (its score is F), so the list
-        // never grows; it may have shifted, so F is always re-appended
-        if (F > 0.0) {
-          S.satt_lohi[si.kb + kept] = make_int2(0, si.len);
-          S.satt_sc[si.kb + kept] = F;
-          ++kept;
-        }
-        na = kept;
-      }
-    }
-    if (one_run) {
-      S.seg_mean[s] = one_run_mean(PtrLut{S.lut + S.lut_off[si.len]}, nl, si.len, lo, hi, v);
-      nl = 0;
-    } else {
-      S.seg_rec[s] = make_int4(si.kb, na, si.len, nl);
-      // many attachments (higher roll-up levels): one wave per segment (k_seg_wave)
-      to_wave = THREAD_MEAN && na > kRegAtt && na <= 64 && nl <= 64 && si.len < kNpyBuf;
-      if (to_wave) nl = 0;
-    }
+    const int kb = si.kb;
+    nl = seg_record(
+        S, s, kb, si.ke - kb, si.len, [&](int t) { return RecAtt{S.satt_lohi[kb + t], S.satt_sc[kb + t]}; },
+        [&](int k, const RecAtt& e) { S.satt_lohi[kb + k] = e.x; S.satt_sc[kb + k] = e.sc; }, true, to_wave);
   }
   S.seg_nleaf[s] = nl;
-  const uint64_t bm = __ballot(to_wave);            // one list append per wave
-  if (bm) {
-    const int lane = threadIdx.x & 63, leader = __builtin_ctzll(bm);
-    int base = 0;
-    if (lane == leader) base = (int)atomicAdd(&S.counters[7], (unsigned long long)__popcll(bm));
-    base = __shfl(base, leader, 64);
-    if (to_wave) S.wave_list[base + __popcll(bm & ((1ull << lane) - 1ull))] = (int)s;
+  wave_list_add(S, s, to_wave);
+}
+
+// The stress contigs' segment front end in one launch (round 6; for the contigs of the LDS
+// radix sort, 4,097..8,192 attachments: k_sort_radix + k_seg_build_wide + k_seg_rec + the
+// leaf-count scan + k_leaf_expand otherwise).  One 512-thread workgroup per contig, the
+// contigs claimed in rank order from a counter (fr[0]):
+//   * the LDS radix sort of the contig's keys (radix_sort_contig);
+//   * segment heads from the sorted keys in LDS (ballots per 64 keys, a scan of the chunk
+//     counts), segment starts into the spare key buffer;
+//   * the contig's first segment from a decoupled look-back over the ranks before it: each
+//     rank publishes its segment count as soon as it has it (status A), then its inclusive
+//     prefix (P); wave 0 reads 64 ranks per step and stops at the nearest P.  A rank waits
+//     only on smaller ranks, claimed earlier by resident workgroups that publish A without
+//     waiting on anything, so the wait ends (bounded anyway: counters[4] records a timeout
+//     and the host fails the call);
+//   * one thread per segment: seg_record over the attachments read through the sorted local
+//     indices (range and score loaded here, once), the leaf-path segments' leaves allocated
+//     from fr[1] with leaf_seg written here.
+// Only the segment table the decisions read (crank_first, seg_cg, seg_mean) and the records
+// of the rare wave / leaf segments reach HBM: no keys, sorted attachment copies, segment
+// starts or per-segment leaf counts.  fr: [0] ticket, [1] leaves, [4 + cr] rank cr's status
+// (zeroed per level).
+constexpr unsigned long long kLbA = 1ull << 62, kLbP = 2ull << 62, kLbVal = (1ull << 62) - 1ull;
+
+__global__ __launch_bounds__(kRadixNT) void k_front_radix(const SArgs S, int n_act, int64_t n_keys,
+                                                        unsigned long long* fr) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const RadixLds R(smem, S.sort_cap);
+  constexpr int kW = kRadixNT / 64;
+  __shared__ int s_red[kW];
+  __shared__ int s_glen[64];
+  __shared__ int s_chunk[kRadixMax / 64];
+  __shared__ int s_cr, s_ns, s_sbase;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t lmask = (1u << S.key_lb) - 1u, tmask = (uint32_t)((1ull << S.key_tb) - 1ull);
+  const KArgs& K = S.k;
+  unsigned long long* const lb = fr + 4;
+  for (;;) {
+    if (tid == 0) s_cr = (int)atomicAdd(&fr[0], 1ull);
+    __syncthreads();
+    const int cr = s_cr;
+    if (cr >= n_act) break;                          // (uniform)
+    const int c = S.act ? S.act[cr] : cr;
+    const int64_t a0 = S.catt_off[c];
+    const int n = (int)(S.catt_off[c + 1] - a0);
+    const int64_t base = S.act_base ? S.act_base[cr] : a0;   // level 0: own offsets
+    const int64_t l0 = K.loc_off[c];
+    const int G = (int)(K.loc_off[c + 1] - l0);
+    if (tid < 64 && tid < G) {                       // locus lengths (G <= 64)
+      const int x = K.lstart[l0 + tid], y = K.lend[l0 + tid];
+      s_glen[tid] = max(x, y) - min(x, y) + 1;
+    }
+    const int cur = n > 0 ? radix_sort_contig(S, a0, n, R, s_red) : 0;
+    const uint32_t* const kk = R.kb(cur);
+    const uint16_t* const ii = R.ib(cur);
+    uint32_t* const sst = R.kb(cur ^ 1);             // segment starts (the spare key buffer)
+    // segment heads: per-chunk counts, their exclusive scan (wave 0, two chunks a lane)
+    const int nch = (n + 63) >> 6;
+    for (int ch = w; ch < nch; ch += kW) {
+      const int t = ch * 64 + lane;
+      const uint64_t m = __ballot(t < n && (t == 0 || kk[t] != kk[t - 1]));
+      if (lane == 0) s_chunk[ch] = __popcll(m);
+    }
+    __syncthreads();
+    if (w == 0) {
+      const int x0 = 2 * lane < nch ? s_chunk[2 * lane] : 0, x1 = 2 * lane + 1 < nch ? s_chunk[2 * lane + 1] : 0;
+      int incl = x0 + x1;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+      }
+      if (2 * lane < nch) s_chunk[2 * lane] = incl - x0 - x1;
+      if (2 * lane + 1 < nch) s_chunk[2 * lane + 1] = incl - x1;
+      if (lane == 63) s_ns = incl;
+    }
+    __syncthreads();
+    const int ns = s_ns;
+    for (int ch = w; ch < nch; ch += kW) {
+      const int t = ch * 64 + lane;
+      const bool head = t < n && (t == 0 || kk[t] != kk[t - 1]);
+      const uint64_t m = __ballot(head);
+      if (head) sst[s_chunk[ch] + __popcll(m & below)] = (uint32_t)t;
+    }
+    // look-back: this rank's first segment
+    if (w == 0) {
+      if (lane == 0)
+        __hip_atomic_store(&lb[cr], (cr == 0 ? kLbP : kLbA) | (unsigned long long)ns, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      long long excl = 0;
+      for (int top = cr - 1; top >= 0;) {
+        const int r = top - lane;
+        unsigned long long v = r >= 0 ? 0ull : kLbP;   // (before rank 0: a zero prefix)
+        for (int spin = 0;; ++spin) {
+          if (r >= 0 && (v >> 62) == 0ull)
+            v = __hip_atomic_load(&lb[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__ballot((v >> 62) == 0ull) == 0ull) break;
+          if (spin >= (1 << 22)) {                   // (never expected: fail the call, not the GPU)
+            if (lane == 0) atomicExch(&S.counters[4], 1ull);
+            if ((v >> 62) == 0ull) v = kLbA;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        const uint64_t pm = __ballot((v >> 62) == 2ull);
+        const int first_p = pm ? __builtin_ctzll(pm) : 64;
+        long long add = lane <= first_p ? (long long)(v & kLbVal) : 0;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) add += __shfl_xor(add, off, 64);
+        excl += add;
+        if (pm) break;
+        top -= 64;
+      }
+      if (lane == 0) {
+        if (cr > 0)
+          __hip_atomic_store(&lb[cr], kLbP | (unsigned long long)(excl + ns), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        s_sbase = (int)excl;
+        S.crank_first[cr] = (int)excl;
+        if (cr == n_act - 1) {
+          S.crank_first[n_act] = (int)excl + ns;
+          if (n_keys > 0) S.seg_id[n_keys - 1] = (int)excl + ns;   // seg_count()
+        }
+      }
+    }
+    __syncthreads();
+    const int sbase = s_sbase;
+    for (int s0 = w * 64; s0 < ns; s0 += kRadixNT) {  // (wave-uniform trips: wave_list_add ballots)
+      const int sl = s0 + lane;
+      bool to_wave = false;
+      const int64_t s = (int64_t)sbase + sl;
+      if (sl < ns) {
+        const int t0 = (int)sst[sl], t1 = sl + 1 < ns ? (int)sst[sl + 1] : n;
+        const uint32_t key = kk[t0];
+        const int g = (int)(key & lmask);
+        int len;
+        if (G <= 64) {
+          len = s_glen[g];
+        } else {
+          const int x = K.lstart[l0 + g], y = K.lend[l0 + g];
+          len = max(x, y) - min(x, y) + 1;
+        }
+        S.seg_cg[s] = make_int2((int)((key >> S.key_lb) & tmask), g);
+        const int kb = (int)(base + t0);
+        const int nl = seg_record(
+            S, s, kb, t1 - t0, len,
+            [&](int t) {
+              const int64_t a = a0 + ii[t0 + t];
+              return RecAtt{make_int2(S.att_lo[a], S.att_hi[a]), S.att_sc[a]};
+            },
+            [&](int k, const RecAtt& e) { S.satt_lohi[kb + k] = e.x; S.satt_sc[kb + k] = e.sc; }, false, to_wave);
+        if (nl > 0) {                                // the leaf kernels' share (rare)
+          const int o = (int)atomicAdd(&fr[1], (unsigned long long)nl);
+          S.leaf_off[s] = o;
+          for (int j = 0; j < nl; ++j) S.leaf_seg[o + j] = (int)s;
+        }
+      }
+      wave_list_add(S, s, to_wave);
+    }
+    __syncthreads();                                 // (LDS and s_cr reused by the next contig)
   }
+}
+
+// After k_front_radix: the leaf total where the leaf kernels read it (leaf_off[segments]).
+__global__ void k_front_fin(const SArgs S, int n_act, const unsigned long long* fr) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) S.leaf_off[S.crank_first[n_act]] = (int)fr[1];
 }
 
 // Segments with 5..64 attachments, one wave each: the max-envelope is swept once into runs
@@ -1557,6 +1767,7 @@ struct StagedState {
   Buf keys0, keys1, vals0, vals1, flags, seg_id, seg_start, seg_crank, seg_mean;
   Buf cnt_leaves, red, seg_nleaf, leaf_off, leaf_seg, leaf_val, annot_best;
   Buf seg_rec, seg_cg, crank_first, satt_lohi, satt_sc, wave_list, lvl_ctr, seg_cnt, seg_len;
+  Buf front;                      // k_front_radix: ticket, leaf count, per-rank look-back words
   Buf span_cnt, spans;                              // --write-details only
   unsigned long long* host_lvl = nullptr;         // pinned: count word of each level
   hipEvent_t lvl_ev[2] = {nullptr, nullptr};
@@ -2330,7 +2541,29 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     sa.keys = nullptr;
     sa.vals = nullptr;
     const int t_seg = t_mark(st, s);
-    if (n_keys > 0) {
+    if (n_keys > 0 && sa.sort_cap > kSortMax && !det) {
+      // the stress contigs' whole front end in one launch (k_front_radix), then the rare
+      // wave / leaf segments it listed
+      static const hipError_t fattr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_front_radix),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                          (int)radix_lds(kRadixMax));
+      ST_TRY(fattr);
+      const size_t fr_bytes = ((size_t)n_act + 4) * sizeof(unsigned long long);
+      ST_TRY(st->front.ensure(s, fr_bytes));
+      ST_TRY(hipMemsetAsync(st->front.p, 0, fr_bytes, s));
+      unsigned long long* fr = st->front.as<unsigned long long>();
+      const size_t lds = radix_lds(sa.sort_cap);
+      const int per_cu = std::max(1, (int)((160 * 1024) / lds));
+      hipLaunchKernelGGL(k_front_radix, dim3(std::min(n_act, st->cus * per_cu)), dim3(kRadixNT), lds, s, sa, n_act,
+                         n_keys, fr);
+      hipLaunchKernelGGL(k_front_fin, dim3(1), dim3(64), 0, s, sa, n_act, fr);
+      hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 32), dim3(64), 0, s, sa);
+      hipLaunchKernelGGL(k_leaf, dim3(leaf_grid), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_seg_combine, dim3(st->cus * 4), dim3(256), 0, s, sa, n_keys);
+      ST_TRY(hipGetLastError());
+      sa.keys = kbuf.Current();
+      sa.vals = vbuf.Current();
+    } else if (n_keys > 0) {
       size_t need = st->tmp.n;
       if (sa.sort_cap > kSortMax) {
         static const hipError_t rattr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sort_radix),
@@ -2387,7 +2620,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
       // short segments' means by one thread each; one wave per multi-attachment segment, a
       // serial envelope sweep (62 VGPRs, 2.8 KB LDS -> 32 waves per CU; roll-up levels have
       // ~10^5 such segments); the rest through the leaf kernels
-      hipLaunchKernelGGL(k_seg_rec<true>, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
+      hipLaunchKernelGGL(k_seg_rec, dim3(grid_for(n_keys + 1)), dim3(256), 0, s, sa, n_keys);
       hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 32), dim3(64), 0, s, sa);
       need = st->tmp.n;
       ST_TRY(hipcub::DeviceScan::ExclusiveSum(st->tmp.p, need, sa.seg_nleaf, sa.leaf_off,
@@ -2417,11 +2650,15 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     ST_TRY(hipGetLastError());
     t_span(st, WF_PHASE_DECIDE, t_dec, t_mark(st, s));
     if (mailbox) {
-      ST_TRY(publish_sync(st, s, sa.counters, 4, nullptr, 0, st->host_counters));
+      ST_TRY(publish_sync(st, s, sa.counters, 5, nullptr, 0, st->host_counters));
     } else {
-      ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 4 * sizeof(unsigned long long),
+      ST_TRY(hipMemcpyAsync(st->host_counters, sa.counters, 5 * sizeof(unsigned long long),
                             hipMemcpyDeviceToHost, s));
       ST_TRY(spin_sync(s, st->lvl_ev[0]));
+    }
+    if (st->host_counters[4]) {                      // (k_front_radix's look-back never completed)
+      *err = "segment look-back timed out";
+      return -2;
     }
     const int n_big = (int)st->host_counters[2];
     int n_dense = 0;                    // contigs that need the dense decision in an HBM slot
