@@ -234,6 +234,35 @@ def test_cfg3_full_size():
     assert_same(slice_results(a, batch, c0, c0 + 300), want, sub)
 
 
+def test_stress_front_end_matches_five_launch_form():
+    """k_front_radix -- the > 4,096-attachment contigs' sort, segments and exact means in one
+    LDS-resident launch per level, segment offsets by decoupled look-back -- against the
+    five-launch form the --write-details path keeps (k_sort_radix, k_seg_build_wide,
+    k_seg_rec, the leaf-count scan, k_leaf_expand), on decoy-heavy contigs whose segments
+    take every mean path (one run; 2..4 overlapping attachments: the leaf kernels; 5..64:
+    k_seg_wave; more: the leaf kernels), at level 0 and the roll-up levels; and the oracle's
+    records on 3 of them."""
+    data = synth.generate(n=48, genes=20, clades=300, decoys=240, lgt_frac=0.5, seed=17)
+    batch, tax = synth.to_batch(data)
+    assert batch.max_hits > 4096
+    per_seg = np.unique(data.hit_contig * 1_000_000 + data.hit_clade * 100 + data.hit_gene,
+                        return_counts=True)[1]
+    assert (per_seg == 1).any() and ((per_seg >= 2) & (per_seg <= 4)).any() and (per_seg >= 5).any()
+    s = engine.GpuScorer(0)
+    s.set_taxonomy(tax)
+    fused = s.score(batch, PARAMS)
+    five, _ = s.score_details(batch, PARAMS)
+    s.close()
+    assert not fused.status.any()
+    assert (fused.iterations > 1).any()
+    assert_same(fused, five, batch)
+    sub = batch.slice(0, 3)
+    contigs = orc.score_contigs(dict(zip(sub.contig_names, sub.contig_lengths.tolist())),
+                                oracle_loci_from_batch(sub), oracle_hits_from_batch(sub, tax),
+                                orc.Taxonomy(data.tax.edges), orc.Params(**PARAMS))
+    assert_same(slice_results(fused, batch, 0, 3), oracle_results(contigs, sub, tax), sub)
+
+
 def test_cfg5_shard_and_embedded_fixture(tmp_path):
     """The cfg5 per-GPU share at 8 GPUs (6,250 stress contigs, ~31 M hits, 5,000 clades):
     equal to its two halves and to the all-segment-table staged form; the reference-generated
