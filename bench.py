@@ -118,6 +118,56 @@ def k2_algorithmic(pair_evals, batch, ppot_sum=None):
             "b_k2_from": "ppot_sum (per call)" if ppot_sum is not None else "pairs (one call per contig)"}
 
 
+OPS_PEAK = 3.93e13            # 256 CUs x 64 lanes x 2.4 GHz simple fp64 / int ops
+
+
+def ops_site(batch, parent, pdict, iters, pair_budget=20_000_000):
+    """OPS_site = sum over the levels a contig is evaluated at of sum over its
+    (clade, locus) pairs with an attached hit of len(locus) -- the reference's site updates and
+    np.mean adds (score_hit / update_gene_scores, orgscorer.py:371-406; raise_taxonomy :431-445)
+    -- from the attachment rule of orgscorer.py:359-369 (calc_overlap, utils.py:487-500) in
+    numpy, on the first contigs whose hit x locus pairs fit `pair_budget`, scaled by contigs.
+    iters: the contigs' evaluated levels (wf_result.iterations; at least level 0).
+    -> (OPS_site for the batch, contigs sampled)."""
+    N = batch.n_contigs
+    if N == 0:
+        return 0.0, 0
+    H, G = np.diff(batch.hit_off), np.diff(batch.loc_off)
+    S = int(np.clip(np.searchsorted(np.cumsum(H * G), pair_budget, side="right"), 1, N))
+    h1 = int(batch.hit_off[S])
+    hc = np.repeat(np.arange(S), H[:S])                       # each hit's contig
+    reps = G[hc]
+    hi = np.repeat(np.arange(h1), reps)                       # (hit, locus of its contig) pairs
+    k = np.arange(len(hi)) - np.repeat(np.cumsum(reps) - reps, reps)
+    li = np.repeat(batch.loc_off[:S][hc], reps) + k
+    qlo, qhi = batch.hit_qlo[hi].astype(np.int64), batch.hit_qhi[hi].astype(np.int64)
+    a, b = qlo.copy(), qhi.copy()
+    qlo, qhi = np.minimum(a, b), np.maximum(a, b)
+    lo = np.minimum(batch.loc_start[li], batch.loc_end[li]).astype(np.int64)
+    up = np.maximum(batch.loc_start[li], batch.loc_end[li]).astype(np.int64)
+    llen = up - lo + 1
+    disjoint = (lo > qhi) | (qlo > up)
+    ov = (np.minimum(qhi, up) - np.maximum(qlo, lo) + 1).astype(np.float64)
+    frac = np.where(disjoint, 0.0, ov / np.minimum(qhi - qlo + 1, llen))
+    ok = (frac >= float(pdict["min_overlap"])) & (batch.hit_scov[hi] >= float(pdict["min_scov"]))
+    if pdict.get("stranded"):
+        ok &= batch.hit_strand[hi] == batch.loc_strand[li]
+    clade = batch.hit_taxon[hi][ok].astype(np.int64)
+    loc, ln, lev = li[ok], llen[ok], np.maximum(iters[:S].astype(np.int64), 1)[hc[hi][ok]]
+    parent = np.asarray(parent, np.int64)
+    for _ in range(max(0, int(pdict.get("jump_taxonomy") or 0))):   # orgscorer.py:955-957
+        clade = parent[clade]
+    T = len(parent)
+    total, L = 0, 0
+    while len(clade) and (lev > L).any():
+        sel = lev > L
+        _, first = np.unique(loc[sel] * T + clade[sel], return_index=True)
+        total += int(ln[sel][first].sum())
+        clade = parent[clade]
+        L += 1
+    return float(total) * N / S, S
+
+
 def file_sha(path):
     """sha256 of a file (the library build a PMC summary was taken on), first 16 hex digits."""
     import hashlib
@@ -602,6 +652,21 @@ def main():
     b_alg = algorithmic_bytes(batch)
     achieved = b_dom / (dom_ms * 1e-3) / 1e9
     achieved_pass = b_alg / (pass_ms * 1e-3) / 1e9
+    # SURVEY 8(d)'s op roofline of the whole pass (this rank's contigs)
+    ops_s, ops_n = ops_site(batch, tax.parent, pdict, iters)
+    t_hbm, t_ops = b_alg / (HBM_PEAK_GBS * 1e9), (ops_s + k2_counts["ops_pair"]) / OPS_PEAK
+    ops_roofline = {
+        "rule": "SURVEY 8(d): roofline_time = max(B_alg / 8.0e12 B/s, OPS_alg / 3.93e13 op/s), OPS_alg "
+                "= OPS_site + OPS_pair; achieved = roofline_time / the pass time",
+        "b_alg": b_alg, "ops_site": ops_s, "ops_pair": k2_counts["ops_pair"],
+        "ops_site_rule": "sum over evaluated levels of len(locus) per (clade, locus) with an attached hit "
+                         "(the reference's site updates); numpy attachment rule on the first {} contigs, "
+                         "scaled".format(ops_n),
+        "t_hbm_ms": t_hbm * 1e3, "t_ops_ms": t_ops * 1e3, "roofline_time_ms": max(t_hbm, t_ops) * 1e3,
+        "pass_ms": pass_ms, "bound": "ops" if t_ops > t_hbm else "hbm",
+        "achieved": max(t_hbm, t_ops) * 1e3 / pass_ms,
+        "note": "counts the reference's per-site work; the closed-form means and the mask-class "
+                "pair search do far less of it"}
     lib_sha = file_sha(L.LIB_PATH)
 
     def pmc_file(path, kind):
@@ -675,6 +740,7 @@ def main():
                                        enumerate(np.bincount(iters[calls != 0].astype(np.int64)))
                                        if v}},
         "main_k2_counts": dict(k2_counts, pair_evals_per_sec=pairs / (elapsed / args.steps)),
+        "ops_roofline": ops_roofline,
         "kernel_ms": dict({"wf_score_pass": pass_ms},
                           **{"phase_" + k: v[0] / max(1, tm.passes)
                              for k, v in tm.phases().items()}),
