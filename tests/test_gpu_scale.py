@@ -234,15 +234,17 @@ def test_cfg3_full_size():
     assert_same(slice_results(a, batch, c0, c0 + 300), want, sub)
 
 
-def test_stress_front_end_matches_five_launch_form():
+@pytest.mark.parametrize("genes,decoys", [(20, 240), (70, 70)], ids=["packed", "wide-loci"])
+def test_stress_front_end_matches_five_launch_form(genes, decoys):
     """k_front_radix -- the > 4,096-attachment contigs' sort, segments and exact means in one
     LDS-resident launch per level, segment offsets by decoupled look-back -- against the
     five-launch form the --write-details path keeps (k_sort_radix, k_seg_build_wide,
     k_seg_rec, the leaf-count scan, k_leaf_expand), on decoy-heavy contigs whose segments
     take every mean path (one run; 2..4 overlapping attachments: the leaf kernels; 5..64:
     k_seg_wave; more: the leaf kernels), at level 0 and the roll-up levels; and the oracle's
-    records on 3 of them."""
-    data = synth.generate(n=48, genes=20, clades=300, decoys=240, lgt_frac=0.5, seed=17)
+    records on 3 of them.  20 loci: the packed sort words (contig-local clade ranks); 70 loci
+    (lb = 7): the key + index buffers."""
+    data = synth.generate(n=48, genes=genes, clades=300, decoys=decoys, lgt_frac=0.5, seed=17)
     batch, tax = synth.to_batch(data)
     assert batch.max_hits > 4096
     per_seg = np.unique(data.hit_contig * 1_000_000 + data.hit_clade * 100 + data.hit_gene,

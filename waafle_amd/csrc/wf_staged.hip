@@ -410,47 +410,35 @@ constexpr int kRadixBits = 8;
 constexpr int kRadixBins = 1 << kRadixBits;
 // dynamic LDS for a capacity of `cap` attachments (a multiple of 512): two key and two index
 // buffers, the per-wave digit counts -- 80 KB at cap 6,144 (two workgroups per CU), 104 KB at 8,192
-inline size_t radix_lds(int cap) { return (size_t)cap * 2 * (4 + 2) + (size_t)(kRadixNT / 64) * kRadixBins * 4 + 64; }
+inline size_t radix_lds(int cap, bool packed = false) {
+  return (size_t)cap * 2 * (packed ? 4 : 4 + 2) + (size_t)(kRadixNT / 64) * kRadixBins * 4 + 64;
+}
 
-// The sort's LDS (dynamic, radix_lds(cap) bytes): the ping-pong key and index buffers and
-// the per-wave digit counts
+// The sort's LDS (dynamic, radix_lds(cap, packed) bytes): the ping-pong key and index buffers
+// (packed: 32-bit words only) and the per-wave digit counts
 struct RadixLds {
   uint32_t* kb0;
   uint16_t* ib0;
   int* cnt;                                            // [wave][bin]
   int cap;
-  __device__ RadixLds(char* smem, int cap_)
+  __device__ RadixLds(char* smem, int cap_, bool packed = false)
       : kb0(reinterpret_cast<uint32_t*>(smem)), ib0(reinterpret_cast<uint16_t*>(smem + 8 * (size_t)cap_)),
-        cnt(reinterpret_cast<int*>(smem + 12 * (size_t)cap_)), cap(cap_) {}
+        cnt(reinterpret_cast<int*>(smem + (packed ? 8 : 12) * (size_t)cap_)), cap(cap_) {}
   __device__ uint32_t* kb(int x) const { return kb0 + x * cap; }   // buffer x of the pair
   __device__ uint16_t* ib(int x) const { return ib0 + x * cap; }
 };
 
-// One contig's n > 0 attachments [a0, a0 + n) sorted by key in LDS (the whole workgroup);
-// returns the buffer holding the sorted keys and their contig-local indices.
-__device__ __forceinline__ int radix_sort_contig(const SArgs& S, int64_t a0, int n, const RadixLds& R, int* s_red) {
+// The stable LSD passes over n loaded elements (buffer 0; 8-bit digits of the low kbits
+// bits above `skip`): each wave owns a contiguous slice; per-wave digit counts from eight
+// ballots, a digit-major / wave-minor prefix, then each wave scatters its chunks in order.
+// PACKED: the key and its index share one 32-bit word (no index buffers).  Returns the
+// buffer holding the sorted sequence.
+template <bool PACKED>
+__device__ __forceinline__ int radix_passes(const RadixLds& R, int n, int kbits, int skip, int* s_red) {
   constexpr int kW = kRadixNT / 64;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  const int kbits = S.key_tb + S.key_lb;              // (<= 32: checked on the host)
   int* const cnt = R.cnt;
-  // (the attachments' clade and locus loads of four strides issued together)
-  for (int i0 = 0; i0 < n; i0 += 4 * kRadixNT) {
-    uint32_t kk[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + r * kRadixNT + tid;
-      kk[r] = i < n ? (uint32_t)make_key(S, 0, (int)(a0 + i)) : 0u;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + r * kRadixNT + tid;
-      if (i < n) {
-        R.kb(0)[i] = kk[r];
-        R.ib(0)[i] = (uint16_t)i;
-      }
-    }
-  }
   // wave w's slice [lo, hi) of the elements
   const int per = (n + kW - 1) / kW;
   const int lo = min(n, w * per), hi = min(n, lo + per);
@@ -461,7 +449,7 @@ __device__ __forceinline__ int radix_sort_contig(const SArgs& S, int64_t a0, int
     // the lanes of this chunk with the same digit (d), from 8 ballots
     auto group = [&](int i, int& d) -> uint64_t {
       const bool live = i < hi;
-      d = live ? (int)((R.kb(cur)[i] >> shift) & (kRadixBins - 1)) : 0;
+      d = live ? (int)((R.kb(cur)[i] >> (skip + shift)) & (kRadixBins - 1)) : 0;
       uint64_t m = __ballot(live);
 #pragma unroll
       for (int b = 0; b < kRadixBits; ++b) {
@@ -507,7 +495,7 @@ __device__ __forceinline__ int radix_sort_contig(const SArgs& S, int64_t a0, int
       if (m) {
         const int pos = cnt[w * kRadixBins + d] + __popcll(m & below);
         R.kb(cur ^ 1)[pos] = R.kb(cur)[i0 + lane];
-        R.ib(cur ^ 1)[pos] = R.ib(cur)[i0 + lane];
+        if (!PACKED) R.ib(cur ^ 1)[pos] = R.ib(cur)[i0 + lane];
       }
       wave_sync();                                   // (reads of the counts before the update)
       if (m && (m >> lane) == 1ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's last lane)
@@ -517,6 +505,86 @@ __device__ __forceinline__ int radix_sort_contig(const SArgs& S, int64_t a0, int
     cur ^= 1;
   }
   return cur;
+}
+
+// One contig's n > 0 attachments [a0, a0 + n) sorted by key (clade << lb | locus) in LDS (the
+// whole workgroup); returns the buffer holding the sorted keys and their contig-local indices.
+__device__ __forceinline__ int radix_sort_contig(const SArgs& S, int64_t a0, int n, const RadixLds& R, int* s_red) {
+  const int tid = threadIdx.x;
+  // (the attachments' clade and locus loads of four strides issued together)
+  for (int i0 = 0; i0 < n; i0 += 4 * kRadixNT) {
+    uint32_t kk[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + r * kRadixNT + tid;
+      kk[r] = i < n ? (uint32_t)make_key(S, 0, (int)(a0 + i)) : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + r * kRadixNT + tid;
+      if (i < n) {
+        R.kb(0)[i] = kk[r];
+        R.ib(0)[i] = (uint16_t)i;
+      }
+    }
+  }
+  return radix_passes<false>(R, n, S.key_tb + S.key_lb, 0, s_red);   // (<= 32 bits: checked on the host)
+}
+
+// The same order from one 32-bit word per attachment: the contig's clades present (a bitmap
+// over the taxonomy's ids, aliasing the digit counts until the passes) ranked in id order, so
+// (rank << lb | locus) << kSortIdxBits | index fits 32 bits and sorts exactly as (clade,
+// locus, index).  8 instead of 12 bytes of LDS per attachment, and only as many passes as the
+// contig's ranks need.  Requires lb <= 6 and a bitmap + word prefix of at most the count
+// area (n_tax <= kPackTaxMax); returns the buffer of sorted words.
+constexpr int kPackTaxMax = (kRadixNT / 64) * kRadixBins * 4 / 6 * 32;   // (6 B a bitmap word <= the counts)
+__device__ __forceinline__ int radix_sort_packed(const SArgs& S, int64_t a0, int n, int n_tax, const RadixLds& R,
+                                                 int* s_red) {
+  constexpr int kW = kRadixNT / 64;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nw = (n_tax + 31) >> 5;
+  uint32_t* const bm = reinterpret_cast<uint32_t*>(R.cnt);
+  uint16_t* const bpre = reinterpret_cast<uint16_t*>(bm + nw);
+  for (int i = tid; i < nw; i += kRadixNT) bm[i] = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += kRadixNT) {
+    const uint32_t cl = (uint32_t)S.att_clade[a0 + i], g = (uint32_t)S.att_loc[a0 + i];
+    atomicOr(&bm[cl >> 5], 1u << (cl & 31u));
+    R.kb(0)[i] = cl << 8 | g;                        // (clade, locus) until the ranks are known
+  }
+  __syncthreads();
+  // the ranks' word prefix: thread t sums words [t k, t k + k), a block scan of the sums
+  const int k = (nw + kRadixNT - 1) / kRadixNT;
+  int own = 0;
+  for (int x = tid * k; x < min(nw, tid * k + k); ++x) own += __popc(bm[x]);
+  int incl = own;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) s_red[w] = incl;
+  __syncthreads();
+  int pre = incl - own, present = 0;
+#pragma unroll
+  for (int x = 0; x < kW; ++x) {
+    pre += x < w ? s_red[x] : 0;
+    present += s_red[x];
+  }
+  for (int x = tid * k; x < min(nw, tid * k + k); ++x) {
+    bpre[x] = (uint16_t)pre;
+    pre += __popc(bm[x]);
+  }
+  __syncthreads();
+  const int lb = S.key_lb;
+  for (int i = tid; i < n; i += kRadixNT) {
+    const uint32_t x = R.kb(0)[i], cl = x >> 8;
+    const uint32_t rank = bpre[cl >> 5] + __popc(bm[cl >> 5] & ((1u << (cl & 31u)) - 1u));
+    R.kb(0)[i] = ((rank << lb) | (x & 255u)) << kSortIdxBits | (uint32_t)i;
+  }
+  __syncthreads();
+  const int rbits = 32 - __clz(max(present - 1, 1));
+  return radix_passes<true>(R, n, rbits + lb, kSortIdxBits, s_red);
 }
 
 __global__ __launch_bounds__(kRadixNT) void k_sort_radix(const SArgs S, int n_act, int level, uint64_t* keys,
@@ -961,12 +1029,15 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
 // of the rare wave / leaf segments reach HBM: no keys, sorted attachment copies, segment
 // starts or per-segment leaf counts.  fr: [0] ticket, [1] leaves, [4 + cr] rank cr's status
 // (zeroed per level).
+// PACKED (the usual shape: lb <= 6, n_tax <= kPackTaxMax): radix_sort_packed, 8 bytes of LDS
+// per attachment, three workgroups per CU at the cfg5 size (80 VGPRs); else radix_sort_contig.
 constexpr unsigned long long kLbA = 1ull << 62, kLbP = 2ull << 62, kLbVal = (1ull << 62) - 1ull;
 
-__global__ __launch_bounds__(kRadixNT) void k_front_radix(const SArgs S, int n_act, int64_t n_keys,
-                                                        unsigned long long* fr) {
+template <bool PACKED>
+__global__ __launch_bounds__(kRadixNT, PACKED ? 6 : 1) void k_front_radix(const SArgs S, int n_act, int64_t n_keys,
+                                                                         int n_tax, unsigned long long* fr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const RadixLds R(smem, S.sort_cap);
+  const RadixLds R(smem, S.sort_cap, PACKED);
   constexpr int kW = kRadixNT / 64;
   __shared__ int s_red[kW];
   __shared__ int s_glen[64];
@@ -992,15 +1063,17 @@ __global__ __launch_bounds__(kRadixNT) void k_front_radix(const SArgs S, int n_a
       const int x = K.lstart[l0 + tid], y = K.lend[l0 + tid];
       s_glen[tid] = max(x, y) - min(x, y) + 1;
     }
-    const int cur = n > 0 ? radix_sort_contig(S, a0, n, R, s_red) : 0;
-    const uint32_t* const kk = R.kb(cur);
-    const uint16_t* const ii = R.ib(cur);
+    const int cur = n == 0 ? 0 : PACKED ? radix_sort_packed(S, a0, n, n_tax, R, s_red) : radix_sort_contig(S, a0, n, R, s_red);
+    const uint32_t* const kk = R.kb(cur);            // sorted keys (PACKED: words)
+    const uint16_t* const ii = R.ib(cur);            // (!PACKED) their indices
     uint32_t* const sst = R.kb(cur ^ 1);             // segment starts (the spare key buffer)
+    auto key_at = [&](int t) -> uint32_t { return PACKED ? kk[t] >> kSortIdxBits : kk[t]; };
+    auto idx_at = [&](int t) -> int { return PACKED ? (int)(kk[t] & ((1u << kSortIdxBits) - 1u)) : (int)ii[t]; };
     // segment heads: per-chunk counts, their exclusive scan (wave 0, two chunks a lane)
     const int nch = (n + 63) >> 6;
     for (int ch = w; ch < nch; ch += kW) {
       const int t = ch * 64 + lane;
-      const uint64_t m = __ballot(t < n && (t == 0 || kk[t] != kk[t - 1]));
+      const uint64_t m = __ballot(t < n && (t == 0 || key_at(t) != key_at(t - 1)));
       if (lane == 0) s_chunk[ch] = __popcll(m);
     }
     __syncthreads();
@@ -1020,7 +1093,7 @@ __global__ __launch_bounds__(kRadixNT) void k_front_radix(const SArgs S, int n_a
     const int ns = s_ns;
     for (int ch = w; ch < nch; ch += kW) {
       const int t = ch * 64 + lane;
-      const bool head = t < n && (t == 0 || kk[t] != kk[t - 1]);
+      const bool head = t < n && (t == 0 || key_at(t) != key_at(t - 1));
       const uint64_t m = __ballot(head);
       if (head) sst[s_chunk[ch] + __popcll(m & below)] = (uint32_t)t;
     }
@@ -1073,7 +1146,7 @@ __global__ __launch_bounds__(kRadixNT) void k_front_radix(const SArgs S, int n_a
       const int64_t s = (int64_t)sbase + sl;
       if (sl < ns) {
         const int t0 = (int)sst[sl], t1 = sl + 1 < ns ? (int)sst[sl + 1] : n;
-        const uint32_t key = kk[t0];
+        const uint32_t key = key_at(t0);
         const int g = (int)(key & lmask);
         int len;
         if (G <= 64) {
@@ -1082,12 +1155,12 @@ __global__ __launch_bounds__(kRadixNT) void k_front_radix(const SArgs S, int n_a
           const int x = K.lstart[l0 + g], y = K.lend[l0 + g];
           len = max(x, y) - min(x, y) + 1;
         }
-        S.seg_cg[s] = make_int2((int)((key >> S.key_lb) & tmask), g);
+        S.seg_cg[s] = make_int2(PACKED ? S.att_clade[a0 + idx_at(t0)] : (int)((key >> S.key_lb) & tmask), g);
         const int kb = (int)(base + t0);
         const int nl = seg_record(
             S, s, kb, t1 - t0, len,
             [&](int t) {
-              const int64_t a = a0 + ii[t0 + t];
+              const int64_t a = a0 + idx_at(t0 + t);
               return RecAtt{make_int2(S.att_lo[a], S.att_hi[a]), S.att_sc[a]};
             },
             [&](int k, const RecAtt& e) { S.satt_lohi[kb + k] = e.x; S.satt_sc[kb + k] = e.sc; }, false, to_wave);
@@ -2544,18 +2617,27 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
     if (n_keys > 0 && sa.sort_cap > kSortMax && !det) {
       // the stress contigs' whole front end in one launch (k_front_radix), then the rare
       // wave / leaf segments it listed
-      static const hipError_t fattr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_front_radix),
+      static const hipError_t fattr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_front_radix<false>),
                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
                                                           (int)radix_lds(kRadixMax));
+      static const hipError_t pattr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_front_radix<true>),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                          (int)radix_lds(kRadixMax, true));
       ST_TRY(fattr);
+      ST_TRY(pattr);
+      const bool packed = sa.key_lb <= 6 && n_tax <= kPackTaxMax;
       const size_t fr_bytes = ((size_t)n_act + 4) * sizeof(unsigned long long);
       ST_TRY(st->front.ensure(s, fr_bytes));
       ST_TRY(hipMemsetAsync(st->front.p, 0, fr_bytes, s));
       unsigned long long* fr = st->front.as<unsigned long long>();
-      const size_t lds = radix_lds(sa.sort_cap);
-      const int per_cu = std::max(1, (int)((160 * 1024) / lds));
-      hipLaunchKernelGGL(k_front_radix, dim3(std::min(n_act, st->cus * per_cu)), dim3(kRadixNT), lds, s, sa, n_act,
-                         n_keys, fr);
+      const size_t lds = radix_lds(sa.sort_cap, packed);
+      const int per_cu = std::max(1, (int)((160 * 1024) / (lds + 1024)));   // (+ its static LDS)
+      if (packed)
+        hipLaunchKernelGGL(k_front_radix<true>, dim3(std::min(n_act, st->cus * per_cu)), dim3(kRadixNT), lds, s, sa,
+                           n_act, n_keys, n_tax, fr);
+      else
+        hipLaunchKernelGGL(k_front_radix<false>, dim3(std::min(n_act, st->cus * per_cu)), dim3(kRadixNT), lds, s, sa,
+                           n_act, n_keys, n_tax, fr);
       hipLaunchKernelGGL(k_front_fin, dim3(1), dim3(64), 0, s, sa, n_act, fr);
       hipLaunchKernelGGL(k_seg_wave, dim3(st->cus * 32), dim3(64), 0, s, sa);
       hipLaunchKernelGGL(k_leaf, dim3(leaf_grid), dim3(256), 0, s, sa, n_keys);
