@@ -428,31 +428,32 @@ struct RadixLds {
   __device__ uint16_t* ib(int x) const { return ib0 + x * cap; }
 };
 
-// The stable LSD passes over n loaded elements (buffer 0; 8-bit digits of the low kbits
-// bits above `skip`): each wave owns a contiguous slice; per-wave digit counts from eight
-// ballots, a digit-major / wave-minor prefix, then each wave scatters its chunks in order.
+// The stable LSD passes over n loaded elements (buffer 0; BITS-bit digits of the low kbits
+// bits above `skip`): each wave owns a contiguous slice; per-wave digit counts (type CT) from
+// BITS ballots, a digit-major / wave-minor prefix, then each wave scatters its chunks in order.
 // PACKED: the key and its index share one 32-bit word (no index buffers).  Returns the
 // buffer holding the sorted sequence.
-template <bool PACKED>
+template <bool PACKED, int BITS = kRadixBits, class CT = int>
 __device__ __forceinline__ int radix_passes(const RadixLds& R, int n, int kbits, int skip, int* s_red) {
-  constexpr int kW = kRadixNT / 64;
+  constexpr int kW = kRadixNT / 64, kBins = 1 << BITS;
+  static_assert(kBins <= kRadixNT && kW * kBins * sizeof(CT) <= kW * kRadixBins * sizeof(int), "count area");
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  int* const cnt = R.cnt;
+  CT* const cnt = reinterpret_cast<CT*>(R.cnt);
   // wave w's slice [lo, hi) of the elements
   const int per = (n + kW - 1) / kW;
   const int lo = min(n, w * per), hi = min(n, lo + per);
   int cur = 0;
-  for (int shift = 0; shift < kbits; shift += kRadixBits) {
-    for (int i = tid; i < kW * kRadixBins; i += kRadixNT) cnt[i] = 0;
+  for (int shift = 0; shift < kbits; shift += BITS) {
+    for (int i = tid; i < kW * kBins; i += kRadixNT) cnt[i] = 0;
     __syncthreads();
-    // the lanes of this chunk with the same digit (d), from 8 ballots
+    // the lanes of this chunk with the same digit (d), from BITS ballots
     auto group = [&](int i, int& d) -> uint64_t {
       const bool live = i < hi;
-      d = live ? (int)((R.kb(cur)[i] >> (skip + shift)) & (kRadixBins - 1)) : 0;
+      d = live ? (int)((R.kb(cur)[i] >> (skip + shift)) & (kBins - 1)) : 0;
       uint64_t m = __ballot(live);
 #pragma unroll
-      for (int b = 0; b < kRadixBits; ++b) {
+      for (int b = 0; b < BITS; ++b) {
         const uint64_t bal = __ballot((d >> b) & 1);
         m &= ((d >> b) & 1) ? bal : ~bal;
       }
@@ -461,19 +462,19 @@ __device__ __forceinline__ int radix_passes(const RadixLds& R, int n, int kbits,
     for (int i0 = lo; i0 < hi; i0 += 64) {           // per-wave digit counts
       int d;
       const uint64_t m = group(i0 + lane, d);
-      if (m && (m & below) == 0ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's first lane)
+      if (m && (m & below) == 0ull) cnt[w * kBins + d] += (CT)__popcll(m);   // (the group's first lane)
     }
     __syncthreads();
     // offsets: digit-major, wave-minor (thread d walks the waves of digit d, then a scan of
     // the digit totals across the block)
     int tot = 0;
-    if (tid < kRadixBins)
+    if (tid < kBins)
       for (int x = 0; x < kW; ++x) {
-        const int v = cnt[x * kRadixBins + tid];
-        cnt[x * kRadixBins + tid] = tot;
+        const int v = cnt[x * kBins + tid];
+        cnt[x * kBins + tid] = (CT)tot;
         tot += v;
       }
-    // exclusive scan of the 256 digit totals (threads 0..255 = waves 0..3)
+    // exclusive scan of the digit totals (thread d: digit d)
     int incl = tot;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -482,10 +483,10 @@ __device__ __forceinline__ int radix_passes(const RadixLds& R, int n, int kbits,
     }
     if (lane == 63) s_red[w] = incl;
     __syncthreads();
-    if (tid < kRadixBins) {
+    if (tid < kBins) {
       int pre = incl - tot;
       for (int x = 0; x < w; ++x) pre += s_red[x];
-      for (int x = 0; x < kW; ++x) cnt[x * kRadixBins + tid] += pre;
+      for (int x = 0; x < kW; ++x) cnt[x * kBins + tid] += (CT)pre;
     }
     __syncthreads();
     // scatter, each wave its chunks in order (stable)
@@ -493,12 +494,12 @@ __device__ __forceinline__ int radix_passes(const RadixLds& R, int n, int kbits,
       int d;
       const uint64_t m = group(i0 + lane, d);
       if (m) {
-        const int pos = cnt[w * kRadixBins + d] + __popcll(m & below);
+        const int pos = cnt[w * kBins + d] + __popcll(m & below);
         R.kb(cur ^ 1)[pos] = R.kb(cur)[i0 + lane];
         if (!PACKED) R.ib(cur ^ 1)[pos] = R.ib(cur)[i0 + lane];
       }
       wave_sync();                                   // (reads of the counts before the update)
-      if (m && (m >> lane) == 1ull) cnt[w * kRadixBins + d] += __popcll(m);   // (the group's last lane)
+      if (m && (m >> lane) == 1ull) cnt[w * kBins + d] += (CT)__popcll(m);   // (the group's last lane)
       wave_sync();
     }
     __syncthreads();
@@ -584,7 +585,12 @@ __device__ __forceinline__ int radix_sort_packed(const SArgs& S, int64_t a0, int
   }
   __syncthreads();
   const int rbits = 32 - __clz(max(present - 1, 1));
-  return radix_passes<true>(R, n, rbits + lb, kSortIdxBits, s_red);
+  // up to 16 key bits: 8-bit digits; 17-18 (level 0 at cfg5): two passes of 9-bit digits with
+  // 16-bit counts in the same count area instead of three of 8 (level 0 1.10 -> 0.98 ms; the
+  // ninth ballot made the 16-bit levels slower)
+  return rbits + lb <= 2 * kRadixBits || rbits + lb > 18
+             ? radix_passes<true>(R, n, rbits + lb, kSortIdxBits, s_red)
+             : radix_passes<true, 9, uint16_t>(R, n, rbits + lb, kSortIdxBits, s_red);
 }
 
 __global__ __launch_bounds__(kRadixNT) void k_sort_radix(const SArgs S, int n_act, int level, uint64_t* keys,
