@@ -13,6 +13,10 @@ constexpr int kBlock = 256;             // 4 waves of 64 lanes per contig workgr
 constexpr int kWaves = kBlock / 64;
 constexpr int kLeafMax = 128;           // numpy pairwise-sum leaf size (PW_BLOCKSIZE)
 constexpr int kNpyBuf = 8192;           // numpy reduction buffer (NPY_BUFSIZE)
+// wf_batch.hit_key (include/waafle_hip.h): taxon | scov >= min_scov << 24 | strand '-' << 25 |
+// systems 0-5 << 26 (k_pack_keys packs it when the caller passes none)
+constexpr uint32_t kKeyTaxon = (1u << 24) - 1u, kKeyScov = 1u << 24, kKeyMinus = 1u << 25;
+constexpr int kKeySys = 26;
 constexpr int kLeafSlots = 160;         // >= leaves of one 8192-element buffer
 constexpr int kMaxIter = 100;           // orgscorer.py:580
 constexpr int kLin = 16;                // lineage row: ancestors at depths 0..15 (64 B)

@@ -143,6 +143,7 @@ __global__ __launch_bounds__(NT) void k_att_contig(const SArgs S_arg, int64_t* c
                     (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
       }
     const int ns = K.n_sys;
+    const bool hkey = K.hkey != nullptr && ns <= 6;  // (the key holds systems 0-5)
     const bool lds_ann = PASS == 1 && (int64_t)G * ns <= kAnnSlots;
     if (lds_ann)
       for (int i = tid; i < G * ns; i += NT) { s_best[i] = 0ull; s_hit[i] = -1; }
@@ -186,18 +187,28 @@ __global__ __launch_bounds__(NT) void k_att_contig(const SArgs S_arg, int64_t* c
       int n = 0;
       long long nl = 0;
       int qlo = 0, qhi = 0, hs = 0, clade = 0;
-      double sc = 0.0, scv = 0.0;
+      double sc = 0.0;
       uint32_t m = 0u;
+      bool scov_ok = false;
       if (h < h1) {                                 // every field of the hit in one round of loads
-        scv = K.scov[h];
-        qlo = K.qlo[h]; qhi = K.qhi[h]; hs = P.stranded ? K.hstrand[h] : 0;
-        if (PASS == 1) {
-          clade = K.taxon[h];
-          sc = K.score[h];
-          m = ns > 0 ? K.sysmask[h] : 0u;
+        qlo = K.qlo[h]; qhi = K.qhi[h];
+        if (PASS == 1) sc = K.score[h];
+        if (hkey) {                                 // the packed word: 20 B a hit instead of 33
+          const uint32_t k = K.hkey[h];
+          scov_ok = (k & kKeyScov) != 0u;
+          hs = P.stranded && (k & kKeyMinus) ? 1 : 0;
+          clade = (int)(k & kKeyTaxon);
+          m = k >> kKeySys;
+        } else {
+          scov_ok = K.scov[h] >= P.min_scov;
+          hs = P.stranded ? K.hstrand[h] : 0;
+          if (PASS == 1) {
+            clade = K.taxon[h];
+            m = ns > 0 ? K.sysmask[h] : 0u;
+          }
         }
       }
-      const bool live = h < h1 && scv >= P.min_scov;
+      const bool live = h < h1 && scov_ok;
       if (live) {
         each_locus(qlo, qhi, hs, [&](int g, const LocView& L) {
           ++n;
@@ -280,7 +291,7 @@ __global__ __launch_bounds__(NT) void k_att_contig(const SArgs S_arg, int64_t* c
       const int64_t a0 = S.catt_off[c];
       for (int64_t a = a0 + tid; a < base; a += NT) {
         const int h = S.att_hit[a];
-        const uint32_t m = K.sysmask[h];
+        const uint32_t m = hkey ? K.hkey[h] >> kKeySys : K.sysmask[h];
         const double sc = S.att_sc[a];
         if (m == 0 || !(sc >= P.annot_ref)) continue;
         const int g = S.att_loc[a];
@@ -2315,6 +2326,7 @@ static int staged_run(StagedState* st, const KArgs& k, int n_tax, int max_loci, 
         ST_TRY(st->hkey.ensure(s, (size_t)std::max<int64_t>(NH, 1) * 4));
         ST_TRY(pack_keys(da.k, NH, st->hkey.as<uint32_t>(), st->cus, s));
         da.k.hkey = st->hkey.as<uint32_t>();
+        sa.k.hkey = da.k.hkey;                         // (k_att_contig reads it too)
       }
       const int t_tri0 = t_mark(st, s);                 // (the triage span: its launch alone)
       ST_TRY(launch_triage(da, st->cnt.as<int64_t>(), st->cnt_leaves.as<int64_t>(), st->pend.as<int32_t>(), max_hits,

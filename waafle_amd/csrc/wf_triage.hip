@@ -81,10 +81,8 @@ __device__ __forceinline__ uint32_t tr_lohi(int qlo, int qhi, int llo, int len) 
   return (uint32_t)start | ((uint32_t)stop << 16);
 }
 
-// The packed hit word (wf_batch.hit_key): taxon | scov >= min_scov << 24 | strand '-' << 25 |
-// systems 0-5 << 26.  After the table pass the low 24 bits hold the clade's table slot + 1.
-constexpr uint32_t kKeyTaxon = (1u << 24) - 1u, kKeyScov = 1u << 24, kKeyMinus = 1u << 25;
-constexpr int kKeySys = 26;
+// The packed hit word (wf_batch.hit_key, kKey* in wf_internal.h).  After the table pass the
+// low 24 bits hold the clade's table slot + 1.
 
 // wf_batch.hit_key when the caller passes none (include/waafle_hip.h)
 __global__ void k_pack_keys(const KArgs K, int64_t n_hits, uint32_t* key) {
@@ -439,12 +437,16 @@ __global__ __launch_bounds__(64, kTrWaves) void k_triage(const SArgs S_arg, int6
 // Unordered or overlapping loci, more than 64, --min-overlap 0: left to the wave form
 // (pend kPendTriage).  Launched after k_triage, only when the batch has such contigs.
 __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int64_t* cleaves, int32_t* pend) {
-  __shared__ int s_lo[kTrLoc], s_hi[kTrLoc];
+  __shared__ int s_lo[kTrLoc], s_hi[kTrLoc], s_nl[kTrLoc];
   __shared__ int8_t s_st[kTrLoc];
   const KArgs& K = S.k;
   const DevParams& P = K.p;
   const int lane = threadIdx.x;
   unsigned long long n_staged = 0;
+  auto leaves = [&](int len) {                       // numpy leaves of a locus (the LUT's counts)
+    return (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
+           (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+  };
   for (int c = blockIdx.x; c < K.n_contigs; c += gridDim.x) {
     const int64_t h0 = K.hit_off[c], h1 = K.hit_off[c + 1];
     if (h1 - h0 <= kTrBig) continue;                 // (k_triage handed it on: pend kPendTriage)
@@ -460,7 +462,7 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
     const int cprev = __shfl_up(chi, 1, 64);
     if (!(G > 0 && G <= kTrLoc && P.min_overlap > 0.0 && __ballot(lane < G && lane >= 1 && clo <= cprev) == 0ull))
       continue;
-    if (lane < G) { s_lo[lane] = clo; s_hi[lane] = chi; s_st[lane] = (int8_t)cst; }
+    if (lane < G) { s_lo[lane] = clo; s_hi[lane] = chi; s_st[lane] = (int8_t)cst; s_nl[lane] = leaves(chi - clo + 1); }
     wave_sync();
     long long n_att = 0, nl = 0;
     for (int64_t hb = h0; hb < h1; hb += 64 * kCntR) {   // kCntR batches' loads issued together
@@ -486,8 +488,7 @@ __global__ __launch_bounds__(64) void k_count(const SArgs S, int64_t* ccnt, int6
           const int len = s_hi[g] - lo + 1;
           if (attaches(P, qlo, qhi, hs, lo, len, s_st[g])) {
             ++n_att;
-            nl += (len / kNpyBuf) * (S.lut_off[kNpyBuf + 1] - S.lut_off[kNpyBuf]) +
-                  (S.lut_off[len % kNpyBuf + 1] - S.lut_off[len % kNpyBuf]);
+            nl += s_nl[g];                             // (per locus, staged above: no table loads here)
           }
         }
       }
