@@ -1050,11 +1050,12 @@ __global__ void k_seg_rec(const SArgs S, int64_t n_keys) {
 // per attachment, three workgroups per CU at the cfg5 size (80 VGPRs); else radix_sort_contig.
 constexpr unsigned long long kLbA = 1ull << 62, kLbP = 2ull << 62, kLbVal = (1ull << 62) - 1ull;
 
+// (S_arg first: the per-contig loop re-reads the argument block through kernarg_fresh, as
+// k_big_sparse -- held across the loop its fields spill SGPRs into VGPR lanes)
 template <bool PACKED>
-__global__ __launch_bounds__(kRadixNT, PACKED ? 6 : 1) void k_front_radix(const SArgs S, int n_act, int64_t n_keys,
+__global__ __launch_bounds__(kRadixNT, PACKED ? 6 : 1) void k_front_radix(const SArgs S_arg, int n_act, int64_t n_keys,
                                                                          int n_tax, unsigned long long* fr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const RadixLds R(smem, S.sort_cap, PACKED);
   constexpr int kW = kRadixNT / 64;
   __shared__ int s_red[kW];
   __shared__ int s_glen[64];
@@ -1062,14 +1063,16 @@ __global__ __launch_bounds__(kRadixNT, PACKED ? 6 : 1) void k_front_radix(const 
   __shared__ int s_cr, s_ns, s_sbase;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint64_t below = (1ull << lane) - 1ull;
-  const uint32_t lmask = (1u << S.key_lb) - 1u, tmask = (uint32_t)((1ull << S.key_tb) - 1ull);
-  const KArgs& K = S.k;
   unsigned long long* const lb = fr + 4;
   for (;;) {
     if (tid == 0) s_cr = (int)atomicAdd(&fr[0], 1ull);
     __syncthreads();
     const int cr = s_cr;
     if (cr >= n_act) break;                          // (uniform)
+    const SArgs& S = kernarg_fresh<SArgs>(S_arg);
+    const KArgs& K = S.k;
+    const RadixLds R(smem, S.sort_cap, PACKED);
+    const uint32_t lmask = (1u << S.key_lb) - 1u, tmask = (uint32_t)((1ull << S.key_tb) - 1ull);
     const int c = S.act ? S.act[cr] : cr;
     const int64_t a0 = S.catt_off[c];
     const int n = (int)(S.catt_off[c + 1] - a0);
